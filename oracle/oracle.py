@@ -1,0 +1,203 @@
+"""Python front of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg may import this module, and only as the checker.  The product path in
+``flame_amd/`` never imports it and has no CPU fallback.
+
+It restates the reference optimizers' ``do()`` control flow (which entries are
+popped, in which order, which rate, which None results) in Python and runs the
+per-element arithmetic in ``fedagg_oracle.c`` (built into ``liboracle.so``).
+References (``/root/reference/lib/python/flame/``):
+  * FedAvg.do            optimizer/fedavg.py:49-87, _aggregate_pytorch :89-104
+  * FedOPT.do            optimizer/fedopt.py:58-92, _adapt_pytorch :102-129
+  * FedBuff.do           optimizer/fedbuff.py:59-99, scale_add :101-127, _aggregate :136-157
+Parity of this oracle is pinned by ``tests/test_oracle_golden.py`` against
+vectors produced by the real reference (``tests/golden/make_golden.py``).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3,
+      torch.int64: 4, torch.int32: 5}
+VARIANT = {"fedadam": 0, "fedyogi": 1, "fedadagrad": 2}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i64, f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float
+        L.flame_oracle_reduce.argtypes = [ctypes.c_int, vp, i64, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+        L.flame_oracle_scale_add.argtypes = [ctypes.c_int, vp, vp, i64, i64, vp]
+        L.flame_oracle_fedopt_adapt.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, i64] + [f32] * 6
+        L.flame_oracle_synth_f32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, i64, i64, f32, vp]
+        for f in ("flame_oracle_reduce", "flame_oracle_scale_add", "flame_oracle_fedopt_adapt",
+                  "flame_oracle_synth_f32"):
+            getattr(L, f).restype = None
+        _lib = L
+    return _lib
+
+
+def _cpu(t):
+    return t.detach().to("cpu").contiguous()
+
+
+# --------------------------------------------------------------------------- kernels
+def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
+    """acc (CPU, contiguous) += Σ_i round(v_i * rate_i), sequential in list order (in place)."""
+    assert acc.is_contiguous() and acc.device.type == "cpu"
+    n = len(clients)
+    cl = [_cpu(c).to(acc.dtype) if c.dtype != acc.dtype else _cpu(c) for c in clients]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in cl])
+    r32 = np.asarray([np.float32(r) for r in rates] or [0], dtype=np.float32)
+    r64 = np.asarray([float(r) for r in rates] or [0], dtype=np.float64)
+    lib().flame_oracle_reduce(DT[acc.dtype], acc.data_ptr(), acc.numel(), ptrs,
+                              r32.ctypes.data, r64.ctypes.data, n, int(bool(init_first)))
+
+
+def scale_add_tensor(base: torch.Tensor, agg: torch.Tensor, goal: int, want_delta=False):
+    assert base.is_contiguous() and base.device.type == "cpu"
+    if base.dtype in (torch.int64, torch.int32):
+        # torch: int_tensor / int -> float32; `base += float` on an int tensor raises
+        raise RuntimeError("result type Float can't be cast to the desired output type "
+                           + str(base.dtype).replace("torch.", "").capitalize())
+    a = _cpu(agg)
+    delta = torch.empty_like(base) if want_delta else None
+    lib().flame_oracle_scale_add(DT[base.dtype], base.data_ptr(), a.data_ptr(), base.numel(), int(goal),
+                                 delta.data_ptr() if delta is not None else None)
+    return delta
+
+
+def fedopt_scalars(beta_1, beta_2, eta, tau):
+    f = np.float32
+    return (f(beta_1), f(1 - beta_1), f(beta_2), f(1 - beta_2), f(eta), f(tau))
+
+
+def adapt_tensor(sort, avg, cur, m, v, hyper):
+    """Returns new cur; m and v (CPU fp32 contiguous) are updated in place."""
+    out = torch.empty_like(cur)
+    lib().flame_oracle_fedopt_adapt(VARIANT[sort], _cpu(avg).data_ptr(), _cpu(cur).data_ptr(),
+                                    m.data_ptr(), v.data_ptr(), out.data_ptr(), cur.numel(),
+                                    *[float(x) for x in hyper])
+    return out
+
+
+def synth_f32(seed, stream, start, n, scale) -> np.ndarray:
+    out = np.empty(n, dtype=np.float32)
+    lib().flame_oracle_synth_f32(seed, stream, start, n, float(scale), out.ctypes.data)
+    return out
+
+
+# --------------------------------------------------------------------------- do() restatements
+class OracleFedAvg:
+    """fedavg.py:49-104 control flow over a cache with iterkeys()/pop()/__len__."""
+
+    def __init__(self):
+        self.agg_weights = None
+
+    def do(self, base_weights, cache, *, total=0, version=0, **kwargs):
+        assert base_weights is not None
+        self.agg_weights = base_weights
+        if len(cache) == 0 or total == 0:
+            return None
+        for k in list(cache.iterkeys()):
+            tres = cache.pop(k)
+            rate = tres.count / total
+            for key, v in tres.weights.items():
+                acc = self.agg_weights[key]
+                reduce_tensor(acc, [v], [rate])
+        return self.agg_weights
+
+
+class OracleFedOPT(OracleFedAvg):
+    """fedopt.py:58-129 with the three _delta_v variants."""
+
+    def __init__(self, sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3):
+        super().__init__()
+        self.sort = sort
+        self.hyper = fedopt_scalars(beta_1, beta_2, eta, tau)
+        self.current_weights = None
+        self.m_t = None
+        self.v_t = None
+
+    def do(self, base_weights, cache, *, total=0, version=0, **kwargs):
+        self.agg_weights = super().do(base_weights, cache, total=total, version=version)
+        if self.agg_weights is None:
+            return self.current_weights
+        if self.current_weights is None:
+            self.current_weights = self.agg_weights
+            return self.current_weights
+        avg, cur = self.agg_weights, self.current_weights
+        if self.m_t is None:
+            self.m_t = {k: torch.zeros_like(avg[k], dtype=torch.float32) for k in avg}
+        if self.v_t is None:
+            self.v_t = {k: torch.zeros_like(avg[k], dtype=torch.float32) for k in avg}
+        self.current_weights = OrderedDict(
+            (k, adapt_tensor(self.sort, avg[k], cur[k], self.m_t[k], self.v_t[k], self.hyper))
+            for k in cur.keys())
+        return self.current_weights
+
+
+class OracleFedBuff:
+    """fedbuff.py:59-157."""
+
+    def __init__(self):
+        self.agg_goal_weights = None
+
+    def do(self, agg_goal_weights, cache, *, total=0, version=0, **kwargs):
+        self.agg_goal_weights = agg_goal_weights
+        none_start = agg_goal_weights is None
+        if len(cache) == 0 or total == 0:
+            return None
+        for k in list(cache.iterkeys()):
+            tres = cache.pop(k)
+            rate = 1 / math.sqrt(1 + version - tres.version)
+            if none_start:
+                self.agg_goal_weights = {}
+            for key, v in tres.weights.items():
+                if none_start:
+                    acc = torch.empty_like(_cpu(v))
+                    reduce_tensor(acc, [v], [rate], init_first=True)
+                    self.agg_goal_weights[key] = acc
+                else:
+                    reduce_tensor(self.agg_goal_weights[key], [v], [rate])
+        return self.agg_goal_weights
+
+    def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal):
+        for k in base_weights.keys():
+            scale_add_tensor(base_weights[k], agg_goal_weights[k], agg_goal)
+        return base_weights
+
+
+class ListCache:
+    """Minimal diskcache.Cache stand-in (sorted iterkeys, pop) for oracle tests."""
+
+    def __init__(self):
+        self._d = {}
+
+    def __setitem__(self, k, v):
+        self._d[k] = v
+
+    def __len__(self):
+        return len(self._d)
+
+    def iterkeys(self):
+        return iter(sorted(self._d))
+
+    def pop(self, k, default=None):
+        return self._d.pop(k, default)

@@ -1,0 +1,247 @@
+"""Replay the golden fixtures through any optimizer implementation.
+
+The same drivers run the CPU oracle (tests/test_oracle_golden.py) and the HIP
+path (tests/test_gpu_parity.py), reproducing the caller conventions recorded
+in tests/golden/make_golden.py.  Each driver returns a list of
+``(label, got_dict, expected_dict)`` for the checker.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from copy import deepcopy
+
+import numpy as np
+import torch
+
+from fixture_io import tensor_to_np
+
+
+class TR:
+    """Duck-typed TrainResult(weights, count, version) (optimizer/train_result.py:19-26)."""
+
+    def __init__(self, weights=None, count=0, version=0):
+        self.weights, self.count, self.version = weights, count, version
+
+
+class SortedCache:
+    def __init__(self):
+        self._d = {}
+
+    def __setitem__(self, k, v):
+        self._d[k] = v
+
+    def __len__(self):
+        return len(self._d)
+
+    def iterkeys(self):
+        return iter(sorted(self._d))
+
+    def pop(self, k, default=None):
+        return self._d.pop(k, default)
+
+
+def to_dev(w, device):
+    return {k: v.to(device, copy=True) for k, v in w.items()}
+
+
+def to_cpu(w):
+    return {k: v.detach().cpu().clone() for k, v in w.items()}
+
+
+def assert_bitwise(label, got, exp):
+    assert list(got.keys()) == list(exp.keys()), label
+    for k in exp:
+        g, e = got[k].detach().cpu(), exp[k]
+        assert g.dtype == e.dtype, f"{label}/{k}: dtype {g.dtype} vs {e.dtype}"
+        assert g.shape == e.shape, f"{label}/{k}: shape {g.shape} vs {e.shape}"
+        ga, _ = tensor_to_np(g)
+        ea, _ = tensor_to_np(e)
+        if not np.array_equal(ga.view(np.uint8), ea.view(np.uint8)):
+            bad = np.flatnonzero(ga.reshape(-1) != ea.reshape(-1))
+            raise AssertionError(f"{label}/{k}: {bad.size} elements differ, first at {bad[:5]}: "
+                                 f"{ga.reshape(-1)[bad[:5]]} vs {ea.reshape(-1)[bad[:5]]}")
+
+
+def assert_close_fedopt(label, got, exp, rtol=1e-6):
+    """SURVEY §8(c) FedOPT contract: elementwise rel err <= rtol where |ref| >= rtol*max|ref|,
+    and rel-L2 <= rtol."""
+    for k in exp:
+        g = got[k].detach().cpu().double()
+        e = exp[k].double()
+        den = e.abs()
+        mask = den >= rtol * den.max()
+        rel = ((g - e).abs()[mask] / den[mask]).max().item() if mask.any() else 0.0
+        l2 = ((g - e).norm() / e.norm().clamp_min(1e-300)).item()
+        assert rel <= rtol, f"{label}/{k}: max elementwise rel err {rel:.3e}"
+        assert l2 <= rtol, f"{label}/{k}: rel-L2 {l2:.3e}"
+
+
+# ---------------------------------------------------------------- drivers
+def run_fedavg(fx, make_opt, device):
+    m = fx.meta
+    base = to_dev(fx.weights("base"), device)
+    cache = SortedCache()
+    for i, (e, c) in enumerate(zip(m["end_ids"], m["counts"])):
+        cache[e] = TR(to_dev(fx.weights(f"client{i}"), device), c)
+    assert list(cache.iterkeys()) == m["order"]
+    opt = make_opt("fedavg")
+    out = opt.do(base, cache, total=m["total"], num_trainers=m["n"])
+    assert out is base, "FedAvg must return (and mutate) the base_weights object (fedavg.py:74,87)"
+    assert len(cache) == 0, "cache entries must be consumed (fedavg.py:82)"
+    return [("out", out, fx.weights("out"))]
+
+
+def run_fedavg_synth(fx, make_opt, device):
+    from flame_amd import synth
+    m = fx.meta
+
+    def gen(stream, sigma):
+        shapes = m["shapes"]
+        total = sum(int(np.prod(s)) for _, s in shapes)
+        flat = synth.synth_f32(m["seed"], stream, total, sigma)
+        out, off = {}, 0
+        for k, s in shapes:
+            n = int(np.prod(s))
+            out[k] = torch.from_numpy(flat[off:off + n].copy()).reshape(s).to(device)
+            off += n
+        return out
+
+    base = gen(m["base_stream"], m["sigma_base"])
+    cache = SortedCache()
+    for e, s, c in zip(m["end_ids"], m["client_streams"], m["counts"]):
+        cache[e] = TR(gen(s, m["sigma_delta"]), c)
+    out = make_opt("fedavg").do(base, cache, total=m["total"], num_trainers=2)
+    for k, d in m["digests"]["out"].items():
+        a, _ = tensor_to_np(out[k].cpu())
+        assert list(a.shape) == d["shape"]
+        assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == d["sha256"], \
+            f"mnist2/{k}: digest mismatch"
+    return []
+
+
+def run_fedavg_eager(fx, make_opt, device):
+    m = fx.meta
+    opt = make_opt("fedavg")
+    cache = SortedCache()
+    base = to_dev(fx.weights("base"), device)
+    total = 0
+    res = []
+    for step, (e, c) in enumerate(zip(m["end_ids"], m["counts"])):
+        total += c
+        cache[e] = TR(to_dev(fx.weights(f"client{step}"), device), c)
+        out = opt.do(base, cache, total=total, num_trainers=m["n"])
+        assert out is base
+        res.append((f"after{step}", deepcopy(to_cpu(out)), fx.weights(f"after{step}")))
+    return res
+
+
+def run_none(fx, make_opt, device):
+    opt = make_opt("fedavg")
+    base = {"w": torch.ones(3, device=device)}
+    assert (opt.do(deepcopy(base), SortedCache(), total=5) is None) == fx.meta["empty_is_none"]
+    c = SortedCache()
+    c["x"] = TR({"w": torch.ones(3, device=device)}, 0)
+    assert (opt.do(deepcopy(base), c, total=0) is None) == fx.meta["total0_is_none"]
+    assert len(c) == fx.meta["total0_cache_len_after"]
+    return []
+
+
+def run_fedbuff_seq(fx, make_opt, device):
+    m = fx.meta
+    opt = make_opt("fedbuff")
+    agg = None
+    res = []
+    for i in range(m["goal"]):
+        cache = SortedCache()
+        cache[f"t{i}"] = TR(to_dev(fx.weights(f"update{i}"), device), m["counts"][i],
+                            m["round"] - m["stale"][i])
+        agg = opt.do(agg, cache, total=m["counts"][i], version=m["round"])
+        res.append((f"agg{i}", deepcopy(to_cpu(agg)), fx.weights(f"agg{i}")))
+    weights = to_dev(fx.weights("weights0"), device)
+    new = opt.scale_add_agg_weights(weights, agg, m["goal"])
+    assert new is weights, "scale_add mutates and returns base_weights (fedbuff.py:122-127)"
+    res.append(("out", new, fx.weights("out")))
+    return res
+
+
+def run_fedbuff_none_multi(fx, make_opt, device):
+    m = fx.meta
+    cache = SortedCache()
+    for i, k in enumerate(["k0", "k1", "k2"]):
+        cache[k] = TR(to_dev(fx.weights(f"update{i}"), device), 10, m["versions"][i])
+    out = make_opt("fedbuff").do(None, cache, total=10, version=m["round"])
+    return [("out", out, fx.weights("out"))]
+
+
+def run_fedopt(fx, make_opt, device):
+    m = fx.meta
+    opt = make_opt(m["sort"], beta_1=m["beta_1"], beta_2=m["beta_2"], eta=m["eta"], tau=m["tau"])
+    weights = to_dev(fx.weights("weights0"), device)
+    res = []
+    for r in range(m["rounds"]):
+        cache = SortedCache()
+        for i, c in enumerate(m["counts"][r]):
+            cache[f"r{r}c{i}"] = TR(to_dev(fx.weights(f"r{r}/client{i}"), device), c)
+        # reference caller: do(deepcopy(self.weights), ...) then self.weights = result
+        weights = opt.do(deepcopy(weights), cache, total=sum(m["counts"][r]), num_trainers=m["n"])
+        res.append((f"r{r}/cur", to_cpu(weights), fx.weights(f"r{r}/cur")))
+        res.append((f"r{r}/avg", to_cpu(opt.agg_weights), fx.weights(f"r{r}/avg")))
+        if f"r{r}/m" in fx.meta["keys"]:
+            res.append((f"r{r}/m", to_cpu(opt.m_t), fx.weights(f"r{r}/m")))
+            res.append((f"r{r}/v", to_cpu(opt.v_t), fx.weights(f"r{r}/v")))
+    return res
+
+
+def run_hier(fx, make_opt, device, delta_fn):
+    m = fx.meta
+    rnd = m["round"]
+    top_w0 = fx.weights("top_w0")
+    res = []
+    deltas = []
+    for mid in range(2):
+        opt = make_opt("fedbuff")
+        mid_w = to_dev(top_w0, device)
+        agg = None
+        for t in range(3):
+            cache = SortedCache()
+            cache[f"m{mid}t{t}"] = TR(to_dev(fx.weights(f"m{mid}/update{t}"), device), 10 + t, rnd - t % 2)
+            agg = opt.do(agg, cache, total=10 + t, version=rnd)
+        prev = deepcopy(mid_w)
+        mid_w = opt.scale_add_agg_weights(mid_w, agg, 3)
+        delta = delta_fn(mid_w, prev)
+        res.append((f"m{mid}/delta", to_cpu(delta), fx.weights(f"m{mid}/delta")))
+        deltas.append(delta)
+    opt = make_opt("fedbuff")
+    agg = None
+    for mid, d in enumerate(deltas):
+        cache = SortedCache()
+        cache[f"mid{mid}"] = TR(d, 30, rnd - mid)
+        agg = opt.do(agg, cache, total=30, version=rnd)
+    top = opt.scale_add_agg_weights(to_dev(top_w0, device), agg, 2)
+    res.append(("top_out", to_cpu(top), fx.weights("top_out")))
+    return res
+
+
+BITWISE_FIXTURES = [
+    ("fedavg_small.npz", run_fedavg),
+    ("fedavg_dtypes.npz", run_fedavg),
+    ("fedavg_edge_p1.npz", run_fedavg),
+    ("fedavg_edge_p4099.npz", run_fedavg),
+    ("fedavg_mnist2.npz", run_fedavg_synth),
+    ("fedavg_eager.npz", run_fedavg_eager),
+    ("fedavg_edge_none.npz", run_none),
+    ("fedbuff_seq_fp32.npz", run_fedbuff_seq),
+    ("fedbuff_seq_bf16.npz", run_fedbuff_seq),
+    ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
+]
+FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz"]
+
+
+def delta_torch(a, b):
+    """common/util.py:152-159 restated."""
+    return {x: a[x] - b[y] for (x, y) in zip(a, b)}
+
+
+def rate_fedbuff(version, tres_version):
+    return 1 / math.sqrt(1 + version - tres_version)
