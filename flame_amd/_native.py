@@ -1,0 +1,74 @@
+"""ctypes binding of ``libflame_amd.so`` (the C ABI in ``include/flame_amd.h``).
+
+The library is REQUIRED: importing the compute entry points without it raises
+immediately -- there is no CPU or eager-PyTorch fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FLAME_AMD_LIB", os.path.join(PKG, "libflame_amd.so"))
+
+# constants mirrored from include/flame_amd.h
+FLAME_OK, FLAME_EINVAL, FLAME_EHIP, FLAME_ENOTSUP = 0, 1, 2, 3
+FLAME_F32, FLAME_BF16, FLAME_F16, FLAME_F64, FLAME_I64, FLAME_I32 = range(6)
+FLAME_AGG_INIT_FIRST = 1
+FLAME_FEDADAM, FLAME_FEDYOGI, FLAME_FEDADAGRAD = 0, 1, 2
+FLAME_OPT_STATE_ZERO = 1
+FLAME_SEG_UNALIGNED = 1
+SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
+
+# every symbol include/flame_amd.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
+    "flame_agg_reduce", "flame_fedopt_reduce_adapt", "flame_fedbuff_scale_add", "flame_synth_fill",
+)
+
+
+class FlameError(RuntimeError):
+    """A nonzero FLAME_E* status returned by the native library."""
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the native library (raises ImportError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"flame_amd native library not found at {LIB_PATH}; build it with "
+            "`python -m flame_amd.build` (hipcc --offload-arch=gfx950). There is no fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u32, u64, f32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint,
+                                   ctypes.c_uint64, ctypes.c_float)
+    L.flame_abi_version.restype = ctypes.c_int
+    L.flame_abi_version.argtypes = []
+    L.flame_last_error.restype = ctypes.c_char_p
+    L.flame_last_error.argtypes = []
+    L.flame_chunk_elems.restype = i64
+    L.flame_chunk_elems.argtypes = [ctypes.c_int]
+    L.flame_scale_add_chunk_elems.restype = i64
+    L.flame_scale_add_chunk_elems.argtypes = [ctypes.c_int]
+    L.flame_agg_reduce.restype = ctypes.c_int
+    L.flame_agg_reduce.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp, vp]
+    L.flame_fedopt_reduce_adapt.restype = ctypes.c_int
+    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [f32] * 6 + [vp]
+    L.flame_fedbuff_scale_add.restype = ctypes.c_int
+    L.flame_fedbuff_scale_add.argtypes = [ctypes.c_int, vp, i32, i64, i64, vp]
+    L.flame_synth_fill.restype = ctypes.c_int
+    L.flame_synth_fill.argtypes = [ctypes.c_int, vp, i64, u64, u64, i64, f32, vp]
+    if L.flame_abi_version() != 1:
+        raise ImportError(f"flame_amd ABI mismatch: library {L.flame_abi_version()} != 1")
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != FLAME_OK:
+        msg = lib().flame_last_error().decode(errors="replace")
+        raise FlameError(f"flame_amd status {rc}: {msg}")

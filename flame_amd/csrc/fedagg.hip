@@ -1,0 +1,592 @@
+// fedagg.hip -- CDNA4 (gfx950) kernels + C ABI for flame's server-side aggregation.
+//
+// Hot path: the weighted reduction of N client updates into
+// one global model, restated from /root/reference/lib/python/flame/
+//   optimizer/fedavg.py:79-104, optimizer/fedbuff.py:89-97,122-157,
+//   optimizer/fedopt.py:102-129 (+ fedadam.py:33-35, fedyogi.py:34-36, fedadagrad.py:33-35).
+//
+// Design:
+//   * HBM-read bound (≈1 flop per byte): no MFMA, no LDS; every byte is read once.
+//   * One workgroup (256 lanes) owns one chunk of one segment; each lane owns
+//     16 contiguous bytes of every client's update (dwordx4, non-temporal), so
+//     every wave instruction is a 1 KiB fully-coalesced read.
+//   * The client axis stays SEQUENTIAL in registers: per element the sum is
+//     acc = round(acc + round(v_i * r_i)) in cache.iterkeys() order, exactly the
+//     reference's torch-CPU op order -> bit-identical results.  Reordering the
+//     fp32 client sum (tree / __shfl_down / split-K) breaks the 1e-6 contract
+//     at N=1024, so it is not done.
+//   * CU clients are unrolled per step so each lane has CU x 16 B loads in
+//     flight (memory-level parallelism); client pointers and rates are
+//     wave-uniform and come through the scalar cache.
+//   * Built with -ffp-contract=off and explicit __f*_rn ops: no FMA contraction.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <cstdarg>
+
+#include "../../include/flame_amd.h"
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(FLAME_EHIP, "%s: %s", what, hipGetErrorString(e));
+    g_err[0] = 0;
+    return FLAME_OK;
+}
+
+// ---------------------------------------------------------------- rounding helpers
+__device__ __forceinline__ float bf16_round(float x) {
+    // RNE fp32 -> bf16 -> fp32 (v_cvt_pk_bf16_f32 on gfx950)
+    return static_cast<float>(static_cast<__bf16>(x));
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t b) {
+    return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16_exact(float x) {  // x already bf16-representable
+    return static_cast<uint16_t>(__float_as_uint(x) >> 16);
+}
+__device__ __forceinline__ float f16_round(float x) {
+    return static_cast<float>(static_cast<_Float16>(x));
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+    _Float16 v;
+    __builtin_memcpy(&v, &h, 2);
+    return static_cast<float>(v);
+}
+__device__ __forceinline__ uint16_t f32_to_f16_bits(float x) {
+    _Float16 v = static_cast<_Float16>(x);
+    uint16_t h;
+    __builtin_memcpy(&h, &v, 2);
+    return h;
+}
+
+// ---------------------------------------------------------------- dtype traits
+// T: storage type; A: register accumulator type; EPT: elements per 16-byte lane vector.
+// tmp(v, r) = the reference's `tmp = (v * rate).to(v.dtype)`; add(a, t) = `agg += tmp`.
+template <int DT> struct Tr;
+
+template <> struct Tr<FLAME_F32> {
+    using T = float; using A = float; static constexpr int EPT = 4;
+    __device__ static A ld(T x) { return x; }
+    __device__ static T st(A a) { return a; }
+    __device__ static A tmp(T v, float r, double) { return __fmul_rn(v, r); }
+    __device__ static A add(A a, A t) { return __fadd_rn(a, t); }
+};
+template <> struct Tr<FLAME_BF16> {
+    using T = uint16_t; using A = float; static constexpr int EPT = 8;
+    __device__ static A ld(T x) { return bf16_to_f32(x); }
+    __device__ static T st(A a) { return f32_to_bf16_exact(a); }
+    __device__ static A tmp(T v, float r, double) { return bf16_round(__fmul_rn(bf16_to_f32(v), r)); }
+    __device__ static A add(A a, A t) { return bf16_round(__fadd_rn(a, t)); }
+};
+template <> struct Tr<FLAME_F16> {
+    using T = uint16_t; using A = float; static constexpr int EPT = 8;
+    __device__ static A ld(T x) { return f16_to_f32(x); }
+    __device__ static T st(A a) { return f32_to_f16_bits(a); }
+    __device__ static A tmp(T v, float r, double) { return f16_round(__fmul_rn(f16_to_f32(v), r)); }
+    __device__ static A add(A a, A t) { return f16_round(__fadd_rn(a, t)); }
+};
+template <> struct Tr<FLAME_F64> {
+    using T = double; using A = double; static constexpr int EPT = 2;
+    __device__ static A ld(T x) { return x; }
+    __device__ static T st(A a) { return a; }
+    __device__ static A tmp(T v, float, double r) { return __dmul_rn(v, r); }
+    __device__ static A add(A a, A t) { return __dadd_rn(a, t); }
+};
+// int tensors: torch promotes int * python-float to fp32, then .to(int) truncates (fedavg.py:93-102)
+template <> struct Tr<FLAME_I64> {
+    using T = int64_t; using A = int64_t; static constexpr int EPT = 2;
+    __device__ static A ld(T x) { return x; }
+    __device__ static T st(A a) { return a; }
+    __device__ static A tmp(T v, float r, double) { return static_cast<int64_t>(__fmul_rn(static_cast<float>(v), r)); }
+    __device__ static A add(A a, A t) { return static_cast<int64_t>(static_cast<uint64_t>(a) + static_cast<uint64_t>(t)); }
+};
+template <> struct Tr<FLAME_I32> {
+    using T = int32_t; using A = int32_t; static constexpr int EPT = 4;
+    __device__ static A ld(T x) { return x; }
+    __device__ static T st(A a) { return a; }
+    __device__ static A tmp(T v, float r, double) { return static_cast<int32_t>(__fmul_rn(static_cast<float>(v), r)); }
+    __device__ static A add(A a, A t) { return static_cast<int32_t>(static_cast<uint32_t>(a) + static_cast<uint32_t>(t)); }
+};
+
+template <int DT> constexpr int64_t chunk_elems() { return static_cast<int64_t>(kBlock) * Tr<DT>::EPT; }
+
+// ---------------------------------------------------------------- memory helpers
+// All device data is accessed through address_space(1) (global) pointers so the
+// compiler emits global_load/store (vmcnt only) instead of flat_* (which also
+// count on lgkmcnt and would serialise against the scalar pointer/rate loads).
+struct alignas(16) V16 { uint32_t w[4]; };
+using u4 = __attribute__((ext_vector_type(4))) uint32_t;
+template <typename T> using gptr = __attribute__((address_space(1))) T*;
+template <typename T> using gcptr = const __attribute__((address_space(1))) T*;
+
+template <typename T> __device__ __forceinline__ gcptr<T> G(const T* p) { return (gcptr<T>)(p); }
+template <typename T> __device__ __forceinline__ gptr<T> G(T* p) { return (gptr<T>)(p); }
+
+__device__ __forceinline__ V16 ld_nt(const void* p) {
+    u4 x = __builtin_nontemporal_load(G(reinterpret_cast<const u4*>(p)));
+    V16 r; r.w[0] = x[0]; r.w[1] = x[1]; r.w[2] = x[2]; r.w[3] = x[3];
+    return r;
+}
+__device__ __forceinline__ V16 ld_v(const void* p) {
+    u4 x = *G(reinterpret_cast<const u4*>(p));
+    V16 r; r.w[0] = x[0]; r.w[1] = x[1]; r.w[2] = x[2]; r.w[3] = x[3];
+    return r;
+}
+__device__ __forceinline__ void st_v(void* p, const V16& v) {
+    u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+    *G(reinterpret_cast<u4*>(p)) = x;
+}
+template <typename T> __device__ __forceinline__ T ld1(const T* p) { return *G(p); }
+template <typename T> __device__ __forceinline__ void st1(T* p, T x) { *G(p) = x; }
+template <typename T, int EPT>
+__device__ __forceinline__ void unpack(const V16& v, T (&x)[EPT]) {
+    static_assert(sizeof(T) * EPT == 16, "lane vector is 16 bytes");
+    __builtin_memcpy(x, v.w, 16);
+}
+template <typename T, int EPT>
+__device__ __forceinline__ V16 pack(const T (&x)[EPT]) {
+    V16 v;
+    __builtin_memcpy(v.w, x, 16);
+    return v;
+}
+
+// Wave-uniform segment lookup: largest s with segs[s].chunk_begin <= chunk.
+__device__ __forceinline__ int find_segment(const flame_segment* __restrict__ segs, int n_segs, int64_t chunk) {
+    int lo = 0, hi = n_segs - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].chunk_begin <= chunk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------- reduction core
+// Reduce clients [0, n) into acc[EPT] for the lane's 16-byte slot at element e0.
+// VEC: whole aligned vector; else element-wise with bounds (tails / unaligned views).
+template <int DT, int CU, bool VEC>
+__device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[Tr<DT>::EPT], bool init_first,
+                                               const uint64_t* __restrict__ cp, int n,
+                                               const float* __restrict__ r32, const double* __restrict__ r64,
+                                               int64_t e0, int64_t numel) {
+    using X = Tr<DT>;
+    using T = typename X::T;
+    constexpr int EPT = X::EPT;
+    int i = 0;
+    auto rate32 = [&](int c) -> float { if constexpr (DT == FLAME_F64) return 0.f; else return r32[c]; };
+    auto rate64 = [&](int c) -> double { if constexpr (DT == FLAME_F64) return r64[c]; else return 0.0; };
+    auto load_client = [&](int c, T (&x)[EPT]) {
+        const T* p = reinterpret_cast<const T*>(cp[c]) + e0;
+        if constexpr (VEC) {
+            unpack<T, EPT>(ld_nt(p), x);
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) x[j] = (e0 + j < numel) ? ld1(p + j) : T(0);
+        }
+    };
+    if (init_first && n > 0) {
+        T x[EPT];
+        load_client(0, x);
+        const float r = rate32(0);
+        const double rd = rate64(0);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) acc[j] = X::tmp(x[j], r, rd);
+        i = 1;
+    }
+    for (; i + CU <= n; i += CU) {
+        T x[CU][EPT];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const float r = rate32(i + u);
+            const double rd = rate64(i + u);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[u][j], r, rd));
+        }
+    }
+    for (; i < n; ++i) {
+        T x[EPT];
+        load_client(i, x);
+        const float r = rate32(i);
+        const double rd = rate64(i);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[j], r, rd));
+    }
+}
+
+template <int DT, int CU>
+__global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                            const uint64_t* __restrict__ clients, int n_clients,
+                                                            const float* __restrict__ r32,
+                                                            const double* __restrict__ r64, unsigned flags) {
+    using X = Tr<DT>;
+    using T = typename X::T;
+    using A = typename X::A;
+    constexpr int EPT = X::EPT;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const bool init_first = (flags & FLAME_AGG_INIT_FIRST) != 0;
+    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    A acc[EPT];
+    if (vec) {
+        if (!init_first) {
+            T b[EPT];
+            unpack<T, EPT>(ld_v(reinterpret_cast<const T*>(sg.in) + e0), b);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[j] = X::ld(b[j]);
+        }
+        reduce_clients<DT, CU, true>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
+        T o[EPT];
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) o[j] = X::st(acc[j]);
+        st_v(reinterpret_cast<T*>(sg.out) + e0, pack<T, EPT>(o));
+    } else {
+        const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
+        if (!init_first) {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[j] = X::ld((e0 + j < sg.numel) ? ld1(bp + j) : T(0));
+        }
+        reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
+        T* op = reinterpret_cast<T*>(sg.out) + e0;
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+            if (e0 + j < sg.numel) st1(op + j, X::st(acc[j]));
+    }
+}
+
+// ---------------------------------------------------------------- fused FedOPT (fp32)
+__device__ __forceinline__ float sign_f(float x) {  // torch.sign: NaN -> 0, -0 -> 0
+    return static_cast<float>((0.0f < x) - (x < 0.0f));
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float& v, float& cur_out,
+                                           float b1, float omb1, float b2, float omb2, float eta, float tau) {
+    const float d = __fsub_rn(avg, cur);
+    const float mn = __fadd_rn(__fmul_rn(b1, m), __fmul_rn(omb1, d));
+    const float d2 = __fmul_rn(d, d);
+    float vn;
+    if constexpr (VARIANT == FLAME_FEDADAM) {
+        vn = __fadd_rn(__fmul_rn(b2, v), __fmul_rn(omb2, d2));
+    } else if constexpr (VARIANT == FLAME_FEDYOGI) {
+        vn = __fsub_rn(v, __fmul_rn(__fmul_rn(omb2, d2), sign_f(__fsub_rn(v, d2))));
+    } else {
+        vn = __fadd_rn(v, d2);
+    }
+    const float q = __fdiv_rn(__fmul_rn(eta, mn), __fadd_rn(__fsqrt_rn(vn), tau));
+    m = mn;
+    v = vn;
+    cur_out = __fadd_rn(cur, q);
+}
+
+template <int VARIANT, int CU>
+__global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                        const uint64_t* __restrict__ clients, int n_clients,
+                                                        const float* __restrict__ r32, unsigned flags, float b1,
+                                                        float omb1, float b2, float omb2, float eta, float tau) {
+    constexpr int DT = FLAME_F32;
+    constexpr int EPT = 4;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
+    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    float acc[EPT], cur[EPT], m[EPT], v[EPT], co[EPT];
+    const float* base = reinterpret_cast<const float*>(sg.in) + e0;
+    const float* curp = reinterpret_cast<const float*>(sg.cur) + e0;
+    float* mp = reinterpret_cast<float*>(sg.m) + e0;
+    float* vp = reinterpret_cast<float*>(sg.v) + e0;
+    if (vec) {
+        unpack<float, EPT>(ld_v(base), acc);
+        reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
+        unpack<float, EPT>(ld_v(curp), cur);
+        if (zero_state) {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) { m[j] = 0.f; v[j] = 0.f; }
+        } else {
+            unpack<float, EPT>(ld_v(mp), m);
+            unpack<float, EPT>(ld_v(vp), v);
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) adapt_elem<VARIANT>(acc[j], cur[j], m[j], v[j], co[j], b1, omb1, b2, omb2, eta, tau);
+        if (sg.out) st_v(reinterpret_cast<float*>(sg.out) + e0, pack<float, EPT>(acc));
+        st_v(mp, pack<float, EPT>(m));
+        st_v(vp, pack<float, EPT>(v));
+        st_v(reinterpret_cast<float*>(sg.cur_out) + e0, pack<float, EPT>(co));
+    } else {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) acc[j] = (e0 + j < sg.numel) ? ld1(base + j) : 0.f;
+        reduce_clients<DT, 1, false>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            if (e0 + j >= sg.numel) continue;
+            float mj = zero_state ? 0.f : ld1(mp + j), vj = zero_state ? 0.f : ld1(vp + j), cj;
+            adapt_elem<VARIANT>(acc[j], ld1(curp + j), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
+            if (sg.out) st1(reinterpret_cast<float*>(sg.out) + e0 + j, acc[j]);
+            st1(mp + j, mj);
+            st1(vp + j, vj);
+            st1(reinterpret_cast<float*>(sg.cur_out) + e0 + j, cj);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- FedBuff scale-add (+delta)
+template <int DT> struct SA;
+template <> struct SA<FLAME_F32> {
+    using T = float; static constexpr int EPT = 4;
+    __device__ static void op(T& b, T a, float g, double, T* d) {
+        const float nb = __fadd_rn(b, __fdiv_rn(a, g));
+        if (d) *d = __fsub_rn(nb, b);
+        b = nb;
+    }
+};
+template <> struct SA<FLAME_F64> {
+    using T = double; static constexpr int EPT = 2;
+    __device__ static void op(T& b, T a, float, double g, T* d) {
+        const double nb = __dadd_rn(b, __ddiv_rn(a, g));
+        if (d) *d = __dsub_rn(nb, b);
+        b = nb;
+    }
+};
+template <> struct SA<FLAME_BF16> {
+    using T = uint16_t; static constexpr int EPT = 8;
+    __device__ static void op(T& b, T a, float g, double, T* d) {
+        const float bo = bf16_to_f32(b);
+        const float q = bf16_round(__fdiv_rn(bf16_to_f32(a), g));
+        const float nb = bf16_round(__fadd_rn(bo, q));
+        if (d) *d = f32_to_bf16_exact(bf16_round(__fsub_rn(nb, bo)));
+        b = f32_to_bf16_exact(nb);
+    }
+};
+template <> struct SA<FLAME_F16> {
+    using T = uint16_t; static constexpr int EPT = 8;
+    __device__ static void op(T& b, T a, float g, double, T* d) {
+        const float bo = f16_to_f32(b);
+        const float q = f16_round(__fdiv_rn(f16_to_f32(a), g));
+        const float nb = f16_round(__fadd_rn(bo, q));
+        if (d) *d = f32_to_f16_bits(__fsub_rn(nb, bo));
+        b = f32_to_f16_bits(nb);
+    }
+};
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void scale_add_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                           float gf, double gd) {
+    using S = SA<DT>;
+    using T = typename S::T;
+    constexpr int EPT = S::EPT;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * (kBlock * EPT) + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    T* bp = reinterpret_cast<T*>(sg.out) + e0;
+    const T* ap = reinterpret_cast<const T*>(sg.in) + e0;
+    T* dp = sg.cur_out ? reinterpret_cast<T*>(sg.cur_out) + e0 : nullptr;
+    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    if (vec) {
+        T b[EPT], a[EPT], d[EPT];
+        unpack<T, EPT>(ld_v(bp), b);
+        unpack<T, EPT>(ld_v(ap), a);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) S::op(b[j], a[j], gf, gd, dp ? &d[j] : nullptr);
+        st_v(bp, pack<T, EPT>(b));
+        if (dp) st_v(dp, pack<T, EPT>(d));
+    } else {
+        for (int j = 0; j < EPT; ++j) {
+            if (e0 + j >= sg.numel) break;
+            T b = ld1(bp + j), d;
+            S::op(b, ld1(ap + j), gf, gd, dp ? &d : nullptr);
+            st1(bp + j, b);
+            if (dp) st1(dp + j, d);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- synthetic generator
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void synth_kernel(void* out, int64_t numel, uint64_t ck, int64_t start, float scale) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < numel; j += stride) {
+        const uint64_t h = mix64(ck + static_cast<uint64_t>(start + j) * 0x9E3779B97F4A7C15ull);
+        const int32_t s = static_cast<int32_t>((h & 0xFFFFu) + ((h >> 16) & 0xFFFFu) + ((h >> 32) & 0xFFFFu) + (h >> 48)) - 131070;
+        const float x = __fmul_rn(static_cast<float>(s), scale);
+        if constexpr (DT == FLAME_F32) st1(reinterpret_cast<float*>(out) + j, x);
+        else if constexpr (DT == FLAME_BF16) st1(reinterpret_cast<uint16_t*>(out) + j, f32_to_bf16_exact(bf16_round(x)));
+        else st1(reinterpret_cast<uint16_t*>(out) + j, f32_to_f16_bits(x));
+    }
+}
+
+constexpr int kClientUnroll = 8;
+
+int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
+    if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
+    if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
+    if (n_clients < 0) return set_err(FLAME_EINVAL, "n_clients < 0");
+    if (n_clients > 0 && !clients) return set_err(FLAME_EINVAL, "client pointer table is NULL");
+    return FLAME_OK;
+}
+
+}  // namespace
+
+// ==================================================================== C ABI
+extern "C" {
+
+int flame_abi_version(void) { return FLAME_ABI_VERSION; }
+
+const char* flame_last_error(void) { return g_err; }
+
+int64_t flame_chunk_elems(int dtype) {
+    switch (dtype) {
+    case FLAME_F32: return chunk_elems<FLAME_F32>();
+    case FLAME_BF16: return chunk_elems<FLAME_BF16>();
+    case FLAME_F16: return chunk_elems<FLAME_F16>();
+    case FLAME_F64: return chunk_elems<FLAME_F64>();
+    case FLAME_I64: return chunk_elems<FLAME_I64>();
+    case FLAME_I32: return chunk_elems<FLAME_I32>();
+    default: return 0;
+    }
+}
+
+int64_t flame_scale_add_chunk_elems(int dtype) {
+    switch (dtype) {
+    case FLAME_F32: return kBlock * SA<FLAME_F32>::EPT;
+    case FLAME_F64: return kBlock * SA<FLAME_F64>::EPT;
+    case FLAME_BF16: return kBlock * SA<FLAME_BF16>::EPT;
+    case FLAME_F16: return kBlock * SA<FLAME_F16>::EPT;
+    default: return 0;
+    }
+}
+
+int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32_t n_segs, int64_t n_chunks,
+                     const void* const* clients, int32_t n_clients, const float* rates32, const double* rates64,
+                     void* stream) {
+    int rc = validate(segs, n_segs, n_chunks, n_clients, clients);
+    if (rc) return rc;
+    if ((flags & FLAME_AGG_INIT_FIRST) && n_clients < 1)
+        return set_err(FLAME_EINVAL, "FLAME_AGG_INIT_FIRST needs at least one client");
+    if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
+        return set_err(FLAME_EINVAL, "rate array is NULL");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    auto cl = reinterpret_cast<const uint64_t*>(clients);
+    switch (dtype) {
+    case FLAME_F32:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    case FLAME_BF16:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    case FLAME_F16:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    case FLAME_F64:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    case FLAME_I64:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    case FLAME_I32:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_agg_reduce: unsupported dtype %d", dtype);
+    }
+    return check_launch("flame_agg_reduce");
+}
+
+int flame_fedopt_reduce_adapt(int variant, unsigned flags, const flame_segment* segs, int32_t n_segs,
+                              int64_t n_chunks, const void* const* clients, int32_t n_clients,
+                              const float* rates32, float b1, float omb1, float b2, float omb2, float eta,
+                              float tau, void* stream) {
+    int rc = validate(segs, n_segs, n_chunks, n_clients, clients);
+    if (rc) return rc;
+    if (n_clients > 0 && !rates32) return set_err(FLAME_EINVAL, "rate array is NULL");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    auto cl = reinterpret_cast<const uint64_t*>(clients);
+    switch (variant) {
+    case FLAME_FEDADAM:
+        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDADAM, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
+        break;
+    case FLAME_FEDYOGI:
+        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDYOGI, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
+        break;
+    case FLAME_FEDADAGRAD:
+        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDADAGRAD, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
+        break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: unknown variant %d", variant);
+    }
+    return check_launch("flame_fedopt_reduce_adapt");
+}
+
+int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int64_t goal,
+                            void* stream) {
+    int rc = validate(segs, n_segs, n_chunks, 0, nullptr);
+    if (rc) return rc;
+    if (goal == 0) return set_err(FLAME_EINVAL, "agg_goal must be nonzero");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const float gf = static_cast<float>(goal);
+    const double gd = static_cast<double>(goal);
+    switch (dtype) {
+    case FLAME_F32: hipLaunchKernelGGL((scale_add_kernel<FLAME_F32>), grid, block, 0, st, segs, n_segs, gf, gd); break;
+    case FLAME_F64: hipLaunchKernelGGL((scale_add_kernel<FLAME_F64>), grid, block, 0, st, segs, n_segs, gf, gd); break;
+    case FLAME_BF16: hipLaunchKernelGGL((scale_add_kernel<FLAME_BF16>), grid, block, 0, st, segs, n_segs, gf, gd); break;
+    case FLAME_F16: hipLaunchKernelGGL((scale_add_kernel<FLAME_F16>), grid, block, 0, st, segs, n_segs, gf, gd); break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_fedbuff_scale_add: dtype %d not supported (integer tensors raise in the reference)", dtype);
+    }
+    return check_launch("flame_fedbuff_scale_add");
+}
+
+int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_t stream_id, int64_t start,
+                     float scale, void* stream) {
+    if (numel < 0 || (numel > 0 && !out)) return set_err(FLAME_EINVAL, "flame_synth_fill: bad buffer");
+    if (numel == 0) return FLAME_OK;
+    const uint64_t ck = mix64((seed * 0x9E3779B97F4A7C15ull) ^ ((stream_id + 1ull) * 0xD1B54A32D192ED03ull));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int64_t blocks = (numel + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    const dim3 grid(static_cast<unsigned>(blocks)), block(kBlock);
+    switch (dtype) {
+    case FLAME_F32: hipLaunchKernelGGL(synth_kernel<FLAME_F32>, grid, block, 0, st, out, numel, ck, start, scale); break;
+    case FLAME_BF16: hipLaunchKernelGGL(synth_kernel<FLAME_BF16>, grid, block, 0, st, out, numel, ck, start, scale); break;
+    case FLAME_F16: hipLaunchKernelGGL(synth_kernel<FLAME_F16>, grid, block, 0, st, out, numel, ck, start, scale); break;
+    default: return set_err(FLAME_ENOTSUP, "flame_synth_fill: dtype %d not supported", dtype);
+    }
+    return check_launch("flame_synth_fill");
+}
+
+}  // extern "C"

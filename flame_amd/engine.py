@@ -1,0 +1,384 @@
+"""Host side of the drop-in path: turns state_dict tensors into segment tables
+and launches the native kernels (``include/flame_amd.h``) on torch's current stream.
+
+Pure-Python planning (``plan_*``, ``rate32``, ``chunk_elems``) needs no GPU and
+is unit-tested on CPU; ``launch_*`` need the native library and a HIP device.
+
+A *segment* is one contiguous tensor (one state_dict entry).  For a reduction,
+row ``s`` of the client table holds, in cache.iterkeys() order, the device
+address of every client's tensor for segment ``s``.  One launch covers all
+segments of one dtype, so a whole model aggregates in one kernel per dtype.
+"""
+from __future__ import annotations
+
+import collections
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+DTYPE_CODE = {
+    torch.float32: N.FLAME_F32, torch.bfloat16: N.FLAME_BF16, torch.float16: N.FLAME_F16,
+    torch.float64: N.FLAME_F64, torch.int64: N.FLAME_I64, torch.int32: N.FLAME_I32,
+}
+FLOAT_CODES = (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16, N.FLAME_F64)
+BLOCK = 256
+VEC_BYTES = 16
+ITEMSIZE = {N.FLAME_F32: 4, N.FLAME_BF16: 2, N.FLAME_F16: 2, N.FLAME_F64: 8, N.FLAME_I64: 8, N.FLAME_I32: 4}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return DTYPE_CODE[dt]
+    except KeyError:
+        raise TypeError(f"flame_amd: tensor dtype {dt} is not supported by the aggregation kernels "
+                        f"(supported: {sorted(str(d) for d in DTYPE_CODE)})") from None
+
+
+def chunk_elems(code: int) -> int:
+    """Elements per workgroup chunk (== flame_chunk_elems / flame_scale_add_chunk_elems)."""
+    return BLOCK * VEC_BYTES // ITEMSIZE[code]
+
+
+def rate32(rate: float) -> float:
+    """torch wraps a Python float scalar and rounds it to the fp32 opmath type (RNE)."""
+    return float(np.float32(rate))
+
+
+# ------------------------------------------------------------------ planning (host only)
+@dataclass
+class Seg:
+    numel: int
+    out: int = 0
+    inp: int = 0
+    cur: int = 0
+    cur_out: int = 0
+    m: int = 0
+    v: int = 0
+    clients: List[int] = field(default_factory=list)
+
+    def pointers(self):
+        return [self.out, self.inp, self.cur, self.cur_out, self.m, self.v] + list(self.clients)
+
+
+@dataclass
+class Plan:
+    code: int
+    meta: np.ndarray      # int64 words: [segments (10 each)] [client table] [rates32 | rates64]
+    n_segs: int
+    n_chunks: int
+    n_clients: int
+    off_clients: int      # byte offsets into the device copy of ``meta``
+    off_r32: int
+    off_r64: int
+
+
+def plan(code: int, segs: Sequence[Seg], rates: Sequence[float], chunk: Optional[int] = None) -> Plan:
+    """Build the device metadata block for one launch (no GPU needed)."""
+    n_segs = len(segs)
+    if n_segs == 0:
+        raise ValueError("empty segment list")
+    n = len(rates)
+    chunk = chunk or chunk_elems(code)
+    words = []
+    begin = 0
+    for s in segs:
+        if len(s.clients) != n:
+            raise ValueError("every segment needs one pointer per client")
+        unaligned = any(p % VEC_BYTES for p in s.pointers() if p)
+        words += [s.out, s.inp, s.cur, s.cur_out, s.m, s.v, s.numel, begin,
+                  N.FLAME_SEG_UNALIGNED if unaligned else 0, 0]
+        begin += -(-s.numel // chunk) if s.numel > 0 else 0
+    if begin == 0:
+        begin = 1  # all segments empty: one (idle) chunk keeps the launch valid
+    off_clients = len(words) * 8
+    for s in segs:
+        words += list(s.clients)
+    off_r32 = len(words) * 8
+    r32 = np.asarray([np.float32(r) for r in rates] + ([np.float32(0)] if n % 2 else []), dtype=np.float32)
+    words_arr = np.asarray([w if w < (1 << 63) else w - (1 << 64) for w in words], dtype=np.int64)
+    r32w = r32.view(np.int64) if r32.size else np.zeros(0, np.int64)
+    off_r64 = off_r32 + r32w.size * 8
+    r64w = np.asarray([float(r) for r in rates], dtype=np.float64).view(np.int64)
+    meta = np.concatenate([words_arr, r32w, r64w]) if n else words_arr
+    return Plan(code, meta, n_segs, begin, n, off_clients, off_r32, off_r64)
+
+
+# ------------------------------------------------------------------ device staging
+class _Staging:
+    """Pinned host -> device upload of plan metadata, ordered on the current stream."""
+
+    def __init__(self):
+        self._inflight = collections.deque()
+
+    def upload(self, meta: np.ndarray, device: torch.device) -> torch.Tensor:
+        while self._inflight and self._inflight[0][0].query():
+            self._inflight.popleft()
+        host = torch.from_numpy(meta)
+        try:
+            host = host.pin_memory()
+        except RuntimeError:
+            pass
+        dev = host.to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._inflight.append((ev, host))
+        return dev
+
+
+_staging = _Staging()
+
+# Optional kernel timing hook (bench.py): when set to a list, every native
+# launch appends (name, start_event, end_event, algorithmic_bytes).  Events are
+# recorded on the stream the kernel is launched on (torch's current stream).
+kernel_events = None
+
+
+class _timed:
+    def __init__(self, name, device, nbytes):
+        self.name, self.device, self.nbytes = name, device, nbytes
+
+    def __enter__(self):
+        if kernel_events is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record(torch.cuda.current_stream(self.device))
+        return self
+
+    def __exit__(self, *exc):
+        if kernel_events is not None and exc[0] is None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(torch.cuda.current_stream(self.device))
+            kernel_events.append((self.name, self.e0, e1, self.nbytes))
+        return False
+
+
+def _stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _keepalive(tensors, device):
+    st = torch.cuda.current_stream(device)
+    for t in tensors:
+        if t.is_cuda:
+            t.record_stream(st)
+
+
+def _device_ptrs(dev_meta: torch.Tensor, p: Plan):
+    base = dev_meta.data_ptr()
+    return base, base + p.off_clients, base + p.off_r32, base + p.off_r64
+
+
+# ------------------------------------------------------------------ launches
+def _as_device(t: torch.Tensor, device) -> torch.Tensor:
+    if t.device != device:
+        t = t.to(device, non_blocking=True)
+    return t.contiguous()
+
+
+def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients: List[List[torch.Tensor]],
+            rates: Sequence[float], *, init_first: bool = False) -> None:
+    """outs[s] = ins[s] (+)= Σ_i round(clients[s][i] * rates[i]) in order (kernel: flame_agg_reduce).
+
+    ``outs`` are written in place (they must be contiguous device tensors);
+    ``ins`` may be the same tensors (FedAvg mutates base_weights in place).
+    """
+    if not outs:
+        return
+    device = outs[0].device
+    if device.type != "cuda":
+        raise RuntimeError("flame_amd.reduce_: output tensors must live on the GPU (no CPU fallback)")
+    groups = collections.OrderedDict()
+    for s, o in enumerate(outs):
+        groups.setdefault(dtype_code(o.dtype), []).append(s)
+    L = N.lib()
+    keep = []
+    for code, idx in groups.items():
+        segs = []
+        for s in idx:
+            o = outs[s]
+            assert o.is_contiguous() and o.device == device
+            row = []
+            for c in clients[s]:
+                if c.dtype != o.dtype:
+                    raise NotImplementedError(
+                        f"flame_amd: client tensor dtype {c.dtype} differs from aggregate dtype {o.dtype}")
+                if c.numel() != o.numel():
+                    raise RuntimeError(f"flame_amd: client tensor has {c.numel()} elements, aggregate {o.numel()}")
+                c = _as_device(c, device)
+                keep.append(c)
+                row.append(c.data_ptr())
+            inp = 0
+            if not init_first:
+                i_t = ins[s]
+                assert i_t.is_contiguous() and i_t.device == device and i_t.numel() == o.numel()
+                inp = i_t.data_ptr()
+            segs.append(Seg(o.numel(), out=o.data_ptr(), inp=inp, clients=row))
+        p = plan(code, segs, rates)
+        dm = _staging.upload(p.meta, device)
+        segp, clp, r32p, r64p = _device_ptrs(dm, p)
+        isz = ITEMSIZE[code]
+        nbytes = sum(s.numel for s in segs) * isz * (p.n_clients + (1 if init_first else 2))
+        with _timed("flame_agg_reduce", device, nbytes):
+            N.check(L.flame_agg_reduce(code, N.FLAME_AGG_INIT_FIRST if init_first else 0, segp, p.n_segs,
+                                       p.n_chunks, clp, p.n_clients, r32p, r64p, _stream_ptr(device)))
+        keep.append(dm)
+    _keepalive(keep, device)
+
+
+FEDOPT_VARIANT = {"fedadam": N.FLAME_FEDADAM, "fedyogi": N.FLAME_FEDYOGI, "fedadagrad": N.FLAME_FEDADAGRAD}
+
+
+def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], base: List[torch.Tensor],
+                         cur: List[torch.Tensor], cur_out: List[torch.Tensor], m: List[torch.Tensor],
+                         v: List[torch.Tensor], clients: List[List[torch.Tensor]], rates: Sequence[float],
+                         hyper, state_zero: bool) -> None:
+    """Fused FedAvg + FedOPT step over fp32 segments (kernel: flame_fedopt_reduce_adapt)."""
+    if not base:
+        return
+    device = base[0].device
+    L = N.lib()
+    segs, keep = [], []
+    for s in range(len(base)):
+        for t in (base[s], cur[s], cur_out[s], m[s], v[s]):
+            assert t.dtype == torch.float32 and t.is_contiguous() and t.device == device
+        row = []
+        for c in clients[s]:
+            if c.dtype != torch.float32 or c.numel() != base[s].numel():
+                raise RuntimeError("flame_amd: FedOPT fused path needs fp32 clients matching the model")
+            c = _as_device(c, device)
+            keep.append(c)
+            row.append(c.data_ptr())
+        segs.append(Seg(base[s].numel(), out=avg_out[s].data_ptr() if avg_out[s] is not None else 0,
+                        inp=base[s].data_ptr(), cur=cur[s].data_ptr(), cur_out=cur_out[s].data_ptr(),
+                        m=m[s].data_ptr(), v=v[s].data_ptr(), clients=row))
+    p = plan(N.FLAME_F32, segs, rates)
+    dm = _staging.upload(p.meta, device)
+    segp, clp, r32p, _ = _device_ptrs(dm, p)
+    P = sum(s.numel for s in segs)
+    # clients + base + cur (+ m, v unless zero state) read; avg, m, v, cur_out written
+    nbytes = 4 * P * (p.n_clients + 2 + (0 if state_zero else 2) + 4)
+    with _timed("flame_fedopt_reduce_adapt", device, nbytes):
+        N.check(L.flame_fedopt_reduce_adapt(FEDOPT_VARIANT[variant], N.FLAME_OPT_STATE_ZERO if state_zero else 0,
+                                            segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
+                                            *[float(x) for x in hyper], _stream_ptr(device)))
+    keep.append(dm)
+    _keepalive(keep, device)
+
+
+def fedopt_scalars(beta_1, beta_2, eta, tau):
+    """fp32 scalars torch uses for `beta_1 * m`, `(1 - beta_1) * d`, ... (fedopt.py:113-129)."""
+    f = np.float32
+    return (f(beta_1), f(1 - beta_1), f(beta_2), f(1 - beta_2), f(eta), f(tau))
+
+
+def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
+               deltas: Optional[List[torch.Tensor]] = None) -> None:
+    """bases[s] += aggs[s] / goal in place; optional deltas[s] = new - old (flame_fedbuff_scale_add)."""
+    if not bases:
+        return
+    device = bases[0].device
+    L = N.lib()
+    groups = collections.OrderedDict()
+    for s, b in enumerate(bases):
+        code = dtype_code(b.dtype)
+        if code not in FLOAT_CODES:
+            # torch: int_tensor / int -> float; in-place add into an int tensor raises
+            raise RuntimeError(f"result type Float can't be cast to the desired output type "
+                               f"{str(b.dtype).replace('torch.', '').capitalize()}")
+        groups.setdefault(code, []).append(s)
+    keep = []
+    for code, idx in groups.items():
+        segs = []
+        for s in idx:
+            b = bases[s]
+            a = _as_device(aggs[s], device)
+            if a.dtype != b.dtype or a.numel() != b.numel():
+                raise NotImplementedError("flame_amd: scale_add needs matching dtype/numel")
+            keep.append(a)
+            d = deltas[s].data_ptr() if deltas is not None else 0
+            segs.append(Seg(b.numel(), out=b.data_ptr(), inp=a.data_ptr(), cur_out=d))
+        p = plan(code, segs, [], chunk=chunk_elems(code))
+        dm = _staging.upload(p.meta, device)
+        nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (3 + (1 if deltas is not None else 0))
+        with _timed("flame_fedbuff_scale_add", device, nbytes):
+            N.check(L.flame_fedbuff_scale_add(code, dm.data_ptr(), p.n_segs, p.n_chunks, int(goal),
+                                              _stream_ptr(device)))
+        keep.append(dm)
+    _keepalive(keep, device)
+
+
+def synth_fill_(out: torch.Tensor, seed: int, stream_id: int, start: int, sigma: float) -> None:
+    """Fill a device tensor with flame_amd.synth values (bench / test inputs)."""
+    from .synth import scale_for_sigma
+    assert out.is_cuda and out.is_contiguous()
+    N.check(N.lib().flame_synth_fill(dtype_code(out.dtype), out.data_ptr(), out.numel(), seed, stream_id,
+                                     start, float(scale_for_sigma(sigma)), _stream_ptr(out.device)))
+
+
+# ------------------------------------------------------------------ dict-level helpers used by the optimizers
+def pick_device(*dicts) -> torch.device:
+    for d in dicts:
+        if d:
+            for t in d.values():
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    return t.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("flame_amd: no HIP device available; the MI355X aggregation path has no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _Target:
+    """A tensor to be updated in place on the device; stages CPU / strided tensors."""
+
+    def __init__(self, t: torch.Tensor, device):
+        self.orig = t
+        self.dev = t if (t.device == device and t.is_contiguous()) else t.to(device).contiguous()
+
+    def writeback(self):
+        if self.dev is not self.orig:
+            self.orig.copy_(self.dev)
+
+
+def accumulate(agg: dict, entries, *, device=None) -> None:
+    """agg[k] += round(v_i[k] * rate_i) for entries (weights, rate) in order, in place.
+
+    Restates the per-client / per-key loop of fedavg.py:79-104 and fedbuff.py:89-97,
+    136-157 (agg not None) as one launch per dtype over all keys and clients.
+    """
+    if not entries:
+        return
+    device = device or pick_device(agg, *[w for w, _ in entries])
+    keys = list(agg.keys())
+    per_key = collections.OrderedDict()
+    for ci, (w, _) in enumerate(entries):
+        for k in w.keys():
+            if k not in agg:
+                raise KeyError(k)
+            per_key.setdefault(k, []).append(ci)
+    # group keys by participating-client set (normally every key has every client)
+    groups = collections.OrderedDict()
+    for k in keys:
+        if k in per_key:
+            groups.setdefault(tuple(per_key[k]), []).append(k)
+    for cis, ks in groups.items():
+        targets = [_Target(agg[k], device) for k in ks]
+        outs = [t.dev for t in targets]
+        clients = [[entries[ci][0][k] for ci in cis] for k in ks]
+        reduce_(outs, outs, clients, [entries[ci][1] for ci in cis])
+        for t in targets:
+            t.writeback()
+
+
+def first_tmp(weights: dict, rate: float, *, device=None) -> dict:
+    """{k: round(v[k] * rate)} as new device tensors (fedbuff.py:139-140,154-155)."""
+    device = device or pick_device(weights)
+    out = collections.OrderedDict()
+    ks = list(weights.keys())
+    for k in ks:
+        v = weights[k]
+        out[k] = torch.empty(v.shape, dtype=v.dtype, device=device)
+    reduce_([out[k] for k in ks], None, [[weights[k]] for k in ks], [rate], init_first=True)
+    return out

@@ -1,0 +1,12 @@
+"""MI355X-native drop-ins for flame's server optimizers (lib/python/flame/optimizer/)."""
+from .abstract import AbstractOptimizer
+from .fedadagrad import FedAdaGrad
+from .fedadam import FedAdam
+from .fedavg import FedAvg
+from .fedbuff import FedBuff
+from .fedopt import FedOPT
+from .fedyogi import FedYogi
+from .train_result import TrainResult
+
+__all__ = ["AbstractOptimizer", "FedAvg", "FedOPT", "FedAdam", "FedYogi", "FedAdaGrad", "FedBuff",
+           "TrainResult"]

@@ -1,0 +1,144 @@
+"""FedOPT family on MI355X -- drop-in for lib/python/flame/optimizer/fedopt.py:33-129.
+
+Control flow is the reference's (fedopt.py:58-92): FedAvg first; ``None`` ->
+return ``current_weights``; round 1 -> ``current_weights = agg_weights`` (no
+adaptive step); afterwards the adaptive step of ``_adapt_pytorch``
+(:102-129) with the subclass's ``_delta_v``.
+
+From the second adaptive-capable round on, fp32 keys go through ONE fused
+kernel (``flame_fedopt_reduce_adapt``): the client reduction, ``d``, ``m_t``,
+``v_t`` and the new ``current`` are computed in registers, reading
+base/cur/m/v once and writing avg/m/v/cur once, instead of ~12 unfused
+torch passes.  Non-fp32 keys (e.g. BatchNorm's int64 ``num_batches_tracked``,
+whose dtype the reference silently promotes to fp32 here) are reduced by the
+same FedAvg kernel and then follow the reference op sequence with torch ops
+on the device.
+
+Ownership: ``base_weights`` is mutated in place into the
+FedAvg result (``self.agg_weights``); ``m_t``/``v_t`` persist across rounds on
+the device; each round returns a NEW OrderedDict of new tensors, like the
+reference.  ``d_t`` is not materialised by the fused path; it is computed
+lazily from ``agg_weights`` and the previous ``current_weights`` on access.
+"""
+import logging
+from abc import abstractmethod
+from collections import OrderedDict
+
+import torch
+
+from .. import engine
+from .fedavg import FedAvg
+
+logger = logging.getLogger(__name__)
+
+
+class FedOPT(FedAvg):
+    """FedOPT class."""
+
+    variant = None  # "fedadam" | "fedyogi" | "fedadagrad"
+
+    def __init__(self, beta_1, beta_2, eta, tau):
+        super().__init__()
+        self.current_weights = None
+        self._d_t = None
+        self._prev_current = None
+        self.m_t = None
+        self.v_t = None
+        self.beta_1 = beta_1
+        self.beta_2 = beta_2
+        self.eta = eta
+        self.tau = tau
+
+    # d_t is an attribute in the reference; keep it readable (and assignable)
+    @property
+    def d_t(self):
+        if self._d_t is None and self._prev_current is not None and self.agg_weights is not None:
+            self._d_t = {k: self.agg_weights[k] - self._prev_current[k] for k in self.agg_weights.keys()}
+        return self._d_t
+
+    @d_t.setter
+    def d_t(self, value):
+        self._d_t = value
+
+    def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
+        logger.debug("calling fedopt (flame_amd)")
+        if self.current_weights is not None and base_weights is not None and len(cache) > 0 and total != 0:
+            return self._do_fused(base_weights, cache, total)
+        self.agg_weights = super().do(base_weights, cache, total=total, version=version)
+        if self.agg_weights is None:
+            return self.current_weights
+        if self.current_weights is None:
+            self.current_weights = self.agg_weights
+        else:  # pragma: no cover - every non-None path with state goes through _do_fused
+            raise AssertionError("unreachable")
+        return self.current_weights
+
+    # ------------------------------------------------------------------ fused round
+    def _do_fused(self, base_weights, cache, total):
+        self.agg_weights = base_weights
+        entries = self._pop_entries(cache, total)
+        current = self.current_weights
+        device = engine.pick_device(base_weights, current, *[w for w, _ in entries])
+        keys = list(base_weights.keys())
+        fused, generic = [], []
+        for k in keys:
+            ok = (base_weights[k].dtype == torch.float32 and k in current
+                  and current[k].dtype == torch.float32 and current[k].shape == base_weights[k].shape
+                  and all(k in w and w[k].dtype == torch.float32 for w, _ in entries)
+                  and (self.m_t is None or (self.m_t[k].dtype == torch.float32 and self.v_t[k].dtype == torch.float32)))
+            (fused if ok else generic).append(k)
+        for w, _ in entries:
+            for k in w.keys():
+                if k not in base_weights:
+                    raise KeyError(k)
+
+        state_zero = self.m_t is None
+        if state_zero:
+            self.m_t, self.v_t = {}, {}
+        new_cur = {}
+        if fused:
+            targets = [engine._Target(base_weights[k], device) for k in fused]
+            curs = [engine._as_device(current[k], device) for k in fused]
+            outs = [torch.empty(base_weights[k].shape, dtype=torch.float32, device=device) for k in fused]
+            ms, vs = [], []
+            for k in fused:
+                if state_zero:
+                    self.m_t[k] = torch.empty(base_weights[k].shape, dtype=torch.float32, device=device)
+                    self.v_t[k] = torch.empty(base_weights[k].shape, dtype=torch.float32, device=device)
+                else:
+                    self.m_t[k] = engine._as_device(self.m_t[k], device)
+                    self.v_t[k] = engine._as_device(self.v_t[k], device)
+                ms.append(self.m_t[k])
+                vs.append(self.v_t[k])
+            hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
+            engine.fedopt_reduce_adapt_(self.variant, [t.dev for t in targets], [t.dev for t in targets], curs,
+                                        outs, ms, vs, [[w[k] for w, _ in entries] for k in fused],
+                                        [r for _, r in entries], hyper, state_zero)
+            for t in targets:
+                t.writeback()
+            new_cur.update(zip(fused, outs))
+        if generic:
+            sub = {k: base_weights[k] for k in generic}
+            engine.accumulate(sub, [({k: w[k] for k in generic if k in w}, r) for w, r in entries], device=device)
+            new_cur.update(self._adapt_generic(generic, base_weights, current, state_zero))
+        self._prev_current = current
+        self._d_t = None
+        self.current_weights = OrderedDict((k, new_cur[k]) for k in current.keys() if k in new_cur)
+        return self.current_weights
+
+    def _adapt_generic(self, keys, average, current, state_zero):
+        """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""
+        out = {}
+        for k in keys:
+            d = average[k] - current[k]
+            m = torch.zeros_like(d) if state_zero or k not in self.m_t else self.m_t[k]
+            m = self.beta_1 * m + (1 - self.beta_1) * d
+            v = torch.zeros_like(d) if state_zero or k not in self.v_t else self.v_t[k]
+            v = self._delta_v_tensor(v, d)
+            self.m_t[k], self.v_t[k] = m, v
+            out[k] = current[k] + self.eta * m / (torch.sqrt(v) + self.tau)
+        return out
+
+    @abstractmethod
+    def _delta_v_tensor(self, v, d):
+        """The subclass's _delta_v_pytorch for one key."""

@@ -1,0 +1,155 @@
+/*
+ * flame_amd.h -- C ABI of the MI355X-native server-side aggregation path.
+ *
+ * Drop-in boundary for cisco-open/flame's lib/python data plane.  Each entry
+ * point replaces one PyTorch op sequence in the reference (paths relative to
+ * /root/reference/lib/python/flame/):
+ *
+ *   flame_agg_reduce            optimizer/fedavg.py:79-104   (FedAvg.do client loop +
+ *                                                             _aggregate_pytorch)
+ *                               optimizer/fedbuff.py:89-97,136-157 (FedBuff.do loop +
+ *                                                             _aggregate_pytorch)
+ *   flame_fedopt_reduce_adapt   optimizer/fedopt.py:80-90,102-129 (FedAvg.do + _adapt_pytorch)
+ *                               + fedadam.py:33-35 / fedyogi.py:34-36 / fedadagrad.py:33-35
+ *   flame_fedbuff_scale_add     optimizer/fedbuff.py:101-127 (scale_add_agg_weights), fused with
+ *                               common/util.py:152-159 (delta_weights_pytorch) as used by
+ *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246
+ *   flame_synth_fill            (bench/test plumbing: counter-based synthetic updates)
+ *
+ * Conventions
+ *   - All pointers passed to the compute entry points are DEVICE pointers
+ *     (HBM of the current HIP device) unless stated otherwise; `stream` is a
+ *     hipStream_t (NULL = default stream).  Calls are asynchronous on `stream`.
+ *   - Per element, clients are combined strictly in the order given (the
+ *     reference's cache.iterkeys() order); each reference op is one IEEE
+ *     round-to-nearest-even rounding in the tensor's dtype (no FMA), so results
+ *     are bit-identical to the reference's torch-CPU arithmetic for
+ *     FedAvg/FedBuff.  Only FedOPT's sqrt differs (torch-CPU's fp32 sqrt is not
+ *     correctly rounded; ours is).
+ *   - Return value: FLAME_OK (0) or a nonzero FLAME_E* status; the message is
+ *     available from flame_last_error() (thread-local).  Nothing aborts.
+ */
+#ifndef FLAME_AMD_H
+#define FLAME_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLAME_ABI_VERSION 1
+
+/* status codes */
+#define FLAME_OK 0
+#define FLAME_EINVAL 1   /* bad argument (message in flame_last_error) */
+#define FLAME_EHIP 2     /* HIP runtime error (launch / device) */
+#define FLAME_ENOTSUP 3  /* dtype / variant not supported by this entry point */
+
+/* element types (torch dtypes of the reference state_dict tensors) */
+#define FLAME_F32 0
+#define FLAME_BF16 1
+#define FLAME_F16 2
+#define FLAME_F64 3
+#define FLAME_I64 4
+#define FLAME_I32 5
+
+/* flame_agg_reduce flags */
+#define FLAME_AGG_INIT_FIRST 1u  /* no base: acc = tmp(client 0) (fedbuff.py:139-140,154-155) */
+
+/* flame_fedopt_reduce_adapt variants and flags */
+#define FLAME_FEDADAM 0
+#define FLAME_FEDYOGI 1
+#define FLAME_FEDADAGRAD 2
+#define FLAME_OPT_STATE_ZERO 1u  /* m_t, v_t were None: treat as zeros, do not read (fedopt.py:108-122) */
+
+/* per-segment flag (flame_segment.flags) */
+#define FLAME_SEG_UNALIGNED 1    /* some pointer of this segment is not 16-byte aligned */
+
+/*
+ * One contiguous run of elements (typically one state_dict tensor, or one
+ * dtype group of a flattened model).  Field roles by entry point:
+ *
+ *                 flame_agg_reduce     flame_fedopt_reduce_adapt   flame_fedbuff_scale_add
+ *   out           aggregate (out)      FedAvg result (out, opt.)   base weights (in/out)
+ *   in            base (in; may ==out) base weights (in)           agg_goal_weights (in)
+ *   cur           -                    current weights (in)        -
+ *   cur_out       -                    new current weights (out)   delta = new-old (out, opt.)
+ *   m, v          -                    m_t, v_t (in/out)           -
+ *
+ * chunk_begin is the prefix sum over previous segments of
+ * ceil(numel / flame_chunk_elems(dtype)); the grid covers n_chunks chunks.
+ * The table lives in device memory.
+ */
+typedef struct flame_segment {
+    void *out;
+    const void *in;
+    const void *cur;
+    void *cur_out;
+    void *m;
+    void *v;
+    int64_t numel;
+    int64_t chunk_begin;
+    int64_t flags;
+    int64_t reserved;
+} flame_segment;
+
+/* Library info. */
+int flame_abi_version(void);
+const char *flame_last_error(void);
+/* Elements one workgroup covers per segment chunk for `dtype` (0 if invalid). */
+int64_t flame_chunk_elems(int dtype);
+/* Elements per chunk for the elementwise scale-add kernel. */
+int64_t flame_scale_add_chunk_elems(int dtype);
+
+/*
+ * Weighted client reduction (FedAvg / FedBuff accumulate).
+ *   clients : device array [n_segs][n_clients] of device pointers; row s holds,
+ *             in iteration order, each client's data for segment s.
+ *   rates32 : device [n_clients] fp32 rates (float(count/total) or
+ *             float(1/sqrt(1+version-tres.version))), used for every dtype but f64.
+ *   rates64 : device [n_clients] fp64 rates, used for FLAME_F64 (may be NULL otherwise).
+ * Per element e of each segment:
+ *   acc = in[e] (or tmp_0 with FLAME_AGG_INIT_FIRST);
+ *   for i: tmp = round(v_i[e] * rate_i) (ints: trunc(float(v)*rate)); acc = round(acc + tmp)
+ *   out[e] = acc.
+ */
+int flame_agg_reduce(int dtype, unsigned flags, const flame_segment *segs, int32_t n_segs,
+                     int64_t n_chunks, const void *const *clients, int32_t n_clients,
+                     const float *rates32, const double *rates64, void *stream);
+
+/*
+ * Fused FedAvg + FedOPT adaptive step, fp32 only.  After the reduction above
+ * (avg kept in registers, optionally written to seg.out), per element:
+ *   d = avg - cur; m = b1*m + omb1*d;
+ *   Adam: v = b2*v + omb2*(d*d);  Yogi: v = v - omb2*(d*d)*sign(v - d*d);  AdaGrad: v = v + d*d
+ *   cur_out = cur + (eta*m) / (sqrt(v) + tau)
+ * Scalars are the fp32 roundings torch applies to the Python floats:
+ *   b1 = f32(beta_1), omb1 = f32(1 - beta_1), b2 = f32(beta_2), omb2 = f32(1 - beta_2),
+ *   eta = f32(eta), tau = f32(tau).
+ */
+int flame_fedopt_reduce_adapt(int variant, unsigned flags, const flame_segment *segs,
+                              int32_t n_segs, int64_t n_chunks, const void *const *clients,
+                              int32_t n_clients, const float *rates32, float b1, float omb1,
+                              float b2, float omb2, float eta, float tau, void *stream);
+
+/*
+ * FedBuff scale-add: out[e] = round(out[e] + round(in[e] / goal)); if seg.cur_out
+ * is non-NULL also cur_out[e] = round(new - old) (the middle aggregator's delta).
+ * Float dtypes only (the reference raises for integer tensors).
+ */
+int flame_fedbuff_scale_add(int dtype, const flame_segment *segs, int32_t n_segs,
+                            int64_t n_chunks, int64_t goal, void *stream);
+
+/*
+ * Fill out[0..numel) with the counter-based generator of flame_amd/synth.py:
+ *   value_f32(seed, stream_id, start + j) * scale, rounded RNE to `dtype`
+ *   (FLAME_F32 / FLAME_BF16 / FLAME_F16).  `out` is a device pointer.
+ */
+int flame_synth_fill(int dtype, void *out, int64_t numel, uint64_t seed, uint64_t stream_id,
+                     int64_t start, float scale, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLAME_AMD_H */

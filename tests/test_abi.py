@@ -1,0 +1,62 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/flame_amd.h declares."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "flame_amd.h")
+
+
+def header_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(flame_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_list():
+    from flame_amd import _native
+    assert header_functions() == sorted(_native.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    from flame_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        from flame_amd import build
+        build.build()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _native.LIB_PATH], text=True)
+    syms = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [f for f in header_functions() if f not in syms]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_constants():
+    from flame_amd import _native, engine
+    L = _native.lib()
+    assert L.flame_abi_version() == 1
+    for code in engine.ITEMSIZE:
+        assert L.flame_chunk_elems(code) == engine.chunk_elems(code)
+    for code in engine.FLOAT_CODES:
+        assert L.flame_scale_add_chunk_elems(code) == engine.chunk_elems(code)
+    assert L.flame_chunk_elems(99) == 0
+
+
+def test_argument_validation_without_gpu():
+    """Invalid arguments are rejected on the host with a message, before any HIP call."""
+    from flame_amd import _native
+    L = _native.lib()
+    assert L.flame_agg_reduce(0, 0, None, 0, 1, None, 0, None, None, None) == _native.FLAME_EINVAL
+    assert b"segment" in L.flame_last_error()
+    assert L.flame_fedbuff_scale_add(0, 8, 1, 1, 0, None) == _native.FLAME_EINVAL
+    assert b"goal" in L.flame_last_error()
+    with pytest.raises(_native.FlameError):
+        _native.check(L.flame_synth_fill(0, None, 5, 0, 0, 0, 1.0, None))
+
+
+def test_segment_struct_size():
+    src = open(HDR).read()
+    body = re.search(r"typedef struct flame_segment \{(.*?)\} flame_segment;", src, re.S).group(1)
+    fields = [ln for ln in body.split(";") if ln.strip()]
+    from flame_amd import _native
+    assert len(fields) == _native.SEGMENT_INT64S  # every field is 8 bytes

@@ -1,0 +1,285 @@
+"""GPU parity: the HIP path (through the C ABI) vs the golden vectors and the oracle.
+
+Bitwise for FedAvg / FedBuff in every dtype; FedOPT within the SURVEY §8(c)
+tolerance (elementwise rel <= 1e-6 where |ref| >= 1e-6*max|ref|, rel-L2 <= 1e-6),
+and bitwise wherever only FedAvg arithmetic has happened.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native_loaded():
+    from flame_amd import _native
+    _native.lib()  # fail loudly if the HIP library is missing
+    assert torch.cuda.is_available()
+
+
+def make_amd(sort, **kw):
+    from flame_amd.optimizers import optimizer_provider
+    return optimizer_provider.get(sort, **kw)
+
+
+# ------------------------------------------------------------------ golden vectors
+@pytest.mark.parametrize("name,driver", S.BITWISE_FIXTURES, ids=[n for n, _ in S.BITWISE_FIXTURES])
+def test_golden_bitwise(golden, name, driver):
+    for label, got, exp in driver(golden(name), make_amd, DEV):
+        S.assert_bitwise(f"{name}:{label}", got, exp)
+
+
+@pytest.mark.parametrize("name", S.FEDOPT_FIXTURES)
+def test_golden_fedopt(golden, name):
+    for label, got, exp in S.run_fedopt(golden(name), make_amd, DEV):
+        if label in ("r0/cur", "r0/avg", "r1/avg"):
+            S.assert_bitwise(f"{name}:{label}", got, exp)
+        else:
+            S.assert_close_fedopt(f"{name}:{label}", got, exp)
+
+
+def test_golden_hier_torch_delta(golden):
+    for label, got, exp in S.run_hier(golden("hier_fedbuff_small.npz"), make_amd, DEV, S.delta_torch):
+        S.assert_bitwise(label, got, exp)
+
+
+def test_golden_hier_fused_delta(golden):
+    """Middle aggregator using the fused scale_add+delta kernel."""
+    fx = golden("hier_fedbuff_small.npz")
+    m = fx.meta
+    rnd = m["round"]
+    top_w0 = fx.weights("top_w0")
+    for mid in range(2):
+        opt = make_amd("fedbuff")
+        mid_w = S.to_dev(top_w0, DEV)
+        agg = None
+        for t in range(3):
+            c = S.SortedCache()
+            c[f"m{mid}t{t}"] = S.TR(S.to_dev(fx.weights(f"m{mid}/update{t}"), DEV), 10 + t, rnd - t % 2)
+            agg = opt.do(agg, c, total=10 + t, version=rnd)
+        new, delta = opt.scale_add_agg_weights_with_delta(mid_w, agg, 3)
+        assert new is mid_w
+        S.assert_bitwise(f"m{mid}/delta", delta, fx.weights(f"m{mid}/delta"))
+
+
+# ------------------------------------------------------------------ oracle comparisons
+def _oracle():
+    from oracle import oracle as O
+    return O
+
+
+def _synth_dev(seed, stream, n, sigma, dtype=torch.float32):
+    from flame_amd import engine
+    t = torch.empty(n, dtype=dtype, device=DEV)
+    engine.synth_fill_(t, seed, stream, 0, sigma)
+    return t
+
+
+def test_synth_device_matches_host():
+    from flame_amd import synth
+    for dt in (torch.float32, torch.bfloat16):
+        t = _synth_dev(3, 17, 100_003, 0.01, dt).cpu()
+        h = synth.synth_f32(3, 17, 100_003, 0.01)
+        if dt == torch.bfloat16:
+            assert np.array_equal(t.view(torch.int16).numpy().view(np.uint16), synth.f32_to_bf16_bits(h))
+        else:
+            assert np.array_equal(t.numpy().view(np.uint32), h.view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64,
+                                   torch.int64, torch.int32])
+@pytest.mark.parametrize("numel", [0, 1, 3, 1023, 1024, 4099, 70_001])
+def test_reduce_vs_oracle_dtypes(dtype, numel):
+    O = _oracle()
+    g = torch.Generator().manual_seed(numel * 7 + 1)
+    n = 37
+    if dtype.is_floating_point:
+        base = torch.randn(numel, generator=g, dtype=torch.float64).to(dtype)
+        cl = [(torch.randn(numel, generator=g, dtype=torch.float64) * 1e-2).to(dtype) for _ in range(n)]
+    else:
+        base = torch.randint(-1000, 1000, (numel,), generator=g, dtype=dtype)
+        cl = [torch.randint(-100, 100, (numel,), generator=g, dtype=dtype) for _ in range(n)]
+    counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+    total = sum(counts)
+    exp = base.clone()
+    O.reduce_tensor(exp, cl, [c / total for c in counts])
+    cache = S.SortedCache()
+    for i, (c, k) in enumerate(zip(cl, counts)):
+        cache[f"{i:04d}"] = S.TR({"x": c.to(DEV)}, k)
+    out = make_amd("fedavg").do({"x": base.to(DEV)}, cache, total=total)
+    S.assert_bitwise(f"{dtype}/{numel}", out, {"x": exp})
+
+
+def test_c2_256x1M_bitwise():
+    """Config 2: 256 clients x (1,000,000 + 4,099) fp32, counts U{1..1000}, seed 1."""
+    from flame_amd import synth
+    O = _oracle()
+    n, shapes = 256, [("w", 1_000_000), ("t", 4_099)]
+    P = sum(s for _, s in shapes)
+    base_flat = _synth_dev(1, 0, P, 1.0)
+    clients = [_synth_dev(1, 1 + i, P, 1e-2) for i in range(n)]
+    counts = synth.counts(1, n)
+    total = int(counts.sum())
+
+    def split(flat):
+        out, off = {}, 0
+        for k, s in shapes:
+            out[k] = flat[off:off + s]
+            off += s
+        return out
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"c{i:04d}"] = S.TR(split(clients[i]), int(counts[i]))
+    base = {k: v.clone() for k, v in split(base_flat).items()}
+    base_cpu = {k: v.cpu() for k, v in base.items()}
+    out = make_amd("fedavg").do(base, cache, total=total)
+    for k, _ in shapes:
+        exp = base_cpu[k].clone()
+        O.reduce_tensor(exp, [split(c)[k].cpu() for c in clients], [int(c) / total for c in counts])
+        S.assert_bitwise(f"c2/{k}", {k: out[k]}, {k: exp})
+
+
+def test_unaligned_and_strided_and_host_base():
+    """Views at odd offsets (scalar path), non-contiguous base, CPU-resident base."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(5)
+    n = 9
+    big = [torch.randn(5001, generator=g) * 1e-2 for _ in range(n)]
+    cl = [b.to(DEV)[1:4998] for b in big]                       # 4-byte misaligned views
+    base_full = torch.randn(2, 4997, generator=g)
+    counts = list(range(1, n + 1))
+    total = sum(counts)
+    exp = base_full[1].clone()
+    O.reduce_tensor(exp, [b[1:4998].clone() for b in big], [c / total for c in counts])
+    # non-contiguous device base (column of a transposed tensor)
+    base_dev = base_full.t().contiguous().to(DEV).t()[1]
+    assert not base_dev.is_contiguous()
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i}"] = S.TR({"x": cl[i]}, counts[i])
+    base = {"x": base_dev}
+    out = make_amd("fedavg").do(base, cache, total=total)
+    assert out["x"] is base_dev
+    S.assert_bitwise("strided", {"x": base_dev.contiguous()}, {"x": exp})
+    # host-resident base and clients (end-to-end path): mutated in place on the host
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i}"] = S.TR({"x": big[i][1:4998].clone()}, counts[i])
+    hb = base_full[1].clone()
+    out = make_amd("fedavg").do({"x": hb}, cache, total=total)
+    assert out["x"] is hb and hb.device.type == "cpu"
+    S.assert_bitwise("host", {"x": hb}, {"x": exp})
+
+
+def test_fedbuff_errors_and_int_scale_add():
+    opt = make_amd("fedbuff")
+    c = S.SortedCache()
+    c["a"] = S.TR({"w": torch.ones(4, device=DEV)}, 3, 5)
+    with pytest.raises(ZeroDivisionError):
+        opt.do(None, c, total=3, version=4)          # 1 + 4 - 5 == 0
+    c["b"] = S.TR({"w": torch.ones(4, device=DEV)}, 3, 9)
+    with pytest.raises(ValueError):
+        opt.do(None, c, total=3, version=4)          # sqrt of a negative
+    with pytest.raises(RuntimeError):
+        opt.scale_add_agg_weights({"n": torch.ones(3, dtype=torch.int64, device=DEV)},
+                                  {"n": torch.ones(3, dtype=torch.int64, device=DEV)}, 2)
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
+def test_fedopt_vs_oracle_random(sort):
+    """Four rounds at N=64, P=300,001 fp32 (+ an int64 buffer on the generic path)."""
+    O = _oracle()
+    g = torch.Generator().manual_seed({"fedadam": 1, "fedyogi": 2, "fedadagrad": 3}[sort])
+    P, n, rounds = 300_001, 64, 4
+    w0 = torch.randn(P, generator=g)
+    data = []
+    for r in range(rounds):
+        cl = [torch.randn(P, generator=g) * 1e-2 for _ in range(n)]
+        counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+        data.append((cl, counts))
+    amd, ora = make_amd(sort), O.OracleFedOPT(sort)
+    wa = {"w": w0.to(DEV), "nbt": torch.tensor(7, dtype=torch.int64, device=DEV)}
+    wo = {"w": w0.clone()}
+    for r, (cl, counts) in enumerate(data):
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i in range(n):
+            ca[f"{i:03d}"] = S.TR({"w": cl[i].to(DEV), "nbt": torch.tensor(r + 1, device=DEV)}, counts[i])
+            co[f"{i:03d}"] = S.TR({"w": cl[i].clone()}, counts[i])
+        wa = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=sum(counts))
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, co, total=sum(counts))
+        if r == 0:
+            S.assert_bitwise(f"{sort}/r0", {"w": wa["w"]}, wo)
+        else:
+            S.assert_close_fedopt(f"{sort}/r{r}/cur", {"w": wa["w"]}, wo)
+            S.assert_close_fedopt(f"{sort}/r{r}/m", {"w": amd.m_t["w"]}, {"w": ora.m_t["w"]})
+    assert wa["nbt"].dtype == torch.float32  # the reference promotes int buffers in the adaptive step
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fedbuff_stream_vs_oracle(dtype):
+    """FedBuff: 12 single-entry do() calls with staleness 0..3, then scale_add (+delta)."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(99)
+    P = 123_457
+    w0 = (torch.randn(P, generator=g)).to(dtype)
+    ups = [(torch.randn(P, generator=g) * 1e-2).to(dtype) for _ in range(12)]
+    stale = [i % 4 for i in range(12)]
+    amd, ora = make_amd("fedbuff"), O.OracleFedBuff()
+    aa = ao = None
+    for i, u in enumerate(ups):
+        ca, co = S.SortedCache(), S.SortedCache()
+        ca[f"{i}"] = S.TR({"w": u.to(DEV)}, 5, 10 - stale[i])
+        co[f"{i}"] = S.TR({"w": u.clone()}, 5, 10 - stale[i])
+        aa = amd.do(aa, ca, total=5, version=10)
+        ao = ora.do(ao, co, total=5, version=10)
+    S.assert_bitwise(f"fedbuff/{dtype}/agg", S.to_cpu(aa), ao)
+    wa = {"w": w0.to(DEV)}
+    wo = {"w": w0.clone()}
+    new, delta = amd.scale_add_agg_weights_with_delta(wa, aa, 12)
+    prev = w0.clone()
+    ora.scale_add_agg_weights(wo, ao, 12)
+    S.assert_bitwise(f"fedbuff/{dtype}/out", S.to_cpu(new), wo)
+    S.assert_bitwise(f"fedbuff/{dtype}/delta", S.to_cpu(delta), {"w": wo["w"] - prev})
+
+
+def test_c3_full_size_sampled_columns():
+    """Config 3 at full size (1024 x 25M fp32 = 102.4 GB in HBM): the kernel's
+    output at 65,536 random elements equals the oracle run on those columns."""
+    from flame_amd import synth, engine
+    O = _oracle()
+    n, P = 1024, 25_000_000
+    free, _ = torch.cuda.mem_get_info()
+    if free < (n + 4) * P * 4:
+        pytest.skip(f"needs {(n + 4) * P * 4 / 1e9:.1f} GB of HBM, {free / 1e9:.1f} GB free")
+    slab = torch.empty((n, P), dtype=torch.float32, device=DEV)
+    for i in range(n):
+        engine.synth_fill_(slab[i], 2, 1 + i, 0, 1e-2)
+    base = _synth_dev(2, 0, P, 1.0)
+    base0 = base.clone()
+    counts = synth.counts(2, n)
+    total = int(counts.sum())
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i:05d}"] = S.TR({"model": slab[i]}, int(counts[i]))
+    out = make_amd("fedavg").do({"model": base}, cache, total=total)
+    torch.cuda.synchronize()
+    idx = torch.from_numpy(np.random.default_rng(0).choice(P, 65_536, replace=False)).to(DEV)
+    idx = torch.cat([idx, torch.tensor([0, P - 1], device=DEV)])
+    cols = slab[:, idx].cpu()                                     # [n, 65538]
+    exp = base0[idx].cpu().clone()
+    O.reduce_tensor(exp, [cols[i].contiguous() for i in range(n)], [int(c) / total for c in counts])
+    got = out["model"][idx].cpu()
+    assert torch.equal(got.view(torch.int32), exp.view(torch.int32))
+    # the device data is the counter generator's: spot-check one column against the host restatement
+    j = int(idx[5])
+    host = np.array([synth.synth_f32(2, 1 + i, np.array([j]), 1e-2)[0] for i in range(0, n, 97)])
+    assert np.array_equal(host.view(np.uint32), cols[::97, 5].numpy().view(np.uint32))
+    del slab
+    torch.cuda.empty_cache()

@@ -1,0 +1,102 @@
+"""Host-side logic of the drop-in path (no GPU): planning, rates, error behaviour, registry."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import scenarios as S
+from flame_amd import _native as N
+from flame_amd import engine
+
+
+def test_rate32_matches_torch_scalar_rounding():
+    x = torch.ones(1)
+    for r in [0.1, 1 / 3, 2000 / 4000, 123 / 517_311, 1 / math.sqrt(3)]:
+        assert (x * r).item() == engine.rate32(r)
+
+
+def test_plan_layout_and_chunks():
+    segs = [engine.Seg(1000, out=4096, inp=4096, clients=[8192, 12288]),
+            engine.Seg(1, out=8004, inp=8004, clients=[16384, 20480]),
+            engine.Seg(0, out=16, inp=16, clients=[32, 48]),
+            engine.Seg(5000, out=64, inp=64, clients=[4, 128])]       # client ptr 4: unaligned
+    p = engine.plan(N.FLAME_F32, segs, [0.25, 0.75])
+    w = p.meta
+    assert p.n_segs == 4 and p.n_clients == 2
+    chunk = engine.chunk_elems(N.FLAME_F32)
+    assert chunk == 1024
+    begins = [w[i * 10 + 7] for i in range(4)]
+    assert begins == [0, 1, 2, 2]
+    assert p.n_chunks == 2 + 5
+    flags = [w[i * 10 + 8] for i in range(4)]
+    assert flags == [0, N.FLAME_SEG_UNALIGNED, 0, N.FLAME_SEG_UNALIGNED]  # 8004 % 16 != 0
+    assert list(w[p.off_clients // 8: p.off_clients // 8 + 8]) == [8192, 12288, 16384, 20480, 32, 48, 4, 128]
+    r32 = w[p.off_r32 // 8:p.off_r64 // 8].view(np.float32)
+    assert r32[0] == np.float32(0.25) and r32[1] == np.float32(0.75)
+    r64 = w[p.off_r64 // 8:].view(np.float64)
+    assert list(r64) == [0.25, 0.75]
+
+
+def test_plan_rejects_ragged_client_rows():
+    with pytest.raises(ValueError):
+        engine.plan(N.FLAME_F32, [engine.Seg(4, clients=[1]), engine.Seg(4, clients=[1, 2])], [0.5, 0.5])
+
+
+def test_dtype_support():
+    assert engine.dtype_code(torch.bfloat16) == N.FLAME_BF16
+    with pytest.raises(TypeError):
+        engine.dtype_code(torch.uint8)
+
+
+def test_fedavg_none_results_need_no_gpu():
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedavg")
+    base = {"w": torch.ones(3)}
+    assert opt.do(base, S.SortedCache(), total=4) is None
+    assert opt.agg_weights is base
+    c = S.SortedCache()
+    c["a"] = S.TR({"w": torch.ones(3)}, 0)
+    assert opt.do(base, c, total=0) is None and len(c) == 1
+    with pytest.raises(AssertionError):
+        opt.do(None, c, total=1)
+
+
+def test_fedopt_none_returns_current():
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedyogi", beta_1=0.5)
+    assert opt.beta_1 == 0.5 and opt.beta_2 == 0.99 and opt.eta == 1e-2 and opt.tau == 1e-3
+    assert opt.do({"w": torch.ones(2)}, S.SortedCache(), total=3) is None
+
+
+def test_fedbuff_stale_errors_raise_before_launch():
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedbuff")
+    c = S.SortedCache()
+    c["a"] = S.TR({"w": torch.ones(2)}, 1, 6)
+    with pytest.raises(ZeroDivisionError):
+        opt.do(None, c, total=1, version=5)
+    assert len(c) == 0  # popped before the rate, like the reference
+    c["b"] = S.TR({"w": torch.ones(2)}, 1, 9)
+    with pytest.raises(ValueError):
+        opt.do(None, c, total=1, version=5)
+    assert opt.do(None, S.SortedCache(), total=1, version=5) is None
+
+
+def test_provider_semantics():
+    from flame_amd.optimizers import optimizer_provider, ObjectFactory, install, DROP_INS
+    with pytest.raises(ValueError):
+        optimizer_provider.get("scaffold")
+    f = ObjectFactory()
+    install(f)
+    for k in DROP_INS:
+        assert isinstance(f.create(k), DROP_INS[k])
+    assert optimizer_provider.get("fedadam").regularizer.get_term() == 0.0
+
+
+def test_synth_generator_stats():
+    from flame_amd import synth
+    x = synth.synth_f32(0, 5, 200_000, 0.01)
+    assert abs(float(x.mean())) < 1e-4 and abs(float(x.std()) / 0.01 - 1) < 0.01
+    c = synth.counts(1, 256)
+    assert c.min() >= 1 and c.max() <= 1000
