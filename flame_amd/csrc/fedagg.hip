@@ -31,7 +31,26 @@
 
 namespace {
 
-constexpr int kBlock = 256;  // 4 waves of 64 lanes
+// Tunables (compile-time; defaults chosen by tools/kernel_sweep.py on MI355X)
+#ifndef FLAME_BLOCK
+#define FLAME_BLOCK 256   // lanes per workgroup of the reduction kernels
+#endif
+#ifndef FLAME_CU
+#define FLAME_CU 8        // clients whose loads are issued together per lane
+#endif
+#ifndef FLAME_VPT
+#define FLAME_VPT 1       // 16-byte vectors per lane per client (block-strided)
+#endif
+#ifndef FLAME_PIPE
+#define FLAME_PIPE 0      // 1: prefetch the next client batch before combining the current one
+#endif
+#ifndef FLAME_NT
+#define FLAME_NT 1        // non-temporal client loads (read once)
+#endif
+
+constexpr int kBlock = FLAME_BLOCK;
+constexpr int kVPT = FLAME_VPT;
+constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
 
@@ -125,7 +144,7 @@ template <> struct Tr<FLAME_I32> {
     __device__ static A add(A a, A t) { return static_cast<int32_t>(static_cast<uint32_t>(a) + static_cast<uint32_t>(t)); }
 };
 
-template <int DT> constexpr int64_t chunk_elems() { return static_cast<int64_t>(kBlock) * Tr<DT>::EPT; }
+template <int DT> constexpr int64_t chunk_elems() { return static_cast<int64_t>(kBlock) * kVPT * Tr<DT>::EPT; }
 
 // ---------------------------------------------------------------- memory helpers
 // All device data is accessed through address_space(1) (global) pointers so the
@@ -140,7 +159,11 @@ template <typename T> __device__ __forceinline__ gcptr<T> G(const T* p) { return
 template <typename T> __device__ __forceinline__ gptr<T> G(T* p) { return (gptr<T>)(p); }
 
 __device__ __forceinline__ V16 ld_nt(const void* p) {
+#if FLAME_NT
     u4 x = __builtin_nontemporal_load(G(reinterpret_cast<const u4*>(p)));
+#else
+    u4 x = *G(reinterpret_cast<const u4*>(p));
+#endif
     V16 r; r.w[0] = x[0]; r.w[1] = x[1]; r.w[2] = x[2]; r.w[3] = x[3];
     return r;
 }
@@ -178,56 +201,91 @@ __device__ __forceinline__ int find_segment(const flame_segment* __restrict__ se
 }
 
 // ---------------------------------------------------------------- reduction core
-// Reduce clients [0, n) into acc[EPT] for the lane's 16-byte slot at element e0.
-// VEC: whole aligned vector; else element-wise with bounds (tails / unaligned views).
+// A lane owns VPT 16-byte vectors of the chunk, at elements e0 + v*kBlock*EPT.
+// Reduce clients [0, n) into acc for those slots.  VEC: every vector whole and
+// aligned; else element-wise with bounds (tails / unaligned views).
 template <int DT, int CU, bool VEC>
-__device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[Tr<DT>::EPT], bool init_first,
+__device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][Tr<DT>::EPT], bool init_first,
                                                const uint64_t* __restrict__ cp, int n,
                                                const float* __restrict__ r32, const double* __restrict__ r64,
                                                int64_t e0, int64_t numel) {
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;  // vector stride in elements
     int i = 0;
     auto rate32 = [&](int c) -> float { if constexpr (DT == FLAME_F64) return 0.f; else return r32[c]; };
     auto rate64 = [&](int c) -> double { if constexpr (DT == FLAME_F64) return r64[c]; else return 0.0; };
-    auto load_client = [&](int c, T (&x)[EPT]) {
+    auto load_client = [&](int c, T (&x)[kVPT][EPT]) {
         const T* p = reinterpret_cast<const T*>(cp[c]) + e0;
-        if constexpr (VEC) {
-            unpack<T, EPT>(ld_nt(p), x);
-        } else {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) x[j] = (e0 + j < numel) ? ld1(p + j) : T(0);
+        for (int v = 0; v < kVPT; ++v) {
+            if constexpr (VEC) {
+                unpack<T, EPT>(ld_nt(p + v * VS), x[v]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) x[v][j] = (e0 + v * VS + j < numel) ? ld1(p + v * VS + j) : T(0);
+            }
         }
     };
+    auto combine = [&](int c, const T (&x)[kVPT][EPT]) {
+        const float r = rate32(c);
+        const double rd = rate64(c);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[v][j] = X::add(acc[v][j], X::tmp(x[v][j], r, rd));
+    };
     if (init_first && n > 0) {
-        T x[EPT];
+        T x[kVPT][EPT];
         load_client(0, x);
         const float r = rate32(0);
         const double rd = rate64(0);
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) acc[j] = X::tmp(x[j], r, rd);
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[v][j], r, rd);
         i = 1;
     }
+#if FLAME_PIPE
+    if (VEC && i + CU <= n) {
+        // two register batches: batch k+1's loads are in flight while batch k is combined
+        T xa[CU][kVPT][EPT], xb[CU][kVPT][EPT];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) load_client(i + u, xa[u]);
+        while (true) {
+            const bool nb = i + 2 * CU <= n;
+            if (nb) {
+#pragma unroll
+                for (int u = 0; u < CU; ++u) load_client(i + CU + u, xb[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, xa[u]);
+            i += CU;
+            if (!nb) break;
+            const bool na = i + 2 * CU <= n;
+            if (na) {
+#pragma unroll
+                for (int u = 0; u < CU; ++u) load_client(i + CU + u, xa[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, xb[u]);
+            i += CU;
+            if (!na) break;
+        }
+    }
+#endif
     for (; i + CU <= n; i += CU) {
-        T x[CU][EPT];
+        T x[CU][kVPT][EPT];
 #pragma unroll
         for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
 #pragma unroll
-        for (int u = 0; u < CU; ++u) {
-            const float r = rate32(i + u);
-            const double rd = rate64(i + u);
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[u][j], r, rd));
-        }
+        for (int u = 0; u < CU; ++u) combine(i + u, x[u]);
     }
     for (; i < n; ++i) {
-        T x[EPT];
+        T x[kVPT][EPT];
         load_client(i, x);
-        const float r = rate32(i);
-        const double rd = rate64(i);
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[j], r, rd));
+        combine(i, x);
     }
 }
 
@@ -240,6 +298,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     using T = typename X::T;
     using A = typename X::A;
     constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
@@ -247,31 +306,42 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const bool init_first = (flags & FLAME_AGG_INIT_FIRST) != 0;
-    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
-    A acc[EPT];
+    const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    A acc[kVPT][EPT];
+    const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
+    T* op = reinterpret_cast<T*>(sg.out) + e0;
     if (vec) {
         if (!init_first) {
-            T b[EPT];
-            unpack<T, EPT>(ld_v(reinterpret_cast<const T*>(sg.in) + e0), b);
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) acc[j] = X::ld(b[j]);
+            for (int v = 0; v < kVPT; ++v) {
+                T b[EPT];
+                unpack<T, EPT>(ld_v(bp + v * VS), b);
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::ld(b[j]);
+            }
         }
         reduce_clients<DT, CU, true>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
-        T o[EPT];
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) o[j] = X::st(acc[j]);
-        st_v(reinterpret_cast<T*>(sg.out) + e0, pack<T, EPT>(o));
+        for (int v = 0; v < kVPT; ++v) {
+            T o[EPT];
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) o[j] = X::st(acc[v][j]);
+            st_v(op + v * VS, pack<T, EPT>(o));
+        }
     } else {
-        const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
         if (!init_first) {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) acc[j] = X::ld((e0 + j < sg.numel) ? ld1(bp + j) : T(0));
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j)
+                    acc[v][j] = X::ld((e0 + v * VS + j < sg.numel) ? ld1(bp + v * VS + j) : T(0));
         }
         reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
-        T* op = reinterpret_cast<T*>(sg.out) + e0;
 #pragma unroll
-        for (int j = 0; j < EPT; ++j)
-            if (e0 + j < sg.numel) st1(op + j, X::st(acc[j]));
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+                if (e0 + v * VS + j < sg.numel) st1(op + v * VS + j, X::st(acc[v][j]));
     }
 }
 
@@ -307,6 +377,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
                                                         float omb1, float b2, float omb2, float eta, float tau) {
     constexpr int DT = FLAME_F32;
     constexpr int EPT = 4;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
@@ -314,43 +385,56 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
-    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
-    float acc[EPT], cur[EPT], m[EPT], v[EPT], co[EPT];
+    const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    float acc[kVPT][EPT];
     const float* base = reinterpret_cast<const float*>(sg.in) + e0;
     const float* curp = reinterpret_cast<const float*>(sg.cur) + e0;
     float* mp = reinterpret_cast<float*>(sg.m) + e0;
     float* vp = reinterpret_cast<float*>(sg.v) + e0;
+    float* ap = reinterpret_cast<float*>(sg.out);
+    float* cop = reinterpret_cast<float*>(sg.cur_out) + e0;
     if (vec) {
-        unpack<float, EPT>(ld_v(base), acc);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) unpack<float, EPT>(ld_v(base + v * VS), acc[v]);
         reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
-        unpack<float, EPT>(ld_v(curp), cur);
-        if (zero_state) {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) { m[j] = 0.f; v[j] = 0.f; }
-        } else {
-            unpack<float, EPT>(ld_v(mp), m);
-            unpack<float, EPT>(ld_v(vp), v);
+        for (int v = 0; v < kVPT; ++v) {
+            float cur[EPT], m[EPT], vv[EPT], co[EPT];
+            unpack<float, EPT>(ld_v(curp + v * VS), cur);
+            if (zero_state) {
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) { m[j] = 0.f; vv[j] = 0.f; }
+            } else {
+                unpack<float, EPT>(ld_v(mp + v * VS), m);
+                unpack<float, EPT>(ld_v(vp + v * VS), vv);
+            }
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+                adapt_elem<VARIANT>(acc[v][j], cur[j], m[j], vv[j], co[j], b1, omb1, b2, omb2, eta, tau);
+            if (ap) st_v(ap + e0 + v * VS, pack<float, EPT>(acc[v]));
+            st_v(mp + v * VS, pack<float, EPT>(m));
+            st_v(vp + v * VS, pack<float, EPT>(vv));
+            st_v(cop + v * VS, pack<float, EPT>(co));
         }
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) adapt_elem<VARIANT>(acc[j], cur[j], m[j], v[j], co[j], b1, omb1, b2, omb2, eta, tau);
-        if (sg.out) st_v(reinterpret_cast<float*>(sg.out) + e0, pack<float, EPT>(acc));
-        st_v(mp, pack<float, EPT>(m));
-        st_v(vp, pack<float, EPT>(v));
-        st_v(reinterpret_cast<float*>(sg.cur_out) + e0, pack<float, EPT>(co));
     } else {
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) acc[j] = (e0 + j < sg.numel) ? ld1(base + j) : 0.f;
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[v][j] = (e0 + v * VS + j < sg.numel) ? ld1(base + v * VS + j) : 0.f;
         reduce_clients<DT, 1, false>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) {
-            if (e0 + j >= sg.numel) continue;
-            float mj = zero_state ? 0.f : ld1(mp + j), vj = zero_state ? 0.f : ld1(vp + j), cj;
-            adapt_elem<VARIANT>(acc[j], ld1(curp + j), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
-            if (sg.out) st1(reinterpret_cast<float*>(sg.out) + e0 + j, acc[j]);
-            st1(mp + j, mj);
-            st1(vp + j, vj);
-            st1(reinterpret_cast<float*>(sg.cur_out) + e0 + j, cj);
-        }
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                const int64_t o = v * VS + j;
+                if (e0 + o >= sg.numel) continue;
+                float mj = zero_state ? 0.f : ld1(mp + o), vj = zero_state ? 0.f : ld1(vp + o), cj;
+                adapt_elem<VARIANT>(acc[v][j], ld1(curp + o), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
+                if (ap) st1(ap + e0 + o, acc[v][j]);
+                st1(mp + o, mj);
+                st1(vp + o, vj);
+                st1(cop + o, cj);
+            }
     }
 }
 
@@ -394,7 +478,7 @@ template <> struct SA<FLAME_F16> {
 };
 
 template <int DT>
-__global__ __launch_bounds__(kBlock) void scale_add_kernel(const flame_segment* __restrict__ segs, int n_segs,
+__global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                            float gf, double gd) {
     using S = SA<DT>;
     using T = typename S::T;
@@ -402,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void scale_add_kernel(const flame_segment* 
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
-    const int64_t e0 = (chunk - sg.chunk_begin) * (kBlock * EPT) + static_cast<int64_t>(threadIdx.x) * EPT;
+    const int64_t e0 = (chunk - sg.chunk_begin) * (kEwBlock * EPT) + static_cast<int64_t>(threadIdx.x) * EPT;
     if (e0 >= sg.numel) return;
     T* bp = reinterpret_cast<T*>(sg.out) + e0;
     const T* ap = reinterpret_cast<const T*>(sg.in) + e0;
@@ -435,9 +519,9 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 template <int DT>
-__global__ __launch_bounds__(kBlock) void synth_kernel(void* out, int64_t numel, uint64_t ck, int64_t start, float scale) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-    for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < numel; j += stride) {
+__global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t numel, uint64_t ck, int64_t start, float scale) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kEwBlock;
+    for (int64_t j = static_cast<int64_t>(blockIdx.x) * kEwBlock + threadIdx.x; j < numel; j += stride) {
         const uint64_t h = mix64(ck + static_cast<uint64_t>(start + j) * 0x9E3779B97F4A7C15ull);
         const int32_t s = static_cast<int32_t>((h & 0xFFFFu) + ((h >> 16) & 0xFFFFu) + ((h >> 32) & 0xFFFFu) + (h >> 48)) - 131070;
         const float x = __fmul_rn(static_cast<float>(s), scale);
@@ -447,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void synth_kernel(void* out, int64_t numel,
     }
 }
 
-constexpr int kClientUnroll = 8;
+constexpr int kClientUnroll = FLAME_CU;
 
 int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
     if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
@@ -480,10 +564,10 @@ int64_t flame_chunk_elems(int dtype) {
 
 int64_t flame_scale_add_chunk_elems(int dtype) {
     switch (dtype) {
-    case FLAME_F32: return kBlock * SA<FLAME_F32>::EPT;
-    case FLAME_F64: return kBlock * SA<FLAME_F64>::EPT;
-    case FLAME_BF16: return kBlock * SA<FLAME_BF16>::EPT;
-    case FLAME_F16: return kBlock * SA<FLAME_F16>::EPT;
+    case FLAME_F32: return kEwBlock * SA<FLAME_F32>::EPT;
+    case FLAME_F64: return kEwBlock * SA<FLAME_F64>::EPT;
+    case FLAME_BF16: return kEwBlock * SA<FLAME_BF16>::EPT;
+    case FLAME_F16: return kEwBlock * SA<FLAME_F16>::EPT;
     default: return 0;
     }
 }
@@ -557,7 +641,7 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs
     if (rc) return rc;
     if (goal == 0) return set_err(FLAME_EINVAL, "agg_goal must be nonzero");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kEwBlock);
     const float gf = static_cast<float>(goal);
     const double gd = static_cast<double>(goal);
     switch (dtype) {
@@ -577,9 +661,9 @@ int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_
     if (numel == 0) return FLAME_OK;
     const uint64_t ck = mix64((seed * 0x9E3779B97F4A7C15ull) ^ ((stream_id + 1ull) * 0xD1B54A32D192ED03ull));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    int64_t blocks = (numel + kBlock - 1) / kBlock;
+    int64_t blocks = (numel + kEwBlock - 1) / kEwBlock;
     if (blocks > 8192) blocks = 8192;
-    const dim3 grid(static_cast<unsigned>(blocks)), block(kBlock);
+    const dim3 grid(static_cast<unsigned>(blocks)), block(kEwBlock);
     switch (dtype) {
     case FLAME_F32: hipLaunchKernelGGL(synth_kernel<FLAME_F32>, grid, block, 0, st, out, numel, ck, start, scale); break;
     case FLAME_BF16: hipLaunchKernelGGL(synth_kernel<FLAME_BF16>, grid, block, 0, st, out, numel, ck, start, scale); break;

@@ -25,7 +25,6 @@ DTYPE_CODE = {
     torch.float64: N.FLAME_F64, torch.int64: N.FLAME_I64, torch.int32: N.FLAME_I32,
 }
 FLOAT_CODES = (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16, N.FLAME_F64)
-BLOCK = 256
 VEC_BYTES = 16
 ITEMSIZE = {N.FLAME_F32: 4, N.FLAME_BF16: 2, N.FLAME_F16: 2, N.FLAME_F64: 8, N.FLAME_I64: 8, N.FLAME_I32: 4}
 
@@ -38,9 +37,19 @@ def dtype_code(dt: torch.dtype) -> int:
                         f"(supported: {sorted(str(d) for d in DTYPE_CODE)})") from None
 
 
-def chunk_elems(code: int) -> int:
-    """Elements per workgroup chunk (== flame_chunk_elems / flame_scale_add_chunk_elems)."""
-    return BLOCK * VEC_BYTES // ITEMSIZE[code]
+_CHUNK = {}
+
+
+def chunk_elems(code: int, scale_add: bool = False) -> int:
+    """Elements one workgroup covers per chunk, as compiled into the library
+    (flame_chunk_elems / flame_scale_add_chunk_elems; the library loads without a GPU)."""
+    key = (code, scale_add)
+    if key not in _CHUNK:
+        L = N.lib()
+        _CHUNK[key] = int(L.flame_scale_add_chunk_elems(code) if scale_add else L.flame_chunk_elems(code))
+        if _CHUNK[key] <= 0:
+            raise TypeError(f"flame_amd: dtype code {code} not supported by this kernel")
+    return _CHUNK[key]
 
 
 def rate32(rate: float) -> float:
@@ -300,7 +309,7 @@ def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
             keep.append(a)
             d = deltas[s].data_ptr() if deltas is not None else 0
             segs.append(Seg(b.numel(), out=b.data_ptr(), inp=a.data_ptr(), cur_out=d))
-        p = plan(code, segs, [], chunk=chunk_elems(code))
+        p = plan(code, segs, [], chunk=chunk_elems(code, scale_add=True))
         dm = _staging.upload(p.meta, device)
         nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (3 + (1 if deltas is not None else 0))
         with _timed("flame_fedbuff_scale_add", device, nbytes):
@@ -364,12 +373,41 @@ def accumulate(agg: dict, entries, *, device=None) -> None:
         if k in per_key:
             groups.setdefault(tuple(per_key[k]), []).append(k)
     for cis, ks in groups.items():
-        targets = [_Target(agg[k], device) for k in ks]
-        outs = [t.dev for t in targets]
-        clients = [[entries[ci][0][k] for ci in cis] for k in ks]
-        reduce_(outs, outs, clients, [entries[ci][1] for ci in cis])
-        for t in targets:
-            t.writeback()
+        same = [k for k in ks if all(entries[ci][0][k].dtype == agg[k].dtype for ci in cis)]
+        mixed = [k for k in ks if k not in same]
+        if same:
+            targets = [_Target(agg[k], device) for k in same]
+            outs = [t.dev for t in targets]
+            clients = [[entries[ci][0][k] for ci in cis] for k in same]
+            reduce_(outs, outs, clients, [entries[ci][1] for ci in cis])
+            for t in targets:
+                t.writeback()
+        for k in mixed:
+            _accumulate_promoted(agg, k, [entries[ci] for ci in cis], device)
+
+
+def _accumulate_promoted(agg: dict, k, entries, device) -> None:
+    """agg[k] += tmp_i where tmp_i = (v_i * rate_i).to(v_i.dtype) has another dtype.
+
+    torch computes ``acc + tmp`` in promote_types(acc, tmp); in place that is only
+    legal when the promotion is acc's own dtype (e.g. an fp32 aggregate receiving
+    int64 ``num_batches_tracked`` after FedOPT promoted it).  Then
+    ``fl(acc + T(tmp))`` == ``fl(acc + fl(T(tmp) * 1.0))``: each tmp_i is formed in
+    its own dtype by the kernel, cast to acc's dtype, and summed in order with rate 1.
+    """
+    acc = agg[k]
+    tmps = []
+    for w, r in entries:
+        v = w[k]
+        if torch.promote_types(acc.dtype, v.dtype) != acc.dtype:
+            raise RuntimeError(f"result type {torch.promote_types(acc.dtype, v.dtype)} can't be cast to the "
+                               f"desired output type {acc.dtype}")
+        t = v if v.dtype == acc.dtype else None
+        tmp = first_tmp({k: v}, r, device=device)[k]
+        tmps.append(tmp.to(acc.dtype) if t is None else tmp)
+    target = _Target(acc, device)
+    reduce_([target.dev], [target.dev], [tmps], [1.0] * len(tmps))
+    target.writeback()
 
 
 def first_tmp(weights: dict, rate: float, *, device=None) -> dict:

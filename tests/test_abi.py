@@ -35,10 +35,11 @@ def test_library_loads_and_reports_constants():
     from flame_amd import _native, engine
     L = _native.lib()
     assert L.flame_abi_version() == 1
-    for code in engine.ITEMSIZE:
-        assert L.flame_chunk_elems(code) == engine.chunk_elems(code)
+    for code, isz in engine.ITEMSIZE.items():
+        ce = L.flame_chunk_elems(code)
+        assert ce == engine.chunk_elems(code) and (ce * isz) % (256 * 16) == 0
     for code in engine.FLOAT_CODES:
-        assert L.flame_scale_add_chunk_elems(code) == engine.chunk_elems(code)
+        assert L.flame_scale_add_chunk_elems(code) == engine.chunk_elems(code, scale_add=True)
     assert L.flame_chunk_elems(99) == 0
 
 

@@ -11,7 +11,7 @@ fatal() { rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -gt 128 ]; }
 python -m flame_amd.build > $OUT/build.log 2>&1 || { echo "build failed"; exit 2; }
 make -s -C oracle >> $OUT/build.log 2>&1
 
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rs ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
 if fatal $rc; then exit $rc; fi
 

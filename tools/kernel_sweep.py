@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Interleaved A/B sweep of compile-time variants of flame_agg_reduce (fp32).
+
+Each variant is a separate build of flame_amd/csrc/fedagg.hip (FLAME_BLOCK,
+FLAME_CU, FLAME_VPT, FLAME_PIPE, FLAME_NT) loaded side by side with ctypes;
+all run in ONE process on the same device-resident 1024 x 25M slab, rounds
+interleaved (cdna_hip_programming.md §5.4 rule 24), outputs checked bitwise
+against the first variant.
+
+    python tools/kernel_sweep.py --build          # build variants (here or on the box)
+    python tools/kernel_sweep.py --rounds 5       # on the GPU
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "build", "variants")
+
+VARIANTS = {
+    "base": {},
+    "nt0": {"FLAME_NT": 0},
+    "cu4": {"FLAME_CU": 4},
+    "cu16": {"FLAME_CU": 16},
+    "vpt2": {"FLAME_VPT": 2},
+    "vpt2cu4": {"FLAME_VPT": 2, "FLAME_CU": 4},
+    "pipe8": {"FLAME_PIPE": 1},
+    "pipe4": {"FLAME_PIPE": 1, "FLAME_CU": 4},
+    "b512": {"FLAME_BLOCK": 512},
+    "b128": {"FLAME_BLOCK": 128},
+    "b64": {"FLAME_BLOCK": 64},
+}
+
+
+def build_variants(names):
+    from flame_amd import build as B
+    os.makedirs(VDIR, exist_ok=True)
+    for name in names:
+        defs = [f"-D{k}={v}" for k, v in VARIANTS[name].items()]
+        out = os.path.join(VDIR, f"lib_{name}.so")
+        cmd = [B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SRC]
+        subprocess.check_call(cmd)
+        print("built", out, flush=True)
+
+
+def load(name):
+    L = ctypes.CDLL(os.path.join(VDIR, f"lib_{name}.so"))
+    vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint
+    L.flame_chunk_elems.restype = i64
+    L.flame_chunk_elems.argtypes = [ctypes.c_int]
+    L.flame_agg_reduce.restype = ctypes.c_int
+    L.flame_agg_reduce.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp, vp]
+    L.flame_last_error.restype = ctypes.c_char_p
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--clients", type=int, default=1024)
+    ap.add_argument("--params", type=int, default=25_000_000)
+    ap.add_argument("--pad", type=int, default=0, help="extra elements per client row (row pitch)")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    args = ap.parse_args()
+    names = args.variants.split(",")
+    if args.build:
+        build_variants(names)
+        return
+
+    import torch
+    from flame_amd import engine, synth
+    from flame_amd import _native as N
+    dev = torch.device("cuda", 0)
+    n, P = args.clients, args.params
+    slab = torch.empty((n, P + args.pad), dtype=torch.float32, device=dev)
+    for i in range(n):
+        engine.synth_fill_(slab[i, :P], 2, 1 + i, 0, 1e-2)
+    base0 = torch.empty(P, dtype=torch.float32, device=dev)
+    engine.synth_fill_(base0, 2, 0, 0, 1.0)
+    out = torch.empty_like(base0)
+    counts = synth.counts(2, n)
+    rates = [int(c) / int(counts.sum()) for c in counts]
+    libs = {nm: load(nm) for nm in names}
+    plans = {}
+    for nm, L in libs.items():
+        seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
+        p = engine.plan(N.FLAME_F32, [seg], rates, chunk=L.flame_chunk_elems(0))
+        dm = torch.from_numpy(p.meta).to(dev)
+        plans[nm] = (p, dm)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def launch(nm):
+        p, dm = plans[nm]
+        b = dm.data_ptr()
+        rc = libs[nm].flame_agg_reduce(0, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
+                                       b + p.off_r32, b + p.off_r64, stream)
+        if rc:
+            raise RuntimeError(libs[nm].flame_last_error())
+
+    # correctness: every variant bitwise equal to the first
+    ref = None
+    for nm in names:
+        launch(nm)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        elif not torch.equal(out.view(torch.int32), ref.view(torch.int32)):
+            raise SystemExit(f"variant {nm} differs from {names[0]}")
+    times = {nm: [] for nm in names}
+    for r in range(args.rounds):
+        for nm in names:
+            evs = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                launch(nm)
+                e1.record()
+                evs.append((e0, e1))
+            torch.cuda.synchronize()
+            times[nm] += [a.elapsed_time(b) for a, b in evs]
+        print(f"round {r} done", flush=True)
+    nbytes = (n + 2) * P * 4
+    res = {}
+    for nm in names:
+        med, mn = statistics.median(times[nm]), min(times[nm])
+        res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nbytes / med / 1e6, "defs": VARIANTS[nm]}
+        print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nbytes / med / 1e6:8.1f} GB/s", flush=True)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump({"clients": n, "params": P, "pad": args.pad, "results": res}, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
