@@ -364,7 +364,7 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
     } else {
         vn = __fadd_rn(v, d2);
     }
-    const float q = __fdiv_rn(__fmul_rn(eta, mn), __fadd_rn(__fsqrt_rn(vn), tau));
+    const float q = __fdiv_rn(__fmul_rn(eta, mn), __fadd_rn(__builtin_sqrtf(vn)  /* correctly rounded (the __fsqrt_rn builtin lowers to the 1-ulp v_sqrt_f32) */, tau));
     m = mn;
     v = vn;
     cur_out = __fadd_rn(cur, q);

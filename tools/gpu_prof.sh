@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM ceiling probe + PMC traffic passes (FETCH_SIZE / WRITE_SIZE in separate runs, no trace domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$PWD
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 python tools/hbm_probe.py > $OUT/probe.log 2>&1 || { echo "probe rc=$?"; exit 1; }
+tail -8 $OUT/probe.log
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex agg_reduce --output-format csv \
+      -d $OUT/pmc_$C -o run -- python bench.py --steps 3 --warmup 1 --cpu-clients 0 ${BENCH_ARGS:-} > $OUT/pmc_$C.log 2>&1 \
+      || { echo "pmc $C rc=$?"; tail -5 $OUT/pmc_$C.log; exit 1; }
+done
+python tools/pmc_traffic.py --fetch $OUT/pmc_FETCH_SIZE --write $OUT/pmc_WRITE_SIZE --out $OUT/traffic.json
