@@ -1,18 +1,23 @@
 #!/usr/bin/env python3
-"""Benchmark: device-resident FedAvg aggregation throughput on MI355X.
+"""Benchmark: device-resident server-side aggregation throughput on MI355X.
 
-Metric (BASELINE.json): aggregated params/sec (device-resident) = N_clients * P / t,
-summed over ranks.  Default workload = config 3: FedAvg of 1024 synthetic clients x
-25,000,000-param fp32 updates, resident in HBM before timing.  A step is one
-``FedAvg.do(base, cache, total=...)`` through flame's optimizer API (cache refill
-+ client-order drain + segment table + one flame_agg_reduce launch).
+Metric (BASELINE.json): aggregated params/sec (device-resident) = clients x params
+per step / step time, summed over ranks.  Default workload = config 3: FedAvg of
+1024 synthetic clients x 25,000,000-param fp32 updates resident in HBM.  A step is
+one ``FedAvg.do(base, cache, total=...)`` through flame's optimizer API (cache
+refill + iterkeys/pop drain + segment-table upload + one flame_agg_reduce launch).
 
-Multi-GPU (torchrun, one process per GPU, RCCL): the parameter vector is sharded
--- each rank owns a 25M-param slice of a (25M x world)-param model and reduces all
-1024 clients over it (weak scaling: per-GPU work fixed), then an RCCL all-gather
-over xGMI reassembles the global model on every rank inside the timed step.
+Multi-GPU (torchrun, one process per GPU, RCCL): the parameter vector is sharded;
+each rank owns a 25M-param slice of a (25M x world)-param model and reduces all
+1024 clients over it (weak scaling: per-GPU work fixed); the RCCL all-gather that
+reassembles the global model on every rank runs inside the timed step, pipelined
+behind the reduction (flame_amd.shard.ShardedSliceFedAvg).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fedavg|fedadam|fedyogi]
+Other workloads (DESIGN.md numbers; the driver's bench line is the default):
+  --workload fedadam|fedyogi|fedadagrad   config 4 (fused FedOPT kernel, round >= 2)
+  --workload hier_fedbuff                 config 5, one GPU's parameter shard
+                                          (4096 clients = 64 middles x 64, bf16)
+  --e2e                                   host-resident updates: H2D + kernel + D2H
 """
 import argparse
 import json
@@ -27,10 +32,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
+METRIC = "aggregated params/sec (device-resident), 1024-client FedAvg @1/2/4/8 GPU"
 
 
 class Cache(dict):
-    """diskcache.Cache surface used by the optimizers: iterkeys() in key order + pop()."""
+    """diskcache.Cache surface the optimizers use: iterkeys() in key order + pop()."""
 
     def iterkeys(self):
         return iter(sorted(self))
@@ -46,18 +52,22 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "fedadam", "fedyogi", "fedadagrad"])
-    ap.add_argument("--clients", type=int, default=1024)
-    ap.add_argument("--params", type=int, default=25_000_000, help="params per GPU shard")
+    ap.add_argument("--workload", default="fedavg",
+                    choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff"])
+    ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
+    ap.add_argument("--params", type=int, default=None,
+                    help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-rounds", type=int, default=3)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+                    help="PMC-derived HBM bytes per launch (tools/gpu_prof.sh -> tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def setup_dist(args):
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -74,7 +84,7 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline(slab, base0, counts, total, n_cpu, rounds):
+def cpu_baseline(slab, base0, counts, n_cpu, rounds):
     """The reference's op sequence (oracle/torch_cpu.py) on host cores, bounded sample."""
     from oracle import torch_cpu
     n_cpu = min(n_cpu, slab.shape[0])
@@ -102,54 +112,16 @@ def cpu_baseline(slab, base0, counts, total, n_cpu, rounds):
     }
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", local)
-    from flame_amd import _native, engine, synth
-    from flame_amd.optimizers import optimizer_provider
-    _native.lib()
-
-    n, P = args.clients, args.params
-    # ---- synthetic, device-resident inputs (counter generator; rank-specific streams)
-    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
-    for i in range(n):
-        engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
-    base = torch.empty(P, dtype=torch.float32, device=dev)
-    engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
-    base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
-    counts = synth.counts(args.seed, n)
-    total = int(counts.sum())
-    keys = [f"{i:05d}" for i in range(n)]
-    gathered = torch.empty(P * world, dtype=torch.float32, device=dev) if world > 1 else None
-    torch.cuda.synchronize()
-
-    opt = optimizer_provider.get(args.workload)
-    weights = {"model": base}
-
-    def step():
-        nonlocal weights
-        cache = Cache()
-        for i, k in enumerate(keys):
-            cache[k] = TR({"model": slab[i]}, int(counts[i]))
-        if args.workload == "fedavg":
-            out = opt.do(weights, cache, total=total, num_trainers=n)
-        else:  # FedOPT caller convention: do(deepcopy(weights)) -> weights
-            out = opt.do({"model": weights["model"].clone()}, cache, total=total, num_trainers=n)
-            weights = out
-        if world > 1:
-            import torch.distributed as dist
-            dist.all_gather_into_tensor(gathered, out["model"])
-        return out
-
-    for _ in range(args.warmup):
+def timed(world, steps, warmup, step):
+    from flame_amd import engine
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     engine.kernel_events = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     barrier(world)
@@ -159,16 +131,75 @@ def main():
     engine.kernel_events = None
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    return elapsed, events
 
-    # dominant kernel: average duration over the timed region (HIP events on the launch stream)
-    name = "flame_fedopt_reduce_adapt" if args.workload != "fedavg" else "flame_agg_reduce"
+
+def kernel_stats(events, name):
     ks = [(e0.elapsed_time(e1) / 1e3, nb) for (nm, e0, e1, nb) in events if nm == name]
-    k_avg = sum(t for t, _ in ks) / len(ks)
-    k_bytes = ks[0][1]
-    achieved = k_bytes / k_avg / 1e9
+    if not ks:
+        return None
+    total_t = sum(t for t, _ in ks)
+    total_b = sum(b for _, b in ks)
+    return {"launches": len(ks), "avg_s": total_t / len(ks), "bytes_per_launch": total_b / len(ks),
+            "achieved_GBps": total_b / total_t / 1e9}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    dev = torch.device("cuda", local)
+    from flame_amd import _native, engine, synth
+    from flame_amd.optimizers import optimizer_provider
+    _native.lib()  # the HIP library is required; no fallback
+
+    if args.workload == "hier_fedbuff":
+        return bench_hier(args, world, rank, dev)
+
+    n = args.clients or 1024
+    P = args.params or 25_000_000
+    # ---- synthetic inputs (counter generator; rank-specific streams)
+    if args.e2e:
+        return bench_e2e(args, n, P, dev)
+    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
+    for i in range(n):
+        engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+    base = torch.empty(P, dtype=torch.float32, device=dev)
+    engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
+    base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
+    counts = synth.counts(args.seed, n)
+    total = int(counts.sum())
+    keys = [f"{i:05d}" for i in range(n)]
+    torch.cuda.synchronize()
+
+    if world > 1 and args.workload == "fedavg":
+        from flame_amd.shard import ShardedSliceFedAvg
+        opt = ShardedSliceFedAvg(fracs=(1.0,) if args.no_overlap else (0.75, 0.20, 0.05))
+    else:
+        opt = optimizer_provider.get(args.workload)
+    state = {"weights": {"model": base}}
+
+    def step():
+        cache = Cache()
+        for i, k in enumerate(keys):
+            cache[k] = TR({"model": slab[i]}, int(counts[i]))
+        if args.workload == "fedavg":
+            opt.do(state["weights"], cache, total=total, num_trainers=n)
+        else:  # FedOPT caller convention: weights = do(deepcopy(weights), ...)
+            state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=total,
+                                      num_trainers=n)
+        if world > 1 and args.workload != "fedavg":
+            import torch.distributed as dist
+            out = torch.empty(P * world, dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(out, state["weights"]["model"])
+
+    if args.workload != "fedavg":
+        step()  # FedOPT round 1 is a passthrough (fedopt.py:87-88); time adaptive rounds only
+    elapsed, events = timed(world, args.steps, args.warmup, step)
+    name = "flame_agg_reduce" if args.workload == "fedavg" else "flame_fedopt_reduce_adapt"
+    ks = kernel_stats(events, name)
 
     if rank == 0:
         traffic = None
@@ -180,11 +211,15 @@ def main():
             pass
         cpu = None
         if world == 1 and args.cpu_clients > 0 and args.workload == "fedavg":
-            cpu = cpu_baseline(slab, base0, counts, total, args.cpu_clients, args.cpu_rounds)
-        value = n * P * world / (elapsed / args.steps)
+            cpu = cpu_baseline(slab, base0, counts, args.cpu_clients, args.cpu_rounds)
+        # a piece-pipelined step has several launches: price the step's kernels as one
+        launches_per_step = ks["launches"] / args.steps
+        k_time = ks["avg_s"] * launches_per_step
+        k_bytes = ks["bytes_per_launch"] * launches_per_step
+        achieved = k_bytes / k_time / 1e9
         line = {
-            "metric": "aggregated params/sec (device-resident), 1024-client FedAvg @1/2/4/8 GPU",
-            "value": value,
+            "metric": METRIC,
+            "value": n * P * world / (elapsed / args.steps),
             "unit": "client-params/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -197,14 +232,16 @@ def main():
             "data": "synthetic (counter-based generator, flame_amd/synth.py), resident in HBM",
             "config": {
                 "workload": f"{args.workload}: {n} clients x {P} fp32 params per GPU"
-                            + (f" (model {P * world} params, parameter-sharded, RCCL all-gather)" if world > 1 else ""),
+                            + (f" (model {P * world} params, parameter-sharded, RCCL all-gather"
+                               f"{'' if args.no_overlap else ' pipelined'})" if world > 1 else ""),
                 "clients": n, "params_per_gpu": P, "global_params": P * world,
                 "parallelism": f"param-shard{world}" if world > 1 else "single",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                "kernel": name, "kernel_ms": k_avg * 1e3, "algorithmic_bytes": k_bytes,
+                "kernel": name, "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
+                "launches_per_step": launches_per_step,
             },
             "cpu_baseline": cpu,
         }
@@ -212,6 +249,119 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def bench_hier(args, world, rank, dev):
+    """Config 5 on one GPU's parameter shard: 64 middle aggregators x 64 clients (bf16,
+    staleness U{0..3}, aggGoal 64 both levels): per middle FedBuff.do per arrival +
+    fused scale_add/delta, then the top FedBuff over the 64 middle deltas + scale_add.
+    Arrival batching (DeferredAggregate) turns each middle's 64 arrivals into one launch."""
+    from flame_amd import engine, synth
+    from flame_amd.optimizers import optimizer_provider
+    M = 64
+    C = (args.clients or 4096) // M
+    P = args.params or 125_000_000 // 8
+    dt = torch.bfloat16
+    slab = torch.empty((M * C, P), dtype=dt, device=dev)
+    for i in range(M * C):
+        engine.synth_fill_(slab[i], args.seed + 4, 1 + i + rank * 100_000, 0, 1e-2)
+    gw = torch.empty(P, dtype=dt, device=dev)
+    engine.synth_fill_(gw, args.seed + 4, rank * 100_000, 0, 1.0)
+    mids = [gw.clone() for _ in range(M)]
+    stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
+    rnd = 10
+    mid_opts = [optimizer_provider.get("fedbuff") for _ in range(M)]
+    top_opt = optimizer_provider.get("fedbuff")
+    torch.cuda.synchronize()
+
+    def step():
+        top_agg = None
+        deltas = []
+        for m in range(M):
+            agg = None
+            opt = mid_opts[m]
+            for t in range(C):
+                i = m * C + t
+                cache = Cache()
+                cache[f"{i:05d}"] = TR({"model": slab[i]}, 1, rnd - stale[i])
+                agg = opt.do(agg, cache, total=1, version=rnd)
+            _, delta = opt.scale_add_agg_weights_with_delta({"model": mids[m]}, agg, C)
+            deltas.append(delta)
+            cache = Cache()
+            cache[f"mid{m:03d}"] = TR(delta, C, rnd - (m % 2))
+            top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
+        top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
+
+    elapsed, events = timed(world, args.steps, args.warmup, step)
+    red = kernel_stats(events, "flame_agg_reduce")
+    sa = kernel_stats(events, "flame_fedbuff_scale_add")
+    if rank == 0:
+        per_step_kernel = (red["avg_s"] * red["launches"] + sa["avg_s"] * sa["launches"]) / args.steps
+        print(json.dumps({
+            "metric": "aggregated params/sec (device-resident), hierarchical FedBuff shard",
+            "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
+            "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
+            "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU"},
+            "kernels": {"flame_agg_reduce": red, "flame_fedbuff_scale_add": sa,
+                        "kernel_ms_per_step": per_step_kernel * 1e3,
+                        "kernel_client_params_per_s": M * C * P / per_step_kernel},
+        }), flush=True)
+
+
+def bench_e2e(args, n, P, dev):
+    """Host-resident updates: pinned host -> HBM (copy stream, overlapped with the
+    reduction of earlier batches) -> FedAvg -> D2H of the global model."""
+    from flame_amd import engine, synth
+    from flame_amd.optimizers import optimizer_provider
+    n = min(n, 64)
+    batch = 8
+    host = torch.empty((n, P), dtype=torch.float32).pin_memory()
+    tmp = torch.empty(P, dtype=torch.float32, device=dev)
+    for i in range(n):
+        engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
+        host[i].copy_(tmp)
+    base_h = torch.empty(P, dtype=torch.float32).pin_memory()
+    engine.synth_fill_(tmp, args.seed, 0, 0, 1.0)
+    base_h.copy_(tmp)
+    counts = synth.counts(args.seed, n)
+    total = int(counts.sum())
+    dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
+    copy_stream = torch.cuda.Stream(dev)
+    opt = optimizer_provider.get("fedavg")
+    torch.cuda.synchronize()
+
+    def step():
+        base = base_h.to(dev, non_blocking=True)
+        cur = torch.cuda.current_stream(dev)
+        done = [torch.cuda.Event(), torch.cuda.Event()]
+        for b0 in range(0, n, batch):
+            slot = (b0 // batch) % 2
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(done[slot]) if b0 >= 2 * batch else None
+                for j in range(batch):
+                    dslab[slot, j].copy_(host[b0 + j], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+            cur.wait_event(ev)
+            cache = Cache()
+            for j in range(batch):
+                cache[f"{b0 + j:05d}"] = TR({"model": dslab[slot, j]}, int(counts[b0 + j]))
+            # streaming (eager-style) accumulation with the final total keeps FedAvg semantics
+            opt.do({"model": base}, cache, total=total)
+            done[slot].record(cur)
+        out = base.to("cpu", non_blocking=True)
+        return out
+
+    elapsed, events = timed(1, args.steps, args.warmup, step)
+    ks = kernel_stats(events, "flame_agg_reduce")
+    print(json.dumps({
+        "metric": "aggregated params/sec, END-TO-END (host-resident updates, H2D + kernel + D2H)",
+        "value": n * P / (elapsed / args.steps), "unit": "client-params/s",
+        "ms_per_step": elapsed / args.steps * 1e3, "clients": n, "params": P, "batch": batch,
+        "h2d_GBps_effective": n * P * 4 / (elapsed / args.steps) / 1e9,
+        "kernel_ms_per_step": ks["avg_s"] * ks["launches"] / args.steps * 1e3,
+        "note": "client order and per-element arithmetic identical to one FedAvg over all clients",
+    }), flush=True)
 
 
 if __name__ == "__main__":

@@ -7,9 +7,25 @@ Python (so stale-version errors raise exactly as in the reference, :96); with
 quirk, kept); otherwise ``agg[k] += tmp`` in place.  ``scale_add_agg_weights``
 mutates and returns ``base_weights`` (:122-127); integer tensors raise like
 torch's ``int += float`` does.
+
+Batching (MI355X-native, on by default): the async callers hand FedBuff ONE
+arrival per ``do()`` (asyncfl/top_aggregator.py:85-92), which as written costs
+an accumulator read+write per arrival (3 passes of P per update).  With
+``defer=True`` ``do()`` returns a :class:`DeferredAggregate` -- a read-only
+Mapping over the same keys -- and queues the arrival; the queued arrivals are
+reduced in ONE launch, in arrival order with the identical per-element
+operation sequence (bit-identical), the moment anything reads the aggregate
+(``agg[k]``, iteration with values, ``scale_add_agg_weights``, ``deepcopy``) or
+``max_pending`` arrivals are queued.  ``defer=False`` restores one launch per
+``do()`` and a plain dict.
 """
+import collections
+import collections.abc
+import copy
 import logging
 import math
+
+import torch
 
 from .. import engine
 from .abstract import AbstractOptimizer
@@ -18,13 +34,70 @@ from .regularizer import Regularizer
 logger = logging.getLogger(__name__)
 
 
+class DeferredAggregate(collections.abc.Mapping):
+    """FedBuff aggregate whose queued arrivals are reduced on first read."""
+
+    def __init__(self, weights, max_pending):
+        self._keys = list(weights.keys())
+        self._meta = {k: (weights[k].shape, weights[k].dtype) for k in self._keys}
+        self._data = None          # dict of device tensors once materialised
+        self._pending = []         # [(weights, rate)] in arrival order
+        self._max_pending = max_pending
+
+    def _queue(self, entries):
+        for w, _ in entries:
+            for k in w.keys():
+                if k not in self._meta:
+                    raise KeyError(k)
+        self._pending.extend(entries)
+        if len(self._pending) >= self._max_pending:
+            self.flush()
+
+    def flush(self):
+        """Reduce every queued arrival (one launch per dtype)."""
+        if not self._pending:
+            return
+        if self._data is None:
+            # None-start: agg = tmp(first) (fedbuff.py:139-140,154-155), then += the rest
+            device = engine.pick_device(*[w for w, _ in self._pending])
+            self._data = collections.OrderedDict(
+                (k, torch.empty(self._meta[k][0], dtype=self._meta[k][1], device=device)) for k in self._keys)
+            engine.reduce_([self._data[k] for k in self._keys], None,
+                           [[w[k] for w, _ in self._pending] for k in self._keys],
+                           [r for _, r in self._pending], init_first=True)
+        else:
+            engine.accumulate(self._data, self._pending)
+        self._pending = []
+
+    def __getitem__(self, k):
+        self.flush()
+        return self._data[k]
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+    def __deepcopy__(self, memo):
+        self.flush()
+        return copy.deepcopy(dict(self._data), memo)
+
+    def materialize(self):
+        """The aggregate as a plain dict of tensors (flushes)."""
+        self.flush()
+        return dict(self._data)
+
+
 class FedBuff(AbstractOptimizer):
     """FedBuff class."""
 
-    def __init__(self):
+    def __init__(self, defer: bool = True, max_pending: int = 256):
         self.agg_goal_weights = None
         self.is_agg_weights_none = True
         self.regularizer = Regularizer()
+        self.defer = defer
+        self.max_pending = max_pending
 
     def do(self, agg_goal_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         logger.debug("calling fedbuff (flame_amd)")
@@ -47,8 +120,16 @@ class FedBuff(AbstractOptimizer):
         if not entries:
             return
         if self.is_agg_weights_none:
+            # each cached entry re-creates the aggregate: only the last one survives (fedbuff.py:139-140)
             weights, rate = entries[-1]
-            self.agg_goal_weights = engine.first_tmp(weights, rate)
+            if self.defer:
+                agg = DeferredAggregate(weights, self.max_pending)
+                agg._queue([(weights, rate)])
+                self.agg_goal_weights = agg
+            else:
+                self.agg_goal_weights = engine.first_tmp(weights, rate)
+        elif isinstance(self.agg_goal_weights, DeferredAggregate):
+            self.agg_goal_weights._queue(entries)
         else:
             engine.accumulate(self.agg_goal_weights, entries)
 
@@ -63,13 +144,14 @@ class FedBuff(AbstractOptimizer):
         (asyncfl/middle_aggregator.py:221-226,246; common/util.py:152-159) in one pass.
         Returns ``(base_weights, delta)``.
         """
-        import torch
         device = engine.pick_device(base_weights, agg_goal_weights)
         delta = {k: torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
                  for k in base_weights.keys()}
         return self._scale_add(base_weights, agg_goal_weights, agg_goal, delta), delta
 
     def _scale_add(self, base_weights, agg_goal_weights, agg_goal, delta):
+        if isinstance(agg_goal_weights, DeferredAggregate):
+            agg_goal_weights.flush()
         keys = list(base_weights.keys())
         device = engine.pick_device(base_weights, agg_goal_weights)
         targets = [engine._Target(base_weights[k], device) for k in keys]

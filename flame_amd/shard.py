@@ -117,3 +117,67 @@ class ShardedFedAvg:
             self.dist.all_gather_into_tensor(full, acc, group=self.group)
             layout.scatter_(base_weights, dtype, full[:numel])
         return base_weights
+
+
+def piece_bounds(numel: int, fracs, align: int) -> List[Tuple[int, int]]:
+    """Split [0, numel) into len(fracs) aligned pieces of roughly the given fractions."""
+    cuts, acc = [0], 0.0
+    for f in fracs[:-1]:
+        acc += f
+        c = int(numel * acc) // align * align
+        cuts.append(min(max(c, cuts[-1]), numel))
+    cuts.append(numel)
+    return [(a, b) for a, b in zip(cuts, cuts[1:]) if b > a]
+
+
+class ShardedSliceFedAvg:
+    """FedAvg ``do()`` over THIS rank's parameter slice, with the RCCL all-gather of
+    the result pipelined behind the reduction.
+
+    Each rank is handed only its slice of every client update (``{key: flat
+    slice}``, e.g. H2D of a sub-range).  The slice is reduced in a few pieces of
+    decreasing size; as soon as piece c is reduced its all-gather starts on the
+    collective stream while piece c+1 is being reduced, so only the last (small)
+    piece's all-gather is exposed.  The reassembled global vector
+    (``self.global_flat``) is piece-major: global elements
+    ``[world*lo_c, world*hi_c)`` hold piece c of rank 0, rank 1, ... in order, i.e.
+    rank r's local element j of piece c is global element
+    ``world*lo_c + r*(hi_c - lo_c) + (j - lo_c)``.
+    """
+
+    def __init__(self, group=None, fracs=(0.75, 0.20, 0.05), reducer: Reducer = hip_reducer, align: int = 1024):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.fracs = fracs
+        self.reducer = reducer
+        self.align = align  # elements; a multiple of the kernel chunk keeps every piece's blocks whole
+        self.global_flat = None
+        self.agg_weights = None
+
+    def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
+        assert base_weights is not None and len(base_weights) == 1, "one flat slice per rank"
+        self.agg_weights = base_weights
+        if len(cache) == 0 or total == 0:
+            return None
+        entries = []
+        for k in list(cache.iterkeys()):
+            tres = cache.pop(k)
+            entries.append((tres.weights, tres.count / total))
+        (key, base), = base_weights.items()
+        P = base.numel()
+        align = self.align
+        if self.global_flat is None or self.global_flat.numel() != P * self.world:
+            self.global_flat = torch.empty(P * self.world, dtype=base.dtype, device=base.device)
+        rates = [r for _, r in entries]
+        works = []
+        for lo, hi in piece_bounds(P, self.fracs, align):
+            piece = base[lo:hi]
+            self.reducer(piece, [w[key][lo:hi] for w, _ in entries], rates)
+            works.append(self.dist.all_gather_into_tensor(
+                self.global_flat[self.world * lo:self.world * hi], piece, group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        return base_weights

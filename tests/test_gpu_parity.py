@@ -304,3 +304,28 @@ def test_c3_full_size_sampled_columns():
     assert np.array_equal(host.view(np.uint32), cols[::97, 5].numpy().view(np.uint32))
     del slab
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fedbuff_deferred_equals_per_arrival(dtype):
+    """Batched (deferred) FedBuff == one launch per arrival, bitwise, across flush boundaries
+    and with intermediate reads of the aggregate."""
+    g = torch.Generator().manual_seed(3)
+    P = 50_001
+    ups = [(torch.randn(P, generator=g) * 1e-2).to(dtype).to(DEV) for _ in range(13)]
+    a = make_amd("fedbuff", defer=True, max_pending=5)
+    b = make_amd("fedbuff", defer=False)
+    aa = ab = None
+    for i, u in enumerate(ups):
+        ca, cb = S.SortedCache(), S.SortedCache()
+        ca["k"] = S.TR({"w": u}, 3, 20 - i % 4)
+        cb["k"] = S.TR({"w": u}, 3, 20 - i % 4)
+        aa = a.do(aa, ca, total=3, version=20)
+        ab = b.do(ab, cb, total=3, version=20)
+        if i == 7:  # a read in the middle flushes and must not change the result
+            S.assert_bitwise("mid", {"w": aa["w"]}, S.to_cpu(ab))
+    S.assert_bitwise("final", S.to_cpu(aa), S.to_cpu(ab))
+    wa, wb = {"w": ups[0].clone()}, {"w": ups[0].clone()}
+    a.scale_add_agg_weights(wa, aa, 13)
+    b.scale_add_agg_weights(wb, ab, 13)
+    S.assert_bitwise("scale_add", S.to_cpu(wa), S.to_cpu(wb))

@@ -100,3 +100,23 @@ def test_synth_generator_stats():
     assert abs(float(x.mean())) < 1e-4 and abs(float(x.std()) / 0.01 - 1) < 0.01
     c = synth.counts(1, 256)
     assert c.min() >= 1 and c.max() <= 1000
+
+
+def test_fedbuff_defers_arrivals_without_launch():
+    """do() per arrival only queues (no GPU touched until the aggregate is read)."""
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.optimizer.fedbuff import DeferredAggregate
+    opt = optimizer_provider.get("fedbuff")
+    agg = None
+    for i in range(5):
+        c = S.SortedCache()
+        c[f"{i}"] = S.TR({"w": torch.ones(3), "b": torch.ones(1)}, 2, 7 - (i % 3))
+        agg = opt.do(agg, c, total=2, version=7)
+    assert isinstance(agg, DeferredAggregate) and opt.agg_goal_weights is agg
+    assert list(agg) == ["w", "b"] and len(agg) == 2 and len(agg._pending) == 5
+    with pytest.raises(KeyError):
+        c = S.SortedCache()
+        c["x"] = S.TR({"zz": torch.ones(1)}, 1, 7)
+        opt.do(agg, c, total=1, version=7)
+    plain = optimizer_provider.get("fedbuff", defer=False)
+    assert plain.defer is False

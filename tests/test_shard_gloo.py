@@ -66,6 +66,24 @@ def _worker(rank, world, port, q):
         O.OracleFedAvg().do(ref, c2, total=sum(counts))
         ok = all(torch.equal(out[k].view(torch.int16) if out[k].dtype == torch.bfloat16 else out[k],
                              ref[k].view(torch.int16) if ref[k].dtype == torch.bfloat16 else ref[k]) for k in ref)
+        # slice mode + pipelined gather: each rank gets only its slice of one flat vector
+        P = 10_000
+        glob_base = torch.randn(P * world, generator=g)
+        glob_cl = [torch.randn(P * world, generator=g) * 1e-2 for _ in range(n)]
+        fr = (0.75, 0.2, 0.05)
+        pieces = shard.piece_bounds(P, fr, 1024)
+
+        def local(v):  # rank's local slice in piece-major global order
+            return torch.cat([v[world * lo + rank * (hi - lo): world * lo + (rank + 1) * (hi - lo)] for lo, hi in pieces])
+        ss = shard.ShardedSliceFedAvg(fracs=fr, reducer=oracle_reducer)
+        c3 = S.SortedCache()
+        for i in range(n):
+            c3[f"{i:02d}"] = S.TR({"m": local(glob_cl[i])}, counts[i])
+        lb = {"m": local(glob_base)}
+        ss.do(lb, c3, total=sum(counts))
+        ref3 = glob_base.clone()
+        O.reduce_tensor(ref3, glob_cl, [c / sum(counts) for c in counts])
+        ok = ok and torch.equal(ss.global_flat, ref3) and torch.equal(lb["m"], local(ref3))
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -82,3 +100,10 @@ def test_sharded_fedavg_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_piece_bounds():
+    assert shard.piece_bounds(10_000, (0.75, 0.2, 0.05), 1024) == [(0, 7168), (7168, 9216), (9216, 10_000)]
+    assert shard.piece_bounds(100, (0.75, 0.2, 0.05), 1024) == [(0, 100)]
+    b = shard.piece_bounds(25_000_000, (0.75, 0.2, 0.05), 1024)
+    assert b[0][0] == 0 and b[-1][1] == 25_000_000 and all(lo % 1024 == 0 for lo, _ in b)
