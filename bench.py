@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
+    ap.add_argument("--e2e-mode", default="zerocopy", choices=["zerocopy", "copy", "pageable"],
+                    help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
+                         "stream overlapped with the reduction; pageable: reference weights_to_model_device")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-rounds", type=int, default=3)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -309,13 +312,20 @@ def bench_hier(args, world, rank, dev):
 
 
 def bench_e2e(args, n, P, dev):
-    """Host-resident updates: pinned host -> HBM (copy stream, overlapped with the
-    reduction of earlier batches) -> FedAvg -> D2H of the global model."""
+    """Host-resident updates -> FedAvg on the GPU -> global model back in host memory.
+
+    zerocopy: the reduction kernel reads the pinned host updates directly over PCIe
+              (no staging copy, no HBM footprint for updates);
+    copy:     pinned host -> HBM on a copy stream, double-buffered batches overlapped
+              with the reduction of the previous batch;
+    pageable: the reference convention (weights_to_model_device: per-tensor .to(device)
+              from pageable memory), then one FedAvg."""
     from flame_amd import engine, synth
     from flame_amd.optimizers import optimizer_provider
     n = min(n, 64)
     batch = 8
-    host = torch.empty((n, P), dtype=torch.float32).pin_memory()
+    mode = args.e2e_mode
+    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode != "pageable"))
     tmp = torch.empty(P, dtype=torch.float32, device=dev)
     for i in range(n):
         engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
@@ -325,42 +335,54 @@ def bench_e2e(args, n, P, dev):
     base_h.copy_(tmp)
     counts = synth.counts(args.seed, n)
     total = int(counts.sum())
-    dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
-    copy_stream = torch.cuda.Stream(dev)
     opt = optimizer_provider.get("fedavg")
+    out_h = torch.empty(P, dtype=torch.float32).pin_memory()
+    if mode == "copy":
+        dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
+        copy_stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
     def step():
         base = base_h.to(dev, non_blocking=True)
-        cur = torch.cuda.current_stream(dev)
-        done = [torch.cuda.Event(), torch.cuda.Event()]
-        for b0 in range(0, n, batch):
-            slot = (b0 // batch) % 2
-            with torch.cuda.stream(copy_stream):
-                copy_stream.wait_event(done[slot]) if b0 >= 2 * batch else None
-                for j in range(batch):
-                    dslab[slot, j].copy_(host[b0 + j], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(copy_stream)
-            cur.wait_event(ev)
+        if mode == "zerocopy":
             cache = Cache()
-            for j in range(batch):
-                cache[f"{b0 + j:05d}"] = TR({"model": dslab[slot, j]}, int(counts[b0 + j]))
-            # streaming (eager-style) accumulation with the final total keeps FedAvg semantics
+            for i in range(n):
+                cache[f"{i:05d}"] = TR({"model": host[i]}, int(counts[i]))
             opt.do({"model": base}, cache, total=total)
-            done[slot].record(cur)
-        out = base.to("cpu", non_blocking=True)
-        return out
+        elif mode == "pageable":
+            cache = Cache()
+            for i in range(n):  # weights_to_model_device (common/util.py:198-208)
+                cache[f"{i:05d}"] = TR({"model": host[i].to(dev)}, int(counts[i]))
+            opt.do({"model": base}, cache, total=total)
+        else:
+            cur = torch.cuda.current_stream(dev)
+            done = [torch.cuda.Event(), torch.cuda.Event()]
+            for b0 in range(0, n, batch):
+                slot = (b0 // batch) % 2
+                with torch.cuda.stream(copy_stream):
+                    if b0 >= 2 * batch:
+                        copy_stream.wait_event(done[slot])
+                    for j in range(batch):
+                        dslab[slot, j].copy_(host[b0 + j], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(copy_stream)
+                cur.wait_event(ev)
+                cache = Cache()
+                for j in range(batch):
+                    cache[f"{b0 + j:05d}"] = TR({"model": dslab[slot, j]}, int(counts[b0 + j]))
+                # batch after batch with the final total == one FedAvg over all (same order, same ops)
+                opt.do({"model": base}, cache, total=total)
+                done[slot].record(cur)
+        out_h.copy_(base, non_blocking=True)
 
     elapsed, events = timed(1, args.steps, args.warmup, step)
     ks = kernel_stats(events, "flame_agg_reduce")
     print(json.dumps({
-        "metric": "aggregated params/sec, END-TO-END (host-resident updates, H2D + kernel + D2H)",
-        "value": n * P / (elapsed / args.steps), "unit": "client-params/s",
-        "ms_per_step": elapsed / args.steps * 1e3, "clients": n, "params": P, "batch": batch,
-        "h2d_GBps_effective": n * P * 4 / (elapsed / args.steps) / 1e9,
+        "metric": "aggregated params/sec, END-TO-END (host-resident updates -> global model in host memory)",
+        "mode": mode, "value": n * P / (elapsed / args.steps), "unit": "client-params/s",
+        "ms_per_step": elapsed / args.steps * 1e3, "clients": n, "params": P,
+        "host_read_GBps": n * P * 4 / (elapsed / args.steps) / 1e9,
         "kernel_ms_per_step": ks["avg_s"] * ks["launches"] / args.steps * 1e3,
-        "note": "client order and per-element arithmetic identical to one FedAvg over all clients",
     }), flush=True)
 
 

@@ -47,6 +47,9 @@ namespace {
 #ifndef FLAME_NT
 #define FLAME_NT 1        // non-temporal client loads (read once)
 #endif
+#ifndef FLAME_OPT_PREFETCH
+#define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
+#endif
 
 constexpr int kBlock = FLAME_BLOCK;
 constexpr int kVPT = FLAME_VPT;
@@ -396,10 +399,29 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
     if (vec) {
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) unpack<float, EPT>(ld_v(base + v * VS), acc[v]);
+#if FLAME_OPT_PREFETCH
+        float curs[kVPT][EPT], ms[kVPT][EPT], vs[kVPT][EPT];
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            unpack<float, EPT>(ld_v(curp + v * VS), curs[v]);
+            if (!zero_state) {
+                unpack<float, EPT>(ld_v(mp + v * VS), ms[v]);
+                unpack<float, EPT>(ld_v(vp + v * VS), vs[v]);
+            }
+        }
+#endif
         reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             float cur[EPT], m[EPT], vv[EPT], co[EPT];
+#if FLAME_OPT_PREFETCH
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                cur[j] = curs[v][j];
+                m[j] = zero_state ? 0.f : ms[v][j];
+                vv[j] = zero_state ? 0.f : vs[v][j];
+            }
+#else
             unpack<float, EPT>(ld_v(curp + v * VS), cur);
             if (zero_state) {
 #pragma unroll
@@ -408,6 +430,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
                 unpack<float, EPT>(ld_v(mp + v * VS), m);
                 unpack<float, EPT>(ld_v(vp + v * VS), vv);
             }
+#endif
 #pragma unroll
             for (int j = 0; j < EPT; ++j)
                 adapt_elem<VARIANT>(acc[v][j], cur[j], m[j], vv[j], co[j], b1, omb1, b2, omb2, eta, tau);

@@ -137,6 +137,12 @@ class _Staging:
         self._inflight.append((ev, host))
         return dev
 
+    def hold(self, host_tensor: torch.Tensor, device) -> None:
+        """Keep a host tensor a kernel reads directly alive until the stream passes this point."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._inflight.append((ev, host_tensor))
+
 
 _staging = _Staging()
 
@@ -169,10 +175,14 @@ def _stream_ptr(device) -> int:
 
 
 def _keepalive(tensors, device):
+    """Call AFTER the launch: device tensors join the stream's allocator bookkeeping,
+    zero-copy host tensors are held until an event recorded behind the kernel fires."""
     st = torch.cuda.current_stream(device)
     for t in tensors:
         if t.is_cuda:
             t.record_stream(st)
+        else:
+            _staging.hold(t, device)
 
 
 def _device_ptrs(dev_meta: torch.Tensor, p: Plan):
@@ -181,8 +191,17 @@ def _device_ptrs(dev_meta: torch.Tensor, p: Plan):
 
 
 # ------------------------------------------------------------------ launches
+# Zero-copy ingest: a pinned (hipHostMalloc'd) host tensor is device-addressable, so the
+# kernel can stream client updates straight from host memory over PCIe instead of
+# staging them into HBM first (FLAME_AMD_ZERO_COPY=0 disables).
+import os as _os  # noqa: E402
+ZERO_COPY_PINNED = _os.environ.get("FLAME_AMD_ZERO_COPY", "1") != "0"
+
+
 def _as_device(t: torch.Tensor, device) -> torch.Tensor:
     if t.device != device:
+        if ZERO_COPY_PINNED and t.device.type == "cpu" and t.is_contiguous() and t.is_pinned():
+            return t  # kept alive past the launch by _keepalive
         t = t.to(device, non_blocking=True)
     return t.contiguous()
 

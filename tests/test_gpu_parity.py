@@ -329,3 +329,22 @@ def test_fedbuff_deferred_equals_per_arrival(dtype):
     a.scale_add_agg_weights(wa, aa, 13)
     b.scale_add_agg_weights(wb, ab, 13)
     S.assert_bitwise("scale_add", S.to_cpu(wa), S.to_cpu(wb))
+
+
+def test_zero_copy_pinned_host_clients():
+    """Pinned host updates are streamed by the kernel directly (no staging copy): bitwise."""
+    O = _oracle()
+    from flame_amd import engine
+    assert engine.ZERO_COPY_PINNED
+    g = torch.Generator().manual_seed(11)
+    P, n = 300_007, 23
+    cl = [(torch.randn(P, generator=g) * 1e-2).pin_memory() for _ in range(n)]
+    base = torch.randn(P, generator=g)
+    counts = list(range(5, 5 + n))
+    exp = base.clone()
+    O.reduce_tensor(exp, cl, [c / sum(counts) for c in counts])
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i:03d}"] = S.TR({"x": cl[i]}, counts[i])
+    out = make_amd("fedavg").do({"x": base.to(DEV)}, cache, total=sum(counts))
+    S.assert_bitwise("zerocopy", S.to_cpu(out), {"x": exp})

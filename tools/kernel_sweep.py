@@ -34,6 +34,7 @@ VARIANTS = {
     "b512": {"FLAME_BLOCK": 512},
     "b128": {"FLAME_BLOCK": 128},
     "b64": {"FLAME_BLOCK": 64},
+    "optpf": {"FLAME_OPT_PREFETCH": 1},
 }
 
 
@@ -56,6 +57,8 @@ def load(name):
     L.flame_agg_reduce.restype = ctypes.c_int
     L.flame_agg_reduce.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp, vp]
     L.flame_last_error.restype = ctypes.c_char_p
+    L.flame_fedopt_reduce_adapt.restype = ctypes.c_int
+    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [ctypes.c_float] * 6 + [vp]
     return L
 
 
@@ -69,6 +72,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    ap.add_argument("--kernel", default="agg", choices=["agg", "fedadam", "fedyogi"],
+                    help="agg: flame_agg_reduce; fedadam/fedyogi: flame_fedopt_reduce_adapt (state present)")
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
@@ -90,26 +95,44 @@ def main():
     rates = [int(c) / int(counts.sum()) for c in counts]
     libs = {nm: load(nm) for nm in names}
     plans = {}
+    if args.kernel != "agg":
+        cur = base0.clone()
+        m = torch.zeros_like(base0)
+        v = torch.zeros_like(base0)
+        cur_out = torch.empty_like(base0)
     for nm, L in libs.items():
-        seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
+        if args.kernel == "agg":
+            seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
+        else:
+            seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), cur=cur.data_ptr(), cur_out=cur_out.data_ptr(),
+                             m=m.data_ptr(), v=v.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
         p = engine.plan(N.FLAME_F32, [seg], rates, chunk=L.flame_chunk_elems(0))
         dm = torch.from_numpy(p.meta).to(dev)
         plans[nm] = (p, dm)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    hyper = engine.fedopt_scalars(0.9, 0.99, 1e-2, 1e-3)
+
     def launch(nm):
         p, dm = plans[nm]
         b = dm.data_ptr()
-        rc = libs[nm].flame_agg_reduce(0, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
-                                       b + p.off_r32, b + p.off_r64, stream)
+        if args.kernel == "agg":
+            rc = libs[nm].flame_agg_reduce(0, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
+                                           b + p.off_r32, b + p.off_r64, stream)
+        else:
+            rc = libs[nm].flame_fedopt_reduce_adapt({"fedadam": 0, "fedyogi": 1}[args.kernel], 0, b, p.n_segs,
+                                                    p.n_chunks, b + p.off_clients, p.n_clients, b + p.off_r32,
+                                                    *[float(x) for x in hyper], stream)
         if rc:
             raise RuntimeError(libs[nm].flame_last_error())
 
-    # correctness: every variant bitwise equal to the first
+    # correctness: every variant bitwise equal to the first (agg kernel; fedopt state evolves)
     ref = None
     for nm in names:
         launch(nm)
         torch.cuda.synchronize()
+        if args.kernel != "agg":
+            continue
         if ref is None:
             ref = out.clone()
         elif not torch.equal(out.view(torch.int32), ref.view(torch.int32)):
@@ -127,7 +150,7 @@ def main():
             torch.cuda.synchronize()
             times[nm] += [a.elapsed_time(b) for a, b in evs]
         print(f"round {r} done", flush=True)
-    nbytes = (n + 2) * P * 4
+    nbytes = (n + 2) * P * 4 if args.kernel == "agg" else (n + 8) * P * 4
     res = {}
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
