@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
-    ap.add_argument("--e2e-mode", default="zerocopy", choices=["zerocopy", "copy", "pageable"],
+    ap.add_argument("--e2e-mode", default="zerocopy",
+                    choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference"],
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
                          "stream overlapped with the reduction; pageable: reference weights_to_model_device")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
@@ -319,13 +320,18 @@ def bench_e2e(args, n, P, dev):
     copy:     pinned host -> HBM on a copy stream, double-buffered batches overlapped
               with the reduction of the previous batch;
     pageable: the reference convention (weights_to_model_device: per-tensor .to(device)
-              from pageable memory), then one FedAvg."""
+              from pageable memory), then one FedAvg;
+    wire*:    starts from the channel's serialized payloads (cloudpickle of
+              {weights, dataset_size}, channel.py:203-218): wire = flame_amd.ingest.decode
+              (zero-copy views into the payload bytes) + H2D; wire_pinned = payloads sit in
+              pinned receive buffers, decode gives device-addressable views the kernel streams
+              directly; wire_reference = cloudpickle.loads + .to(device) (the reference ingest)."""
     from flame_amd import engine, synth
     from flame_amd.optimizers import optimizer_provider
     n = min(n, 64)
     batch = 8
     mode = args.e2e_mode
-    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode != "pageable"))
+    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode in ("zerocopy", "copy")))
     tmp = torch.empty(P, dtype=torch.float32, device=dev)
     for i in range(n):
         engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
@@ -337,6 +343,19 @@ def bench_e2e(args, n, P, dev):
     total = int(counts.sum())
     opt = optimizer_provider.get("fedavg")
     out_h = torch.empty(P, dtype=torch.float32).pin_memory()
+    if mode.startswith("wire"):
+        import cloudpickle
+        from flame_amd import ingest
+        payloads = []
+        for i in range(n):
+            b = cloudpickle.dumps({"weights": {"model": host[i]}, "dataset_size": int(counts[i])})
+            if mode == "wire_pinned":
+                pb = torch.empty(len(b), dtype=torch.uint8, pin_memory=True)
+                pb.numpy()[:] = memoryview(b)
+                payloads.append(pb.numpy())
+            else:
+                payloads.append(b)
+        del host
     if mode == "copy":
         dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
         copy_stream = torch.cuda.Stream(dev)
@@ -348,6 +367,17 @@ def bench_e2e(args, n, P, dev):
             cache = Cache()
             for i in range(n):
                 cache[f"{i:05d}"] = TR({"model": host[i]}, int(counts[i]))
+            opt.do({"model": base}, cache, total=total)
+        elif mode.startswith("wire"):
+            cache = Cache()
+            for i in range(n):
+                if mode == "wire_reference":
+                    msg = cloudpickle.loads(payloads[i])
+                    w = {k: v.to(dev) for k, v in msg["weights"].items()}
+                else:
+                    msg = ingest.decode(payloads[i])
+                    w = msg["weights"]
+                cache[f"{i:05d}"] = TR(w, msg["dataset_size"])
             opt.do({"model": base}, cache, total=total)
         elif mode == "pageable":
             cache = Cache()

@@ -348,3 +348,39 @@ def test_zero_copy_pinned_host_clients():
         cache[f"{i:03d}"] = S.TR({"x": cl[i]}, counts[i])
     out = make_amd("fedavg").do({"x": base.to(DEV)}, cache, total=sum(counts))
     S.assert_bitwise("zerocopy", S.to_cpu(out), {"x": exp})
+
+
+@pytest.mark.parametrize("where", ["bytes", "pinned", "cache_hbm", "cache_host"])
+def test_ingest_wire_payloads_to_fedavg(where):
+    """Channel payloads (cloudpickle, channel.py:203-218) -> ingest.decode (zero-copy) ->
+    FedAvg on the GPU == oracle on the original tensors, bitwise."""
+    import cloudpickle
+    from flame_amd import ingest
+    O = _oracle()
+    g = torch.Generator().manual_seed(21)
+    n = 12
+    ws = [{"w": torch.randn(4097, 3, generator=g) * 1e-2, "b": (torch.randn(65, generator=g) * 1e-2).bfloat16(),
+           "nbt": torch.tensor(i, dtype=torch.int64)} for i in range(n)]
+    base = {"w": torch.randn(4097, 3, generator=g), "b": torch.randn(65, generator=g).bfloat16(),
+            "nbt": torch.tensor(100, dtype=torch.int64)}
+    counts = [10 + 7 * i for i in range(n)]
+    total = sum(counts)
+    keep = []
+    cache = ingest.DeviceUpdateCache(placement="hbm" if where == "cache_hbm" else "host") \
+        if where.startswith("cache") else S.SortedCache()
+    for i in range(n):
+        b = cloudpickle.dumps({"weights": ws[i], "dataset_size": counts[i]})
+        if where == "pinned":
+            pb = torch.empty(len(b), dtype=torch.uint8, pin_memory=True)
+            pb.numpy()[:] = memoryview(b)
+            b = pb.numpy()
+        keep.append(b)
+        msg = ingest.decode(b)
+        if where == "pinned":
+            assert all(t.is_pinned() for t in msg["weights"].values() if t.numel())
+        cache[f"{i:03d}"] = S.TR(msg["weights"], msg["dataset_size"])
+    out = make_amd("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache, total=total)
+    for k in base:
+        exp = base[k].clone()
+        O.reduce_tensor(exp, [w[k] for w in ws], [c / total for c in counts])
+        S.assert_bitwise(f"{where}/{k}", {k: out[k]}, {k: exp})

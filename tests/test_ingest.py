@@ -1,0 +1,103 @@
+"""Zero-copy restricted decoding of flame channel payloads (flame_amd.ingest)."""
+import enum
+import io
+import os
+import pickle
+import time
+
+import cloudpickle
+import numpy as np
+import pytest
+import torch
+
+from flame_amd import ingest
+
+
+class MsgType(enum.Enum):  # stand-in for flame.common.constants.MessageType
+    WEIGHTS = 1
+    DATASET_SIZE = 3
+    MODEL_VERSION = 5
+
+
+def _msg():
+    g = torch.Generator().manual_seed(0)
+    big = torch.randn(64, 33, generator=g)
+    return {
+        MsgType.WEIGHTS: {
+            "conv.weight": torch.randn(16, 3, 3, 3, generator=g),
+            "bias": torch.randn(16, generator=g).to(torch.bfloat16),
+            "half": torch.randn(7, generator=g).half(),
+            "dbl": torch.randn(5, generator=g).double(),
+            "nbt": torch.tensor(12345678901, dtype=torch.int64),
+            "i32": torch.arange(10, dtype=torch.int32),
+            "mask": torch.tensor([True, False, True]),
+            "empty": torch.empty(0, 4),
+            "slice": big[5:9],            # storage offset != 0
+            "transposed": big.t(),         # non-contiguous strides
+        },
+        MsgType.DATASET_SIZE: 2000,
+        MsgType.MODEL_VERSION: 7,
+        "meta": {"ratio": 0.5, "name": "trainer-1", "tags": ["a", "b"], "none": None, "pair": (1, 2.5)},
+    }
+
+
+def _same(a, b):
+    assert a.dtype == b.dtype and a.shape == b.shape and a.stride() == b.stride() or a.numel() == 0
+    if a.dtype == torch.bfloat16:
+        a, b = a.view(torch.int16), b.view(torch.int16)
+    assert torch.equal(a, b)
+
+
+def test_decode_matches_cloudpickle_and_is_zero_copy():
+    msg = _msg()
+    payload = cloudpickle.dumps(msg)
+    out = ingest.decode(payload, extra_globals=ingest.allow_enum(MsgType))
+    ref = cloudpickle.loads(payload)
+    assert out[MsgType.DATASET_SIZE] == 2000 and out[MsgType.MODEL_VERSION] == 7
+    assert out["meta"] == ref["meta"]
+    base = np.frombuffer(payload, dtype=np.uint8).ctypes.data
+    for k, v in ref[MsgType.WEIGHTS].items():
+        got = out[MsgType.WEIGHTS][k]
+        _same(got, v)
+        if got.numel():
+            assert base <= got.data_ptr() < base + len(payload), f"{k} was copied"
+
+
+def test_decode_refuses_arbitrary_globals():
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("true",))
+    with pytest.raises(pickle.UnpicklingError):
+        ingest.decode(pickle.dumps({"x": Evil()}, protocol=5))
+    with pytest.raises(pickle.UnpicklingError):
+        ingest.decode(cloudpickle.dumps({"f": lambda x: x}))
+    # the channel-level loads() falls back to the reference decoder for non-update messages
+    assert ingest.loads(cloudpickle.dumps({"f": 1.5}))["f"] == 1.5
+
+
+def test_decode_protocols_and_large_update_speed():
+    w = {"fc.weight": torch.randn(1 << 22)}    # 16 MB
+    for proto in (2, 4, 5):
+        payload = pickle.dumps({"w": w, "n": 3}, protocol=proto)
+        out = ingest.decode(payload)
+        assert torch.equal(out["w"]["fc.weight"], w["fc.weight"]) and out["n"] == 3
+    payload = cloudpickle.dumps({"w": w})
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ingest.decode(payload)
+    t_dec = (time.perf_counter() - t0) / 5
+    t0 = time.perf_counter()
+    for _ in range(5):
+        cloudpickle.loads(payload)
+    t_ref = (time.perf_counter() - t0) / 5
+    assert t_dec < t_ref, (t_dec, t_ref)
+
+
+def test_device_update_cache_host_placement_orders_and_pops():
+    from scenarios import TR
+    c = ingest.DeviceUpdateCache(placement="host")
+    for k in ["b", "a", "c"]:
+        c[k] = TR({"w": torch.ones(3)}, 1)
+    assert len(c) == 3 and list(c.iterkeys()) == ["a", "b", "c"] and "a" in c
+    t = c.pop("a")
+    assert t.count == 1 and len(c) == 2 and c.pop("zz") is None

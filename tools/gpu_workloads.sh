@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-WL=${WORKLOADS:-"fedadam fedyogi hier e2e_zerocopy e2e_copy e2e_pageable"}
+WL=${WORKLOADS:-"fedadam fedyogi hier e2e_zerocopy e2e_copy e2e_pageable e2e_wire e2e_wire_pinned e2e_wire_reference"}
 for w in $WL; do
   case $w in
     hier) W="--workload hier_fedbuff --steps 3 --warmup 1";;
