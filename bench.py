@@ -348,7 +348,8 @@ def bench_e2e(args, n, P, dev):
         from flame_amd import ingest
         payloads = []
         for i in range(n):
-            b = cloudpickle.dumps({"weights": {"model": host[i]}, "dataset_size": int(counts[i])})
+            # a trainer's update owns its storage (pickling a view would ship the whole slab)
+            b = cloudpickle.dumps({"weights": {"model": host[i].clone()}, "dataset_size": int(counts[i])})
             if mode == "wire_pinned":
                 pb = torch.empty(len(b), dtype=torch.uint8, pin_memory=True)
                 pb.numpy()[:] = memoryview(b)

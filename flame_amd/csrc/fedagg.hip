@@ -38,6 +38,9 @@ namespace {
 #ifndef FLAME_CU
 #define FLAME_CU 8        // clients whose loads are issued together per lane
 #endif
+#ifndef FLAME_CU16
+#define FLAME_CU16 FLAME_CU  // client unroll for 16-bit dtypes (8 elements per lane vector)
+#endif
 #ifndef FLAME_VPT
 #define FLAME_VPT 1       // 16-byte vectors per lane per client (block-strided)
 #endif
@@ -555,6 +558,7 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 }
 
 constexpr int kClientUnroll = FLAME_CU;
+constexpr int kClientUnroll16 = FLAME_CU16;
 
 int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
     if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
@@ -612,10 +616,10 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
         hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
         break;
     case FLAME_BF16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
         break;
     case FLAME_F16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
         break;
     case FLAME_F64:
         hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);

@@ -5,8 +5,9 @@ from .fedadam import FedAdam
 from .fedavg import FedAvg
 from .fedbuff import FedBuff
 from .fedopt import FedOPT
+from .fedprox import FedProx
 from .fedyogi import FedYogi
 from .train_result import TrainResult
 
 __all__ = ["AbstractOptimizer", "FedAvg", "FedOPT", "FedAdam", "FedYogi", "FedAdaGrad", "FedBuff",
-           "TrainResult"]
+           "FedProx", "TrainResult"]

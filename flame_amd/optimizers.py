@@ -4,11 +4,11 @@ flame's own provider so existing roles pick them up unchanged.
 
 ``OptimizerType`` is a closed enum validated by flame's config
 (config.py:55-70,121-123), so the drop-in re-registers the existing keys
-(``fedavg``, ``fedadagrad``, ``fedadam``, ``fedyogi``, ``fedbuff``) instead of
-adding new ones.  Keys the MI355X path does not cover (fedprox, feddyn,
+(``fedavg``, ``fedadagrad``, ``fedadam``, ``fedyogi``, ``fedbuff``, ``fedprox``)
+instead of adding new ones.  Keys the MI355X path does not cover (feddyn,
 scaffold, fedgft) keep flame's own classes.
 """
-from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedYogi
+from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedProx, FedYogi
 
 DROP_INS = {
     "fedavg": FedAvg,
@@ -16,6 +16,7 @@ DROP_INS = {
     "fedadam": FedAdam,
     "fedyogi": FedYogi,
     "fedbuff": FedBuff,
+    "fedprox": FedProx,
 }
 
 

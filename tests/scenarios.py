@@ -57,6 +57,7 @@ def assert_bitwise(label, got, exp):
         assert g.shape == e.shape, f"{label}/{k}: shape {g.shape} vs {e.shape}"
         ga, _ = tensor_to_np(g)
         ea, _ = tensor_to_np(e)
+        ga, ea = ga.reshape(-1), ea.reshape(-1)
         if not np.array_equal(ga.view(np.uint8), ea.view(np.uint8)):
             bad = np.flatnonzero(ga.reshape(-1) != ea.reshape(-1))
             raise AssertionError(f"{label}/{k}: {bad.size} elements differ, first at {bad[:5]}: "

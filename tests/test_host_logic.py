@@ -90,7 +90,8 @@ def test_provider_semantics():
     f = ObjectFactory()
     install(f)
     for k in DROP_INS:
-        assert isinstance(f.create(k), DROP_INS[k])
+        kw = {"mu": 0.01} if k == "fedprox" else {}
+        assert isinstance(f.create(k, **kw), DROP_INS[k])
     assert optimizer_provider.get("fedadam").regularizer.get_term() == 0.0
 
 
@@ -120,3 +121,13 @@ def test_fedbuff_defers_arrivals_without_launch():
         opt.do(agg, c, total=1, version=7)
     plain = optimizer_provider.get("fedbuff", defer=False)
     assert plain.defer is False
+
+
+def test_fedprox_is_fedavg_with_regularizer():
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.optimizer.fedavg import FedAvg
+    opt = optimizer_provider.get("fedprox", mu=0.1)
+    assert isinstance(opt, FedAvg) and opt.mu == 0.1
+    w = [torch.ones(3), torch.zeros(2)]
+    wt = [torch.zeros(3), torch.zeros(2)]
+    assert abs(float(opt.regularizer.get_term(w=w, w_t=wt)) - 0.15) < 1e-7

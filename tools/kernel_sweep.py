@@ -35,6 +35,9 @@ VARIANTS = {
     "b128": {"FLAME_BLOCK": 128},
     "b64": {"FLAME_BLOCK": 64},
     "optpf": {"FLAME_OPT_PREFETCH": 1},
+    "c16_4": {"FLAME_CU16": 4},
+    "c16_2": {"FLAME_CU16": 2},
+    "c16_4v2": {"FLAME_CU16": 4, "FLAME_VPT": 2},
 }
 
 
@@ -72,6 +75,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--kernel", default="agg", choices=["agg", "fedadam", "fedyogi"],
                     help="agg: flame_agg_reduce; fedadam/fedyogi: flame_fedopt_reduce_adapt (state present)")
     args = ap.parse_args()
@@ -85,10 +89,12 @@ def main():
     from flame_amd import _native as N
     dev = torch.device("cuda", 0)
     n, P = args.clients, args.params
-    slab = torch.empty((n, P + args.pad), dtype=torch.float32, device=dev)
+    tdt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    code = N.FLAME_F32 if args.dtype == "f32" else N.FLAME_BF16
+    slab = torch.empty((n, P + args.pad), dtype=tdt, device=dev)
     for i in range(n):
         engine.synth_fill_(slab[i, :P], 2, 1 + i, 0, 1e-2)
-    base0 = torch.empty(P, dtype=torch.float32, device=dev)
+    base0 = torch.empty(P, dtype=tdt, device=dev)
     engine.synth_fill_(base0, 2, 0, 0, 1.0)
     out = torch.empty_like(base0)
     counts = synth.counts(2, n)
@@ -106,7 +112,7 @@ def main():
         else:
             seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), cur=cur.data_ptr(), cur_out=cur_out.data_ptr(),
                              m=m.data_ptr(), v=v.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
-        p = engine.plan(N.FLAME_F32, [seg], rates, chunk=L.flame_chunk_elems(0))
+        p = engine.plan(code, [seg], rates, chunk=L.flame_chunk_elems(code))
         dm = torch.from_numpy(p.meta).to(dev)
         plans[nm] = (p, dm)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -117,7 +123,7 @@ def main():
         p, dm = plans[nm]
         b = dm.data_ptr()
         if args.kernel == "agg":
-            rc = libs[nm].flame_agg_reduce(0, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
+            rc = libs[nm].flame_agg_reduce(code, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
                                            b + p.off_r32, b + p.off_r64, stream)
         else:
             rc = libs[nm].flame_fedopt_reduce_adapt({"fedadam": 0, "fedyogi": 1}[args.kernel], 0, b, p.n_segs,
@@ -135,7 +141,7 @@ def main():
             continue
         if ref is None:
             ref = out.clone()
-        elif not torch.equal(out.view(torch.int32), ref.view(torch.int32)):
+        elif not torch.equal(out.view(torch.int16), ref.view(torch.int16)):
             raise SystemExit(f"variant {nm} differs from {names[0]}")
     times = {nm: [] for nm in names}
     for r in range(args.rounds):
@@ -150,7 +156,8 @@ def main():
             torch.cuda.synchronize()
             times[nm] += [a.elapsed_time(b) for a, b in evs]
         print(f"round {r} done", flush=True)
-    nbytes = (n + 2) * P * 4 if args.kernel == "agg" else (n + 8) * P * 4
+    isz = 4 if args.dtype == "f32" else 2
+    nbytes = (n + 2) * P * isz if args.kernel == "agg" else (n + 8) * P * 4
     res = {}
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
