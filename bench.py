@@ -75,10 +75,18 @@ def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; FLAME_BENCH_BACKEND=gloo lets several ranks share one GPU to
+    # rehearse the N>1 path on a single-GPU box (the driver's N>1 runs use RCCL = "nccl")
+    backend = os.environ.get("FLAME_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -135,7 +143,8 @@ def timed(world, steps, warmup, step):
     engine.kernel_events = None
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, events
@@ -196,8 +205,12 @@ def main():
                                       num_trainers=n)
         if world > 1 and args.workload != "fedavg":
             import torch.distributed as dist
-            out = torch.empty(P * world, dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(out, state["weights"]["model"])
+            if dist.get_backend() == "gloo":
+                out = torch.empty(P * world, dtype=torch.float32)
+                dist.all_gather_into_tensor(out, state["weights"]["model"].cpu())
+            else:
+                out = torch.empty(P * world, dtype=torch.float32, device=dev)
+                dist.all_gather_into_tensor(out, state["weights"]["model"])
 
     if args.workload != "fedavg":
         step()  # FedOPT round 1 is a passthrough (fedopt.py:87-88); time adaptive rounds only

@@ -173,11 +173,17 @@ class ShardedSliceFedAvg:
             self.global_flat = torch.empty(P * self.world, dtype=base.dtype, device=base.device)
         rates = [r for _, r in entries]
         works = []
+        staged = base.is_cuda and self.dist.get_backend(self.group) == "gloo"  # gloo: host collectives
         for lo, hi in piece_bounds(P, self.fracs, align):
             piece = base[lo:hi]
             self.reducer(piece, [w[key][lo:hi] for w, _ in entries], rates)
-            works.append(self.dist.all_gather_into_tensor(
-                self.global_flat[self.world * lo:self.world * hi], piece, group=self.group, async_op=True))
+            dst = self.global_flat[self.world * lo:self.world * hi]
+            if staged:
+                host = torch.empty(dst.numel(), dtype=dst.dtype)
+                self.dist.all_gather_into_tensor(host, piece.cpu(), group=self.group)
+                dst.copy_(host)
+            else:
+                works.append(self.dist.all_gather_into_tensor(dst, piece, group=self.group, async_op=True))
         for w in works:
             w.wait()
         return base_weights
