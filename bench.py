@@ -250,7 +250,8 @@ def main():
             "config": {
                 "workload": f"{args.workload}: {n} clients x {P} fp32 params per GPU"
                             + (f" (model {P * world} params, parameter-sharded, RCCL all-gather"
-                               f"{'' if args.no_overlap else ' pipelined'})" if world > 1 else ""),
+                               f"{' pipelined' if (args.workload == 'fedavg' and not args.no_overlap) else ''})"
+                               if world > 1 else ""),
                 "clients": n, "params_per_gpu": P, "global_params": P * world,
                 "parallelism": f"param-shard{world}" if world > 1 else "single",
             },
