@@ -6,20 +6,20 @@
 
 using u4 = __attribute__((ext_vector_type(4))) uint32_t;
 
-template <int NT>
+template <int NT, int UN = 8>
 __global__ __launch_bounds__(256) void read_kernel(const u4* __restrict__ p, int64_t n4, uint32_t* out) {
     const int64_t stride = (int64_t)gridDim.x * 256;
     uint32_t acc = 0;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 7 * stride < n4; i += 8 * stride) {
-        u4 v[8];
+    for (; i + (UN - 1) * stride < n4; i += UN * stride) {
+        u4 v[UN];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < UN; ++u) {
             auto q = (const __attribute__((address_space(1))) u4*)(p + i + u * stride);
             v[u] = NT ? __builtin_nontemporal_load(q) : *q;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+        for (int u = 0; u < UN; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
     }
     for (; i < n4; i += stride) { u4 v = p[i]; acc ^= v[0] ^ v[1] ^ v[2] ^ v[3]; }
     if (acc == 0x12345678u) out[0] = acc;  // keep the loads live
@@ -27,7 +27,34 @@ __global__ __launch_bounds__(256) void read_kernel(const u4* __restrict__ p, int
 
 extern "C" int probe_read(const void* p, int64_t bytes, void* out, int blocks, int nt, void* stream) {
     const int64_t n4 = bytes / 16;
-    if (nt) hipLaunchKernelGGL(read_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u4*)p, n4, (uint32_t*)out);
-    else hipLaunchKernelGGL(read_kernel<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u4*)p, n4, (uint32_t*)out);
+    if (nt == 2) hipLaunchKernelGGL((read_kernel<1, 16>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u4*)p, n4, (uint32_t*)out);
+    else if (nt) hipLaunchKernelGGL((read_kernel<1, 8>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u4*)p, n4, (uint32_t*)out);
+    else hipLaunchKernelGGL((read_kernel<0, 8>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u4*)p, n4, (uint32_t*)out);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// LDS-DMA ceiling: each wave streams 1 KiB pieces (global_load_lds_dwordx4) into a private
+// 8-slot LDS ring and never consumes them (transfer-only upper bound, cf. MI355X_MICROARCH.md
+// row 'ldsdma-fill').  AUX = cache policy bits (2 = nt).
+template <int AUX>
+__global__ __launch_bounds__(256) void read_lds_kernel(const uint8_t* __restrict__ p, int64_t pieces) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[4 * 8 * 1024];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    int it = 0;
+    for (int64_t pc = gw; pc < pieces; pc += nw, ++it) {
+        auto src = (const __attribute__((address_space(1))) void*)(p + pc * 1024 + lane * 16);
+        auto dst = (__attribute__((address_space(3))) void*)(ring + wave * 8192 + (it & 7) * 1024);
+        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, AUX);
+        if ((it & 7) == 7) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+extern "C" int probe_read_lds(const void* p, int64_t bytes, int blocks, int nt, void* stream) {
+    const int64_t pieces = bytes / 1024;
+    if (nt) hipLaunchKernelGGL(read_lds_kernel<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, pieces);
+    else hipLaunchKernelGGL(read_lds_kernel<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, pieces);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }

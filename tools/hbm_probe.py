@@ -30,7 +30,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     res = {}
     for blocks in (2048, 4096, 8192, 16384):
-        for nt in (0, 1):
+        for nt in (0, 1, 2):
             ts = []
             for _ in range(5):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,7 +41,23 @@ def main():
                 ts.append(e0.elapsed_time(e1))
             t = statistics.median(ts)
             res[f"blocks{blocks}_nt{nt}"] = {"ms": t, "GBps": nbytes / t / 1e6}
-            print(f"blocks {blocks:6d} nt {nt}: {t:8.3f} ms  {nbytes / t / 1e6:8.1f} GB/s", flush=True)
+            print(f"blocks {blocks:6d} nt {nt} (2: nt + 16 loads/lane): {t:8.3f} ms  {nbytes / t / 1e6:8.1f} GB/s",
+                  flush=True)
+    L.probe_read_lds.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    for blocks in (1024, 2048, 4096):
+        for nt in (0, 1):
+            ts = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                assert L.probe_read_lds(buf.data_ptr(), nbytes, blocks, nt, st) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            t = statistics.median(ts)
+            res[f"lds_blocks{blocks}_nt{nt}"] = {"ms": t, "GBps": nbytes / t / 1e6}
+            print(f"LDS-DMA blocks {blocks:6d} nt {nt}: {t:8.3f} ms  {nbytes / t / 1e6:8.1f} GB/s", flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "hbm_probe.json"), "w"), indent=1)
 
 

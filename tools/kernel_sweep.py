@@ -38,6 +38,7 @@ VARIANTS = {
     "c16_4": {"FLAME_CU16": 4},
     "c16_2": {"FLAME_CU16": 2},
     "c16_4v2": {"FLAME_CU16": 4, "FLAME_VPT": 2},
+    "cu16b128": {"FLAME_CU": 16, "FLAME_BLOCK": 128},
 }
 
 
@@ -99,6 +100,9 @@ def main():
     out = torch.empty_like(base0)
     counts = synth.counts(2, n)
     rates = [int(c) / int(counts.sum()) for c in counts]
+    probe = "probe" in names
+    if probe:
+        names = [x for x in names if x != "probe"]
     libs = {nm: load(nm) for nm in names}
     plans = {}
     if args.kernel != "agg":
@@ -120,6 +124,9 @@ def main():
     hyper = engine.fedopt_scalars(0.9, 0.99, 1e-2, 1e-3)
 
     def launch(nm):
+        if nm == "probe":
+            assert PL.probe_read(slab.data_ptr(), pbytes, pout.data_ptr(), 16384, 2, stream) == 0
+            return
         p, dm = plans[nm]
         b = dm.data_ptr()
         if args.kernel == "agg":
@@ -132,12 +139,25 @@ def main():
         if rc:
             raise RuntimeError(libs[nm].flame_last_error())
 
+    if probe:  # same-process HBM read ceiling (tools/hbm_probe.hip, best config) over the same slab
+        PL = ctypes.CDLL(os.path.join(ROOT, "build", "hbm_probe.so"))
+        PL.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p]
+        pout = torch.zeros(4, dtype=torch.int32, device=dev)
+        pbytes = slab.numel() * slab.element_size() // 4096 * 4096
+
+        class _P:
+            pass
+        libs["probe"] = _P()
+        plans["probe"] = None
+        names = names + ["probe"]
+
     # correctness: every variant bitwise equal to the first (agg kernel; fedopt state evolves)
     ref = None
     for nm in names:
         launch(nm)
         torch.cuda.synchronize()
-        if args.kernel != "agg":
+        if args.kernel != "agg" or nm == "probe":
             continue
         if ref is None:
             ref = out.clone()
@@ -161,8 +181,9 @@ def main():
     res = {}
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
-        res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nbytes / med / 1e6, "defs": VARIANTS[nm]}
-        print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nbytes / med / 1e6:8.1f} GB/s", flush=True)
+        nb = pbytes if nm == "probe" else nbytes
+        res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nb / med / 1e6, "defs": VARIANTS.get(nm, {})}
+        print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nb / med / 1e6:8.1f} GB/s", flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump({"clients": n, "params": P, "pad": args.pad, "results": res}, open(args.out, "w"), indent=1)
 
