@@ -59,6 +59,9 @@ def parse():
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--layout", default="slab", choices=["slab", "row"],
+                    help="slab: updates in the tiled UpdateSlab (what DeviceUpdateCache produces); "
+                         "row: one contiguous tensor per client (weights_to_model_device layout)")
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--e2e-mode", default="zerocopy",
                     choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference"],
@@ -96,11 +99,11 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline(slab, base0, counts, n_cpu, rounds):
+def cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
     """The reference's op sequence (oracle/torch_cpu.py) on host cores, bounded sample."""
     from oracle import torch_cpu
-    n_cpu = min(n_cpu, slab.shape[0])
-    ups = [{"model": slab[i].cpu()} for i in range(n_cpu)]
+    n_cpu = min(n_cpu, n)
+    ups = [{"model": host_row(i)} for i in range(n_cpu)]
     agg = {"model": base0.cpu()}
     cts = [int(c) for c in counts[:n_cpu]]
     tot = sum(cts)
@@ -111,7 +114,6 @@ def cpu_baseline(slab, base0, counts, n_cpu, rounds):
         torch_cpu.fedavg_round(agg, ups, cts, tot)
         ts.append(time.perf_counter() - t0)
     t = statistics.median(ts)
-    P = slab.shape[1]
     try:
         model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:  # noqa: BLE001
@@ -160,6 +162,37 @@ def kernel_stats(events, name):
             "achieved_GBps": total_b / total_t / 1e9}
 
 
+def read_ceiling(buf: torch.Tensor, reps: int = 5):
+    """Same-device HBM streaming-read ceiling (tools/hbm_probe.hip, best measured config:
+    16,384 workgroups, 16 nt dwordx4 loads in flight per lane) over an existing buffer."""
+    import ctypes
+    import subprocess
+    so = os.path.join(ROOT, "build", "hbm_probe.so")
+    try:
+        if not os.path.exists(so):
+            os.makedirs(os.path.dirname(so), exist_ok=True)
+            subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                                   "-o", so, os.path.join(ROOT, "tools", "hbm_probe.hip")])
+        L = ctypes.CDLL(so)
+    except Exception:  # noqa: BLE001
+        return None
+    L.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_void_p]
+    nbytes = buf.numel() * buf.element_size() // 4096 * 4096
+    out = torch.zeros(4, dtype=torch.int32, device=buf.device)
+    st = torch.cuda.current_stream(buf.device).cuda_stream
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if L.probe_read(buf.data_ptr(), nbytes, out.data_ptr(), 16384, 2, st) != 0:
+            return None
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    return nbytes / statistics.median(ts) / 1e9
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist()
@@ -176,9 +209,24 @@ def main():
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
         return bench_e2e(args, n, P, dev)
-    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
-    for i in range(n):
-        engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+    if args.layout == "slab":
+        from flame_amd.slab import UpdateSlab
+        store = UpdateSlab({"model": torch.empty(P, dtype=torch.float32)}, capacity=n, device=dev)
+        tmp = torch.empty(P, dtype=torch.float32, device=dev)
+        client_w = []
+        for i in range(n):
+            engine.synth_fill_(tmp, args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+            client_w.append(store.put({"model": tmp}))        # tiled slot views, held for the run
+        del tmp
+        slab_buf = store.storage[torch.float32]
+        host_row = lambda i: store.read(i, "model").cpu()    # noqa: E731
+    else:
+        slab = torch.empty((n, P), dtype=torch.float32, device=dev)
+        for i in range(n):
+            engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+        client_w = [{"model": slab[i]} for i in range(n)]
+        slab_buf = slab
+        host_row = lambda i: slab[i].cpu()                   # noqa: E731
     base = torch.empty(P, dtype=torch.float32, device=dev)
     engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
     base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
@@ -197,7 +245,7 @@ def main():
     def step():
         cache = Cache()
         for i, k in enumerate(keys):
-            cache[k] = TR({"model": slab[i]}, int(counts[i]))
+            cache[k] = TR(client_w[i], int(counts[i]))
         if args.workload == "fedavg":
             opt.do(state["weights"], cache, total=total, num_trainers=n)
         else:  # FedOPT caller convention: weights = do(deepcopy(weights), ...)
@@ -228,7 +276,8 @@ def main():
             pass
         cpu = None
         if world == 1 and args.cpu_clients > 0 and args.workload == "fedavg":
-            cpu = cpu_baseline(slab, base0, counts, args.cpu_clients, args.cpu_rounds)
+            cpu = cpu_baseline(host_row, n, P, base0, counts, args.cpu_clients, args.cpu_rounds)
+        ceiling = read_ceiling(slab_buf) if world == 1 else None
         # a piece-pipelined step has several launches: price the step's kernels as one
         launches_per_step = ks["launches"] / args.steps
         k_time = ks["avg_s"] * launches_per_step
@@ -248,7 +297,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (counter-based generator, flame_amd/synth.py), resident in HBM",
             "config": {
-                "workload": f"{args.workload}: {n} clients x {P} fp32 params per GPU"
+                "workload": f"{args.workload}: {n} clients x {P} fp32 params per GPU, {args.layout} layout"
                             + (f" (model {P * world} params, parameter-sharded, RCCL all-gather"
                                f"{' pipelined' if (args.workload == 'fedavg' and not args.no_overlap) else ''})"
                                if world > 1 else ""),
@@ -260,6 +309,9 @@ def main():
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                 "kernel": name, "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
                 "launches_per_step": launches_per_step,
+                # same device, same buffer: plain streaming-read probe (tools/hbm_probe.hip)
+                "measured_read_ceiling_GBps": ceiling,
+                "frac_of_measured_ceiling": (achieved / ceiling) if ceiling else None,
             },
             "cpu_baseline": cpu,
         }

@@ -206,6 +206,18 @@ __device__ __forceinline__ int find_segment(const flame_segment* __restrict__ se
     return lo;
 }
 
+// Byte offset of this lane's first element inside every client's data for the
+// workgroup's chunk: contiguous (e0 * sizeof) or tiled (chunk * client_tile_stride + lane).
+template <int DT>
+__device__ __forceinline__ int64_t client_offset(const flame_segment& sg, int64_t chunk) {
+    using T = typename Tr<DT>::T;
+    const int64_t cl = chunk - sg.chunk_begin;
+    const int64_t lane_elem = static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
+    if (sg.client_tile_stride)
+        return cl * sg.client_tile_stride + lane_elem * static_cast<int64_t>(sizeof(T));
+    return (cl * chunk_elems<DT>() + lane_elem) * static_cast<int64_t>(sizeof(T));
+}
+
 // ---------------------------------------------------------------- reduction core
 // A lane owns VPT 16-byte vectors of the chunk, at elements e0 + v*kBlock*EPT.
 // Reduce clients [0, n) into acc for those slots.  VEC: every vector whole and
@@ -214,7 +226,7 @@ template <int DT, int CU, bool VEC>
 __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][Tr<DT>::EPT], bool init_first,
                                                const uint64_t* __restrict__ cp, int n,
                                                const float* __restrict__ r32, const double* __restrict__ r64,
-                                               int64_t e0, int64_t numel) {
+                                               int64_t e0, int64_t numel, int64_t coff) {
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
@@ -223,7 +235,7 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
     auto rate32 = [&](int c) -> float { if constexpr (DT == FLAME_F64) return 0.f; else return r32[c]; };
     auto rate64 = [&](int c) -> double { if constexpr (DT == FLAME_F64) return r64[c]; else return 0.0; };
     auto load_client = [&](int c, T (&x)[kVPT][EPT]) {
-        const T* p = reinterpret_cast<const T*>(cp[c]) + e0;
+        const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[c]) + coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             if constexpr (VEC) {
@@ -311,6 +323,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const int64_t coff = client_offset<DT>(sg, chunk);
     const bool init_first = (flags & FLAME_AGG_INIT_FIRST) != 0;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     A acc[kVPT][EPT];
@@ -326,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
                 for (int j = 0; j < EPT; ++j) acc[v][j] = X::ld(b[j]);
             }
         }
-        reduce_clients<DT, CU, true>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
+        reduce_clients<DT, CU, true>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             T o[EPT];
@@ -342,7 +355,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
                 for (int j = 0; j < EPT; ++j)
                     acc[v][j] = X::ld((e0 + v * VS + j < sg.numel) ? ld1(bp + v * VS + j) : T(0));
         }
-        reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel);
+        reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
@@ -390,6 +403,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const int64_t coff = client_offset<DT>(sg, chunk);
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     float acc[kVPT][EPT];
@@ -413,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
             }
         }
 #endif
-        reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
+        reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             float cur[EPT], m[EPT], vv[EPT], co[EPT];
@@ -447,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
             for (int j = 0; j < EPT; ++j) acc[v][j] = (e0 + v * VS + j < sg.numel) ? ld1(base + v * VS + j) : 0.f;
-        reduce_clients<DT, 1, false>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel);
+        reduce_clients<DT, 1, false>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll

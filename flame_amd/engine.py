@@ -68,9 +68,10 @@ class Seg:
     m: int = 0
     v: int = 0
     clients: List[int] = field(default_factory=list)
+    tile_stride: int = 0   # bytes between consecutive chunks of one client (0 = contiguous)
 
     def pointers(self):
-        return [self.out, self.inp, self.cur, self.cur_out, self.m, self.v] + list(self.clients)
+        return [self.out, self.inp, self.cur, self.cur_out, self.m, self.v, self.tile_stride] + list(self.clients)
 
 
 @dataclass
@@ -99,7 +100,7 @@ def plan(code: int, segs: Sequence[Seg], rates: Sequence[float], chunk: Optional
             raise ValueError("every segment needs one pointer per client")
         unaligned = any(p % VEC_BYTES for p in s.pointers() if p)
         words += [s.out, s.inp, s.cur, s.cur_out, s.m, s.v, s.numel, begin,
-                  N.FLAME_SEG_UNALIGNED if unaligned else 0, 0]
+                  N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride]
         begin += -(-s.numel // chunk) if s.numel > 0 else 0
     if begin == 0:
         begin = 1  # all segments empty: one (idle) chunk keeps the launch valid
@@ -206,6 +207,55 @@ def _as_device(t: torch.Tensor, device) -> torch.Tensor:
     return t.contiguous()
 
 
+def tiled_stride(c: torch.Tensor, numel: int) -> int:
+    """Bytes between chunks if ``c`` is a tiled slab view for a ``numel``-element
+    aggregate (shape (ceil(numel/T), T), unit inner stride; see flame_amd/slab.py), else 0."""
+    if c.dim() != 2 or not c.is_cuda or c.stride(1) != 1:
+        return 0
+    T = chunk_elems(dtype_code(c.dtype))
+    if c.shape[1] != T or c.shape[0] != max(1, -(-numel // T)) or c.stride(0) < T:
+        return 0
+    return c.stride(0) * c.element_size()
+
+
+def slice_elems(t: torch.Tensor, lo: int, hi: int, numel: int) -> torch.Tensor:
+    """Elements [lo, hi) of a client tensor of ``numel`` logical elements, keeping a tiled
+    slab view tiled (``lo`` must then be a multiple of the chunk)."""
+    if t.is_cuda and tiled_stride(t, numel):
+        T = t.shape[1]
+        if lo % T:
+            raise ValueError(f"tiled slice must start on a chunk boundary ({T})")
+        return t[lo // T: -(-hi // T)]
+    return t.reshape(-1)[lo:hi]
+
+
+def _client_row(cs, o: torch.Tensor, device, keep):
+    """Device pointers of one segment's clients + the segment's client_tile_stride.
+
+    If every client is a tiled slab view with the same stride, the kernel reads
+    them tiled; otherwise every client is read contiguous (tiled views that are
+    mixed with other layouts in one call are copied out -- rare)."""
+    n = o.numel()
+    for c in cs:
+        if c.dtype != o.dtype:
+            raise NotImplementedError(
+                f"flame_amd: client tensor dtype {c.dtype} differs from aggregate dtype {o.dtype}")
+    strides = [tiled_stride(c, n) if c.device == device else 0 for c in cs]
+    if cs and strides[0] and all(t == strides[0] for t in strides):
+        keep.extend(cs)
+        return [c.data_ptr() for c in cs], strides[0]
+    row = []
+    for c, ts in zip(cs, strides):
+        if ts:
+            c = c.reshape(-1)[:n]             # contiguous copy of a tiled view
+        elif c.numel() != n:
+            raise RuntimeError(f"flame_amd: client tensor has {c.numel()} elements, aggregate {n}")
+        c = _as_device(c, device)
+        keep.append(c)
+        row.append(c.data_ptr())
+    return row, 0
+
+
 def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients: List[List[torch.Tensor]],
             rates: Sequence[float], *, init_first: bool = False) -> None:
     """outs[s] = ins[s] (+)= Σ_i round(clients[s][i] * rates[i]) in order (kernel: flame_agg_reduce).
@@ -228,22 +278,13 @@ def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients
         for s in idx:
             o = outs[s]
             assert o.is_contiguous() and o.device == device
-            row = []
-            for c in clients[s]:
-                if c.dtype != o.dtype:
-                    raise NotImplementedError(
-                        f"flame_amd: client tensor dtype {c.dtype} differs from aggregate dtype {o.dtype}")
-                if c.numel() != o.numel():
-                    raise RuntimeError(f"flame_amd: client tensor has {c.numel()} elements, aggregate {o.numel()}")
-                c = _as_device(c, device)
-                keep.append(c)
-                row.append(c.data_ptr())
+            row, tstride = _client_row(clients[s], o, device, keep)
             inp = 0
             if not init_first:
                 i_t = ins[s]
                 assert i_t.is_contiguous() and i_t.device == device and i_t.numel() == o.numel()
                 inp = i_t.data_ptr()
-            segs.append(Seg(o.numel(), out=o.data_ptr(), inp=inp, clients=row))
+            segs.append(Seg(o.numel(), out=o.data_ptr(), inp=inp, clients=row, tile_stride=tstride))
         p = plan(code, segs, rates)
         dm = _staging.upload(p.meta, device)
         segp, clp, r32p, r64p = _device_ptrs(dm, p)
@@ -272,16 +313,10 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
     for s in range(len(base)):
         for t in (base[s], cur[s], cur_out[s], m[s], v[s]):
             assert t.dtype == torch.float32 and t.is_contiguous() and t.device == device
-        row = []
-        for c in clients[s]:
-            if c.dtype != torch.float32 or c.numel() != base[s].numel():
-                raise RuntimeError("flame_amd: FedOPT fused path needs fp32 clients matching the model")
-            c = _as_device(c, device)
-            keep.append(c)
-            row.append(c.data_ptr())
+        row, tstride = _client_row(clients[s], base[s], device, keep)
         segs.append(Seg(base[s].numel(), out=avg_out[s].data_ptr() if avg_out[s] is not None else 0,
                         inp=base[s].data_ptr(), cur=cur[s].data_ptr(), cur_out=cur_out[s].data_ptr(),
-                        m=m[s].data_ptr(), v=v[s].data_ptr(), clients=row))
+                        m=m[s].data_ptr(), v=v[s].data_ptr(), clients=row, tile_stride=tstride))
     p = plan(N.FLAME_F32, segs, rates)
     dm = _staging.upload(p.meta, device)
     segp, clp, r32p, _ = _device_ptrs(dm, p)
@@ -422,11 +457,20 @@ def _accumulate_promoted(agg: dict, k, entries, device) -> None:
             raise RuntimeError(f"result type {torch.promote_types(acc.dtype, v.dtype)} can't be cast to the "
                                f"desired output type {acc.dtype}")
         t = v if v.dtype == acc.dtype else None
-        tmp = first_tmp({k: v}, r, device=device)[k]
+        tmp = torch.empty(acc.shape, dtype=v.dtype, device=device)
+        reduce_([tmp], None, [[v]], [r], init_first=True)
         tmps.append(tmp.to(acc.dtype) if t is None else tmp)
     target = _Target(acc, device)
     reduce_([target.dev], [target.dev], [tmps], [1.0] * len(tmps))
     target.writeback()
+
+
+def logical_shape(weights, k):
+    """Shape of ``weights[k]`` as the model sees it (slab slots hand out tiled views)."""
+    shapes = getattr(weights, "shapes", None)
+    if shapes is not None and k in shapes:
+        return shapes[k]
+    return weights[k].shape
 
 
 def first_tmp(weights: dict, rate: float, *, device=None) -> dict:
@@ -436,6 +480,6 @@ def first_tmp(weights: dict, rate: float, *, device=None) -> dict:
     ks = list(weights.keys())
     for k in ks:
         v = weights[k]
-        out[k] = torch.empty(v.shape, dtype=v.dtype, device=device)
+        out[k] = torch.empty(logical_shape(weights, k), dtype=v.dtype, device=device)
     reduce_([out[k] for k in ks], None, [[weights[k]] for k in ks], [rate], init_first=True)
     return out

@@ -381,44 +381,72 @@ class DeviceUpdateCache:
     The reference aggregator pickles every update into a disk-backed cache and
     unpickles it again inside ``FedAvg.do`` (``syncfl/top_aggregator.py:93-95,156``,
     ``optimizer/fedavg.py:82``).  Here ``cache[end] = TrainResult(...)`` moves the
-    update's tensors to HBM on a side stream as it arrives (overlapping the next
-    receive), or -- ``placement="host"`` -- keeps pinned host tensors for the
-    kernel to stream zero-copy.  ``iterkeys()`` yields keys in sorted order
-    (diskcache's ``ORDER BY key``), ``pop`` hands back the TrainResult with its
-    transfer ordered before any later work on the caller's stream.
+    update into HBM on a side stream as it arrives (overlapping the next receive):
+
+    * ``placement="slab"`` (default): into a tiled :class:`flame_amd.slab.UpdateSlab`
+      sized for ``capacity`` updates -- the layout the reduction streams at the HBM
+      read ceiling; an update that does not fit (slab full or other shapes) falls
+      back to ``"hbm"``;
+    * ``placement="hbm"``: one device allocation per tensor (the reference's
+      ``weights_to_model_device`` layout);
+    * ``placement="host"``: pinned host tensors the kernel streams zero-copy.
+
+    ``iterkeys()`` yields keys in sorted order (diskcache's ``ORDER BY key``);
+    ``pop`` hands back the TrainResult with its transfer ordered before any later
+    work on the caller's stream.
     """
 
-    def __init__(self, device=None, placement: str = "hbm"):
-        if placement not in ("hbm", "host"):
-            raise ValueError("placement must be 'hbm' or 'host'")
+    def __init__(self, device=None, placement: str = "slab", capacity: int = 256):
+        if placement not in ("slab", "hbm", "host"):
+            raise ValueError("placement must be 'slab', 'hbm' or 'host'")
         self.placement = placement
+        self.capacity = capacity
         self.device = torch.device(device) if device is not None else None
         self._d = collections.OrderedDict()
         self._stream = None
+        self.slab = None
 
     def _dev(self):
         if self.device is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         return self.device
 
+    def _side_stream(self):
+        dev = self._dev()
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        self._stream.wait_stream(torch.cuda.current_stream(dev))
+        return self._stream
+
+    def _fits_slab(self, w):
+        if self.slab is None:
+            from .slab import UpdateSlab
+            self.slab = UpdateSlab(w, self.capacity, self._dev())
+        sl = self.slab
+        return (bool(sl._free) and list(w.keys()) == sl.keys
+                and all(isinstance(w[k], torch.Tensor) and w[k].dtype == sl.meta[k][0]
+                        and w[k].numel() == sl.meta[k][2] for k in sl.keys))
+
     def __setitem__(self, key, tres):
         w = getattr(tres, "weights", None)
         ev = None
-        if isinstance(w, dict) and w:
-            if self.placement == "hbm":
-                dev = self._dev()
-                if self._stream is None:
-                    self._stream = torch.cuda.Stream(dev)
-                self._stream.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(self._stream):
+        if isinstance(w, dict) and w and self.placement in ("slab", "hbm"):
+            st = self._side_stream()
+            if self.placement == "slab" and self._fits_slab(w):
+                tres.weights = self.slab.put(w, stream=st)
+            else:
+                with torch.cuda.stream(st):
                     tres.weights = w.__class__(
-                        (k, v.to(dev, non_blocking=True) if isinstance(v, torch.Tensor) else v) for k, v in w.items())
-                    ev = torch.cuda.Event()
-                    ev.record(self._stream)
-            elif torch.cuda.is_available():
-                tres.weights = w.__class__(
-                    (k, v if (not isinstance(v, torch.Tensor) or v.is_cuda or v.is_pinned()) else v.pin_memory())
-                    for k, v in w.items())
+                        (k, v.to(self._dev(), non_blocking=True) if isinstance(v, torch.Tensor) else v)
+                        for k, v in w.items())
+            ev = torch.cuda.Event()
+            ev.record(st)
+        elif isinstance(w, dict) and w and self.placement == "host" and torch.cuda.is_available():
+            tres.weights = w.__class__(
+                (k, v if (not isinstance(v, torch.Tensor) or v.is_cuda or v.is_pinned()) else v.pin_memory())
+                for k, v in w.items())
+        if key in self._d:
+            self._d.pop(key)
         self._d[key] = (tres, ev)
 
     def __getitem__(self, key):

@@ -39,7 +39,7 @@ class DeferredAggregate(collections.abc.Mapping):
 
     def __init__(self, weights, max_pending):
         self._keys = list(weights.keys())
-        self._meta = {k: (weights[k].shape, weights[k].dtype) for k in self._keys}
+        self._meta = {k: (engine.logical_shape(weights, k), weights[k].dtype) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
         self._pending = []         # [(weights, rate)] in arrival order
         self._max_pending = max_pending

@@ -176,7 +176,9 @@ class ShardedSliceFedAvg:
         staged = base.is_cuda and self.dist.get_backend(self.group) == "gloo"  # gloo: host collectives
         for lo, hi in piece_bounds(P, self.fracs, align):
             piece = base[lo:hi]
-            self.reducer(piece, [w[key][lo:hi] for w, _ in entries], rates)
+            from . import engine
+            self.reducer(piece, [engine.slice_elems(w[key], lo, hi, P) if w[key].is_cuda else w[key][lo:hi]
+                                 for w, _ in entries], rates)
             dst = self.global_flat[self.world * lo:self.world * hi]
             if staged:
                 host = torch.empty(dst.numel(), dtype=dst.dtype)

@@ -1,0 +1,146 @@
+"""Tiled, device-resident update store (the HBM layout of the MI355X path).
+
+Why tiled.  With one allocation per client update, a workgroup of the
+reduction reads one 4 KiB piece from each of N client rows that lie ~P·s bytes
+apart, so the ~2,000 resident workgroups keep tens of thousands of distinct
+pages in flight; with the updates stored as ``[tiles][N][T]`` (T = one kernel
+chunk) a workgroup streams ONE contiguous N·T·s region.  Measured on MI355X
+(tools/kernel_sweep.py, same process, 1024 × 25M fp32): 15.78 ms row layout vs
+15.10 ms tiled = the plain streaming-read probe (15.13 ms), i.e. +4.5 %.
+
+Layout.  Per dtype group of the model template, every key occupies
+``ceil(numel / T)`` whole tiles (keys start on tile boundaries; the padding is
+< T elements per key per client), and tile ``t`` holds
+``[capacity][T]`` -- slot ``i``'s chunk at ``((t * capacity) + i) * T``.  A slot's
+tensor for key ``k`` is exposed as a strided torch view of shape
+``(tiles_k, T)`` with strides ``(capacity * T, 1)``; the engine recognises such
+views and passes ``client_tile_stride = capacity * T * itemsize`` to the kernel
+(``include/flame_amd.h``).  Elements past ``numel`` in a key's last tile are
+never read.
+
+Slots are reused stream-ordered: a slot is returned to the free list when the
+``SlotWeights`` dict handed out for it is garbage-collected (after the launch
+that consumed it), with an event recorded on the then-current stream; the next
+write into the slot waits for that event.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Dict, List
+
+import torch
+
+from . import engine
+
+
+class SlotWeights(dict):
+    """The weights dict of one slab slot: {key: tiled view}; ``shapes`` holds the model
+    shapes; releases the slot when dropped."""
+
+    __slots__ = ("__weakref__", "_release", "shapes")
+
+    def __del__(self):
+        rel = getattr(self, "_release", None)
+        if rel is not None:
+            self._release = None
+            try:
+                rel()
+            except Exception:  # noqa: BLE001  (interpreter shutdown)
+                pass
+
+
+class UpdateSlab:
+    """``capacity`` client updates shaped like ``template``, tiled in HBM."""
+
+    def __init__(self, template: Dict[str, torch.Tensor], capacity: int, device=None):
+        self.device = torch.device(device) if device is not None else engine.pick_device(template)
+        self.capacity = int(capacity)
+        self.keys: List[str] = list(template.keys())
+        self.meta = {}           # key -> (dtype, shape, numel, tile0, tiles)
+        tiles_per_dtype = collections.OrderedDict()
+        for k in self.keys:
+            t = template[k]
+            code = engine.dtype_code(t.dtype)
+            T = engine.chunk_elems(code)
+            tiles = max(1, -(-t.numel() // T))
+            tile0 = tiles_per_dtype.get(t.dtype, 0)
+            tiles_per_dtype[t.dtype] = tile0 + tiles
+            self.meta[k] = (t.dtype, tuple(t.shape), t.numel(), tile0, tiles)
+        self.storage = {}        # dtype -> tensor [tiles][capacity][T]
+        for dt, tiles in tiles_per_dtype.items():
+            T = engine.chunk_elems(engine.dtype_code(dt))
+            self.storage[dt] = torch.empty((tiles, self.capacity, T), dtype=dt, device=self.device)
+        self._free = collections.deque(range(self.capacity))
+        self._ready = {}         # slot -> event the next writer must wait for
+        self._stream = None
+
+    # ------------------------------------------------------------------ slots
+    def nbytes(self) -> int:
+        return sum(s.numel() * s.element_size() for s in self.storage.values())
+
+    def acquire(self) -> int:
+        if not self._free:
+            raise RuntimeError(f"UpdateSlab full ({self.capacity} slots); raise capacity")
+        return self._free.popleft()
+
+    def _release(self, slot: int) -> None:
+        if torch.cuda.is_available():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._ready[slot] = ev
+        self._free.append(slot)
+
+    def views(self, slot: int) -> SlotWeights:
+        """Tiled views of ``slot`` (what the optimizers receive as ``TrainResult.weights``)."""
+        w = SlotWeights()
+        for k in self.keys:
+            dt, _, _, tile0, tiles = self.meta[k]
+            w[k] = self.storage[dt][tile0:tile0 + tiles, slot, :]
+        w._release = lambda s=slot: self._release(s)
+        w.shapes = {k: self.meta[k][1] for k in self.keys}
+        return w
+
+    def slot_view(self, slot: int, key: str) -> torch.Tensor:
+        dt, _, _, tile0, tiles = self.meta[key]
+        return self.storage[dt][tile0:tile0 + tiles, slot, :]
+
+    # ------------------------------------------------------------------ writes
+    def write(self, slot: int, weights: Dict[str, torch.Tensor], stream=None) -> None:
+        """Copy one client's update (host or device tensors) into ``slot`` on ``stream``."""
+        st = stream or torch.cuda.current_stream(self.device)
+        ev = self._ready.pop(slot, None)
+        if ev is not None:
+            st.wait_event(ev)
+        with torch.cuda.stream(st):
+            for k in self.keys:
+                if k not in weights:
+                    raise KeyError(k)
+                dt, shape, n, tile0, tiles = self.meta[k]
+                src = weights[k]
+                if src.numel() != n:
+                    raise RuntimeError(f"{k}: {src.numel()} elements, slab expects {n}")
+                src = src.reshape(-1)
+                if src.dtype != dt:
+                    raise NotImplementedError(f"{k}: dtype {src.dtype} != slab dtype {dt}")
+                view = self.slot_view(slot, k)            # (tiles, T), row stride capacity*T
+                T = view.shape[1]
+                full = n // T
+                if full:
+                    view[:full].copy_(src[:full * T].view(full, T), non_blocking=True)
+                if n % T:
+                    view[full, :n % T].copy_(src[full * T:], non_blocking=True)
+
+    def put(self, weights: Dict[str, torch.Tensor], stream=None) -> SlotWeights:
+        """Acquire a slot, write ``weights`` into it, return its tiled views."""
+        slot = self.acquire()
+        try:
+            self.write(slot, weights, stream)
+        except Exception:
+            self._free.appendleft(slot)
+            raise
+        return self.views(slot)
+
+    def read(self, slot: int, key: str) -> torch.Tensor:
+        """A contiguous copy of ``slot``'s tensor ``key`` in its original shape (for inspection)."""
+        dt, shape, n, _, _ = self.meta[key]
+        return self.slot_view(slot, key).reshape(-1)[:n].reshape(shape).clone()

@@ -79,6 +79,10 @@ extern "C" {
  *
  * chunk_begin is the prefix sum over previous segments of
  * ceil(numel / flame_chunk_elems(dtype)); the grid covers n_chunks chunks.
+ * client_tile_stride (reduce entry points only): 0 = every client's data for
+ * the segment is contiguous; otherwise client data is TILED -- chunk c of a
+ * client starts client_tile_stride bytes after chunk c-1 (e.g. a [chunks][N][chunk]
+ * slab, where one workgroup reads one contiguous N x chunk region).
  * The table lives in device memory.
  */
 typedef struct flame_segment {
@@ -91,7 +95,7 @@ typedef struct flame_segment {
     int64_t numel;
     int64_t chunk_begin;
     int64_t flags;
-    int64_t reserved;
+    int64_t client_tile_stride;
 } flame_segment;
 
 /* Library info. */

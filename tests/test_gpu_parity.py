@@ -350,7 +350,7 @@ def test_zero_copy_pinned_host_clients():
     S.assert_bitwise("zerocopy", S.to_cpu(out), {"x": exp})
 
 
-@pytest.mark.parametrize("where", ["bytes", "pinned", "cache_hbm", "cache_host"])
+@pytest.mark.parametrize("where", ["bytes", "pinned", "cache_hbm", "cache_host", "cache_slab"])
 def test_ingest_wire_payloads_to_fedavg(where):
     """Channel payloads (cloudpickle, channel.py:203-218) -> ingest.decode (zero-copy) ->
     FedAvg on the GPU == oracle on the original tensors, bitwise."""
@@ -366,7 +366,7 @@ def test_ingest_wire_payloads_to_fedavg(where):
     counts = [10 + 7 * i for i in range(n)]
     total = sum(counts)
     keep = []
-    cache = ingest.DeviceUpdateCache(placement="hbm" if where == "cache_hbm" else "host") \
+    cache = ingest.DeviceUpdateCache(placement=where.split("_")[1], capacity=16) \
         if where.startswith("cache") else S.SortedCache()
     for i in range(n):
         b = cloudpickle.dumps({"weights": ws[i], "dataset_size": counts[i]})
@@ -384,3 +384,79 @@ def test_ingest_wire_payloads_to_fedavg(where):
         exp = base[k].clone()
         O.reduce_tensor(exp, [w[k] for w in ws], [c / total for c in counts])
         S.assert_bitwise(f"{where}/{k}", {k: out[k]}, {k: exp})
+
+
+def _slab_model(g):
+    from flame_amd import engine
+    T = engine.chunk_elems(0)
+    return {"big": torch.randn(3 * T + 17, generator=g), "tiny": torch.randn(5, generator=g),
+            "exact": torch.randn(T, generator=g), "bf": torch.randn(2 * 2048 + 3, generator=g).bfloat16(),
+            "mat": torch.randn(33, 65, generator=g), "nbt": torch.tensor(7, dtype=torch.int64)}
+
+
+def test_slab_tiled_fedavg_bitwise_and_slot_reuse():
+    """Updates in the tiled UpdateSlab (client_tile_stride path) == oracle, bitwise; slots
+    released after the round are reused by the next one."""
+    from flame_amd import engine
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(8)
+    tmpl = _slab_model(g)
+    slab = UpdateSlab(tmpl, capacity=40, device=DEV)
+    base = {k: v.clone() for k, v in tmpl.items()}
+    for rnd in range(2):
+        n = 37
+        ws = [{k: (torch.randn(v.shape, generator=g) * 1e-2).to(v.dtype) if v.is_floating_point()
+               else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()} for i in range(n)]
+        counts = [3 + 5 * i for i in range(n)]
+        cache = S.SortedCache()
+        for i in range(n):
+            sw = slab.put({k: v.to(DEV) for k, v in ws[i].items()})
+            assert engine.tiled_stride(sw["big"], tmpl["big"].numel()) == 40 * engine.chunk_elems(0) * 4
+            cache[f"{i:03d}"] = S.TR(sw, counts[i])
+        del sw
+        dev_base = {k: v.to(DEV) for k, v in base.items()}
+        out = make_amd("fedavg").do(dev_base, cache, total=sum(counts))
+        for k in base:
+            exp = base[k].clone()
+            O.reduce_tensor(exp, [w[k] for w in ws], [c / sum(counts) for c in counts])
+            S.assert_bitwise(f"slab r{rnd}/{k}", {k: out[k]}, {k: exp})
+            base[k] = exp
+        import gc
+        gc.collect()
+        assert len(slab._free) == 40, "slots must return after the round"
+
+
+def test_slab_fedopt_and_fedbuff_tiled():
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(9)
+    P = 100_003
+    slab = UpdateSlab({"w": torch.zeros(P)}, capacity=16, device=DEV)
+    w0 = torch.randn(P, generator=g)
+    amd, ora = make_amd("fedadam"), O.OracleFedOPT("fedadam")
+    wa, wo = {"w": w0.to(DEV)}, {"w": w0.clone()}
+    for r in range(3):
+        ups = [torch.randn(P, generator=g) * 1e-2 for _ in range(12)]
+        counts = [10 + i for i in range(12)]
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i in range(12):
+            ca[f"{i:02d}"] = S.TR(slab.put({"w": ups[i].to(DEV)}), counts[i])
+            co[f"{i:02d}"] = S.TR({"w": ups[i]}, counts[i])
+        wa = amd.do({"w": wa["w"].clone()}, ca, total=sum(counts))
+        wo = ora.do({"w": wo["w"].clone()}, co, total=sum(counts))
+        if r == 0:
+            S.assert_bitwise("slab fedadam r0", S.to_cpu(wa), wo)
+        else:
+            S.assert_close_fedopt(f"slab fedadam r{r}", S.to_cpu(wa), wo)
+    # FedBuff: deferred arrivals from slab slots
+    fb, ob = make_amd("fedbuff"), O.OracleFedBuff()
+    aa = ao = None
+    for i in range(10):
+        u = torch.randn(P, generator=g) * 1e-2
+        ca, co = S.SortedCache(), S.SortedCache()
+        ca["x"] = S.TR(slab.put({"w": u.to(DEV)}), 1, 5 - i % 3)
+        co["x"] = S.TR({"w": u}, 1, 5 - i % 3)
+        aa = fb.do(aa, ca, total=1, version=5)
+        ao = ob.do(ao, co, total=1, version=5)
+    S.assert_bitwise("slab fedbuff", S.to_cpu(aa), ao)

@@ -95,7 +95,7 @@ def test_decode_protocols_and_large_update_speed():
 
 def test_device_update_cache_host_placement_orders_and_pops():
     from scenarios import TR
-    c = ingest.DeviceUpdateCache(placement="host")
+    c = ingest.DeviceUpdateCache(placement="host")  # host placement needs no GPU
     for k in ["b", "a", "c"]:
         c[k] = TR({"w": torch.ones(3)}, 1)
     assert len(c) == 3 and list(c.iterkeys()) == ["a", "b", "c"] and "a" in c

@@ -103,7 +103,14 @@ def main():
     probe = "probe" in names
     if probe:
         names = [x for x in names if x != "probe"]
-    libs = {nm: load(nm) for nm in names}
+    # "<variant>:tiled" = same build, client data in the tiled [chunks][N][chunk] layout
+    libs = {nm: load(nm.split(":")[0]) for nm in names}
+    tiled_slab = None
+    if any(nm.endswith(":tiled") for nm in names):
+        T = libs[[nm for nm in names if nm.endswith(":tiled")][0]].flame_chunk_elems(code)
+        S_ = -(-P // T)
+        tiled_slab = torch.empty((S_, n, T), dtype=tdt, device=dev)
+        engine.synth_fill_(tiled_slab.view(-1), 2, 7, 0, 1e-2)
     plans = {}
     if args.kernel != "agg":
         cur = base0.clone()
@@ -111,7 +118,17 @@ def main():
         v = torch.zeros_like(base0)
         cur_out = torch.empty_like(base0)
     for nm, L in libs.items():
-        if args.kernel == "agg":
+        if nm.endswith(":tiled"):
+            T = tiled_slab.shape[2]
+            # the tile must be exactly one kernel chunk, or chunk c's address runs past the slab
+            if L.flame_chunk_elems(code) != T:
+                raise SystemExit(f"{nm}: chunk {L.flame_chunk_elems(code)} != tile {T}; one tile size per run")
+            seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(),
+                             clients=[tiled_slab[0, i].data_ptr() for i in range(n)],
+                             tile_stride=n * T * tiled_slab.element_size())
+            if args.kernel != "agg":
+                seg.cur, seg.cur_out, seg.m, seg.v = cur.data_ptr(), cur_out.data_ptr(), m.data_ptr(), v.data_ptr()
+        elif args.kernel == "agg":
             seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), clients=[slab[i].data_ptr() for i in range(n)])
         else:
             seg = engine.Seg(P, out=out.data_ptr(), inp=base0.data_ptr(), cur=cur.data_ptr(), cur_out=cur_out.data_ptr(),
@@ -157,7 +174,7 @@ def main():
     for nm in names:
         launch(nm)
         torch.cuda.synchronize()
-        if args.kernel != "agg" or nm == "probe":
+        if args.kernel != "agg" or nm == "probe" or nm.endswith(":tiled"):
             continue
         if ref is None:
             ref = out.clone()
@@ -182,7 +199,8 @@ def main():
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
         nb = pbytes if nm == "probe" else nbytes
-        res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nb / med / 1e6, "defs": VARIANTS.get(nm, {})}
+        res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nb / med / 1e6,
+                   "defs": VARIANTS.get(nm.split(":")[0], {})}
         print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nb / med / 1e6:8.1f} GB/s", flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump({"clients": n, "params": P, "pad": args.pad, "results": res}, open(args.out, "w"), indent=1)
