@@ -270,7 +270,8 @@ def main():
         traffic = None
         try:
             tr = json.load(open(args.traffic))
-            if tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P:
+            if (tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P
+                    and tr.get("layout", "row") == args.layout):
                 traffic = tr["hbm_bytes_per_launch"]
         except Exception:  # noqa: BLE001
             pass
@@ -332,9 +333,14 @@ def bench_hier(args, world, rank, dev):
     C = (args.clients or 4096) // M
     P = args.params or 125_000_000 // 8
     dt = torch.bfloat16
-    slab = torch.empty((M * C, P), dtype=dt, device=dev)
+    from flame_amd.slab import UpdateSlab
+    store = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M * C, device=dev)
+    tmp = torch.empty(P, dtype=dt, device=dev)
+    client_w = []
     for i in range(M * C):
-        engine.synth_fill_(slab[i], args.seed + 4, 1 + i + rank * 100_000, 0, 1e-2)
+        engine.synth_fill_(tmp, args.seed + 4, 1 + i + rank * 100_000, 0, 1e-2)
+        client_w.append(store.put({"model": tmp}))
+    del tmp
     gw = torch.empty(P, dtype=dt, device=dev)
     engine.synth_fill_(gw, args.seed + 4, rank * 100_000, 0, 1.0)
     mids = [gw.clone() for _ in range(M)]
@@ -353,7 +359,7 @@ def bench_hier(args, world, rank, dev):
             for t in range(C):
                 i = m * C + t
                 cache = Cache()
-                cache[f"{i:05d}"] = TR({"model": slab[i]}, 1, rnd - stale[i])
+                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
                 agg = opt.do(agg, cache, total=1, version=rnd)
             _, delta = opt.scale_add_agg_weights_with_delta({"model": mids[m]}, agg, C)
             deltas.append(delta)

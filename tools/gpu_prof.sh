@@ -13,4 +13,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
       -d $OUT/pmc_$C -o run -- python bench.py --steps 3 --warmup 1 --cpu-clients 0 ${BENCH_ARGS:-} > $OUT/pmc_$C.log 2>&1 \
       || { echo "pmc $C rc=$?"; tail -5 $OUT/pmc_$C.log; exit 1; }
 done
-python tools/pmc_traffic.py --fetch $OUT/pmc_FETCH_SIZE --write $OUT/pmc_WRITE_SIZE --out $OUT/traffic.json
+python tools/pmc_traffic.py --fetch $OUT/pmc_FETCH_SIZE --write $OUT/pmc_WRITE_SIZE --layout slab --out $OUT/traffic.json

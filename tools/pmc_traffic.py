@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--clients", type=int, default=1024)
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--out", default="profiles/traffic.json")
+    ap.add_argument("--layout", default="slab")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -47,7 +48,7 @@ def main():
     write_b = w_kb * 1024
     algo = (a.clients + 2) * a.params * 4
     res = {
-        "kernel": a.name, "clients": a.clients, "params": a.params,
+        "kernel": a.name, "clients": a.clients, "params": a.params, "layout": a.layout,
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb, "dispatches": [len(fetch), len(write)],
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
