@@ -269,10 +269,11 @@ def main():
     if rank == 0:
         traffic = None
         try:
-            tr = json.load(open(args.traffic))
-            if (tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P
-                    and tr.get("layout", "row") == args.layout):
-                traffic = tr["hbm_bytes_per_launch"]
+            doc = json.load(open(args.traffic))
+            for tr in (doc["entries"] if "entries" in doc else [doc]):
+                if (tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P
+                        and tr.get("layout", "row") == args.layout):
+                    traffic = tr["hbm_bytes_per_launch"]
         except Exception:  # noqa: BLE001
             pass
         cpu = None

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--layout", default="slab")
+    ap.add_argument("--extra-arrays", type=int, default=2,
+                    help="P-sized arrays besides the N clients in the algorithmic bytes (FedAvg 2, FedOPT 8)")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -46,7 +48,7 @@ def main():
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     read_b = 2.0 * f_kb * 1024
     write_b = w_kb * 1024
-    algo = (a.clients + 2) * a.params * 4
+    algo = (a.clients + a.extra_arrays) * a.params * 4
     res = {
         "kernel": a.name, "clients": a.clients, "params": a.params, "layout": a.layout,
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb, "dispatches": [len(fetch), len(write)],
@@ -57,7 +59,15 @@ def main():
         "correction": "read = 2*FETCH_SIZE KiB (gfx950 half-count on 16B/lane streams), write = WRITE_SIZE KiB",
     }
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
-    json.dump(res, open(a.out, "w"), indent=1)
+    # the file holds one entry per (kernel, clients, params, layout); replace ours
+    try:
+        doc = json.load(open(a.out))
+        entries = doc["entries"] if "entries" in doc else [doc]
+    except Exception:  # noqa: BLE001
+        entries = []
+    key = lambda e: (e.get("kernel"), e.get("clients"), e.get("params"), e.get("layout", "row"))  # noqa: E731
+    entries = [e for e in entries if key(e) != key(res)] + [res]
+    json.dump({"entries": entries}, open(a.out, "w"), indent=1)
     print(json.dumps(res))
 
 
