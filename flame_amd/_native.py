@@ -24,6 +24,7 @@ SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
     "flame_agg_reduce", "flame_fedopt_reduce_adapt", "flame_fedbuff_scale_add", "flame_synth_fill",
+    "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
 )
 
 
@@ -62,6 +63,12 @@ def lib() -> ctypes.CDLL:
     L.flame_fedbuff_scale_add.argtypes = [ctypes.c_int, vp, i32, i64, i64, vp]
     L.flame_synth_fill.restype = ctypes.c_int
     L.flame_synth_fill.argtypes = [ctypes.c_int, vp, i64, u64, u64, i64, f32, vp]
+    L.flame_host_register.restype = ctypes.c_int
+    L.flame_host_register.argtypes = [vp, u64]
+    L.flame_host_unregister.restype = ctypes.c_int
+    L.flame_host_unregister.argtypes = [vp]
+    L.flame_host_device_pointer.restype = ctypes.c_int
+    L.flame_host_device_pointer.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p)]
     if L.flame_abi_version() != 1:
         raise ImportError(f"flame_amd ABI mismatch: library {L.flame_abi_version()} != 1")
     _lib = L

@@ -696,6 +696,27 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs
     return check_launch("flame_fedbuff_scale_add");
 }
 
+int flame_host_register(void* host, uint64_t nbytes) {
+    if (!host || nbytes == 0) return set_err(FLAME_EINVAL, "flame_host_register: empty range");
+    hipError_t e = hipHostRegister(host, static_cast<size_t>(nbytes), hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) return set_err(FLAME_EHIP, "hipHostRegister: %s", hipGetErrorString(e));
+    return FLAME_OK;
+}
+
+int flame_host_unregister(void* host) {
+    if (!host) return set_err(FLAME_EINVAL, "flame_host_unregister: NULL");
+    hipError_t e = hipHostUnregister(host);
+    if (e != hipSuccess) return set_err(FLAME_EHIP, "hipHostUnregister: %s", hipGetErrorString(e));
+    return FLAME_OK;
+}
+
+int flame_host_device_pointer(void* host, void** device) {
+    if (!host || !device) return set_err(FLAME_EINVAL, "flame_host_device_pointer: NULL");
+    hipError_t e = hipHostGetDevicePointer(device, host, 0);
+    if (e != hipSuccess) return set_err(FLAME_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    return FLAME_OK;
+}
+
 int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_t stream_id, int64_t start,
                      float scale, void* stream) {
     if (numel < 0 || (numel > 0 && !out)) return set_err(FLAME_EINVAL, "flame_synth_fill: bad buffer");

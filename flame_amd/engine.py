@@ -1,8 +1,9 @@
 """Host side of the drop-in path: turns state_dict tensors into segment tables
 and launches the native kernels (``include/flame_amd.h``) on torch's current stream.
 
-Pure-Python planning (``plan_*``, ``rate32``, ``chunk_elems``) needs no GPU and
-is unit-tested on CPU; ``launch_*`` need the native library and a HIP device.
+Pure-Python planning (``plan``, ``rate32``, ``chunk_elems``) needs no GPU and is
+unit-tested on CPU; the launchers (``reduce_``, ``fedopt_reduce_adapt_``,
+``scale_add_``, ``synth_fill_``) need the native library and a HIP device.
 
 A *segment* is one contiguous tensor (one state_dict entry).  For a reduction,
 row ``s`` of the client table holds, in cache.iterkeys() order, the device
@@ -12,6 +13,8 @@ segments of one dtype, so a whole model aggregates in one kernel per dtype.
 from __future__ import annotations
 
 import collections
+import ctypes
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -138,6 +141,12 @@ class _Staging:
         self._inflight.append((ev, host))
         return dev
 
+    def drain(self) -> None:
+        """Wait for every in-flight staging copy / zero-copy read and drop the host refs."""
+        while self._inflight:
+            ev, _ = self._inflight.popleft()
+            ev.synchronize()
+
     def hold(self, host_tensor: torch.Tensor, device) -> None:
         """Keep a host tensor a kernel reads directly alive until the stream passes this point."""
         ev = torch.cuda.Event()
@@ -195,8 +204,7 @@ def _device_ptrs(dev_meta: torch.Tensor, p: Plan):
 # Zero-copy ingest: a pinned (hipHostMalloc'd) host tensor is device-addressable, so the
 # kernel can stream client updates straight from host memory over PCIe instead of
 # staging them into HBM first (FLAME_AMD_ZERO_COPY=0 disables).
-import os as _os  # noqa: E402
-ZERO_COPY_PINNED = _os.environ.get("FLAME_AMD_ZERO_COPY", "1") != "0"
+ZERO_COPY_PINNED = os.environ.get("FLAME_AMD_ZERO_COPY", "1") != "0"
 
 
 def _as_device(t: torch.Tensor, device) -> torch.Tensor:
@@ -252,8 +260,15 @@ def _client_row(cs, o: torch.Tensor, device, keep):
             raise RuntimeError(f"flame_amd: client tensor has {c.numel()} elements, aggregate {n}")
         c = _as_device(c, device)
         keep.append(c)
-        row.append(c.data_ptr())
+        row.append(c.data_ptr() if c.is_cuda else host_device_pointer(c.data_ptr()))
     return row, 0
+
+
+def host_device_pointer(host_ptr: int) -> int:
+    """Device address of a pinned / hipHostRegister-ed host address (zero-copy reads)."""
+    out = ctypes.c_void_p()
+    N.check(N.lib().flame_host_device_pointer(host_ptr, ctypes.byref(out)))
+    return int(out.value or 0)
 
 
 def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients: List[List[torch.Tensor]],

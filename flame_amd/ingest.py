@@ -374,6 +374,38 @@ def loads(payload):
         return cloudpickle.loads(payload)
 
 
+# ------------------------------------------------------------------ registered receive buffers
+class RegisteredBuffer:
+    """Page-lock + map a host buffer (bytearray, mmap, numpy array, shm segment) so the
+    reduction kernel can read tensors decoded from it zero-copy over PCIe
+    (``flame_host_register``).  Use as a context manager or call ``close()``."""
+
+    def __init__(self, buf):
+        import numpy as np
+        from . import _native as N
+        self.buf = buf
+        self.arr = np.frombuffer(buf, dtype=np.uint8)
+        self.ptr = self.arr.ctypes.data
+        N.check(N.lib().flame_host_register(self.ptr, self.arr.nbytes))
+        self._open = True
+
+    def close(self):
+        """Unregister after every kernel that may read the buffer has finished."""
+        if self._open:
+            from . import _native as N
+            from . import engine
+            engine._staging.drain()
+            N.check(N.lib().flame_host_unregister(self.ptr))
+            self._open = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
 # ------------------------------------------------------------------ device-resident cache
 class DeviceUpdateCache:
     """``diskcache.Cache`` stand-in that keeps received updates resident on the GPU.

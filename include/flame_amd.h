@@ -146,6 +146,19 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment *segs, int32_t n_segs
                             int64_t n_chunks, int64_t goal, void *stream);
 
 /*
+ * Host buffers the kernels read zero-copy over PCIe (ingest; flame_amd/ingest.py).
+ *   flame_host_register:   page-lock + map an existing host range (e.g. a received
+ *                          channel payload or the LIFL shared-memory segment,
+ *                          lib/python/flame/backend/shm.py:386-403) for device access.
+ *   flame_host_unregister: undo it.
+ *   flame_host_device_pointer: device address of a pinned / registered host address
+ *                          (hipHostMalloc'd memory maps to itself).
+ */
+int flame_host_register(void *host, uint64_t nbytes);
+int flame_host_unregister(void *host);
+int flame_host_device_pointer(void *host, void **device);
+
+/*
  * Fill out[0..numel) with the counter-based generator of flame_amd/synth.py:
  *   value_f32(seed, stream_id, start + j) * scale, rounded RNE to `dtype`
  *   (FLAME_F32 / FLAME_BF16 / FLAME_F16).  `out` is a device pointer.

@@ -460,3 +460,37 @@ def test_slab_fedopt_and_fedbuff_tiled():
         aa = fb.do(aa, ca, total=1, version=5)
         ao = ob.do(ao, co, total=1, version=5)
     S.assert_bitwise("slab fedbuff", S.to_cpu(aa), ao)
+
+
+def test_registered_shared_memory_payloads_zero_copy():
+    """Payloads in a registered mmap (stand-in for the LIFL shm segment) are decoded in
+    place and read by the kernel over PCIe: no host copy anywhere, result bitwise."""
+    import mmap
+    import cloudpickle
+    from flame_amd import ingest
+    O = _oracle()
+    g = torch.Generator().manual_seed(31)
+    n, P = 6, 50_021
+    ws = [{"w": torch.randn(P, generator=g) * 1e-2} for _ in range(n)]
+    blobs = [cloudpickle.dumps({"weights": w, "dataset_size": 10 + i}) for i, w in enumerate(ws)]
+    size = sum(len(b) for b in blobs)
+    mm = mmap.mmap(-1, (size + 4095) // 4096 * 4096)
+    offs, o = [], 0
+    for b in blobs:
+        mm[o:o + len(b)] = b
+        offs.append(o)
+        o += len(b)
+    with ingest.RegisteredBuffer(mm) as reg:
+        mv = memoryview(mm)
+        cache = S.SortedCache()
+        for i, (b, off) in enumerate(zip(blobs, offs)):
+            msg = ingest.decode(mv[off:off + len(b)])
+            assert msg["weights"]["w"].is_pinned()
+            cache[f"{i}"] = S.TR(msg["weights"], msg["dataset_size"])
+        base = torch.randn(P, generator=g)
+        out = make_amd("fedavg").do({"w": base.to(DEV)}, cache, total=sum(10 + i for i in range(n)))
+        torch.cuda.synchronize()
+        exp = base.clone()
+        O.reduce_tensor(exp, [w["w"] for w in ws], [(10 + i) / sum(10 + j for j in range(n)) for i in range(n)])
+        S.assert_bitwise("registered", S.to_cpu(out), {"w": exp})
+        del cache, msg
