@@ -31,6 +31,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+ISSUE_S = None  # host issue time of the timed steps (set by timed())
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
 METRIC = "aggregated params/sec (device-resident), 1024-client FedAvg @1/2/4/8 GPU"
 
@@ -137,6 +138,8 @@ def timed(world, steps, warmup, step):
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    global ISSUE_S
+    ISSUE_S = time.perf_counter() - t0   # host time to issue the steps (GPU runs behind)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -293,6 +296,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "host_issue_ms_per_step": ISSUE_S / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
