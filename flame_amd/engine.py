@@ -244,14 +244,21 @@ def _client_row(cs, o: torch.Tensor, device, keep):
     them tiled; otherwise every client is read contiguous (tiled views that are
     mixed with other layouts in one call are copied out -- rare)."""
     n = o.numel()
+    dt = o.dtype
     for c in cs:
-        if c.dtype != o.dtype:
+        if c.dtype != dt:
             raise NotImplementedError(
-                f"flame_amd: client tensor dtype {c.dtype} differs from aggregate dtype {o.dtype}")
+                f"flame_amd: client tensor dtype {c.dtype} differs from aggregate dtype {dt}")
+    if cs and cs[0].device == device:
+        ts0 = tiled_stride(cs[0], n)
+        if ts0:
+            sh, st = cs[0].shape, cs[0].stride()
+            if all(c.stride() == st and c.shape == sh and c.device == device for c in cs):
+                if ts0 == chunk_elems(dtype_code(dt)) * o.element_size():
+                    keep.extend(cs)   # ordinary contiguous (k, T) tensors: keep allocator bookkeeping
+                # else: UpdateSlab views -- the slab outlives them, slot reuse is event-guarded
+                return [c.data_ptr() for c in cs], ts0
     strides = [tiled_stride(c, n) if c.device == device else 0 for c in cs]
-    if cs and strides[0] and all(t == strides[0] for t in strides):
-        keep.extend(cs)
-        return [c.data_ptr() for c in cs], strides[0]
     row = []
     for c, ts in zip(cs, strides):
         if ts:

@@ -61,8 +61,19 @@ def _cpu(t):
 def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
     """acc (CPU, contiguous) += Σ_i round(v_i * rate_i), sequential in list order (in place)."""
     assert acc.is_contiguous() and acc.device.type == "cpu"
+    if any(c.dtype != acc.dtype for c in clients):
+        # fedavg.py:93-104 with v.dtype != agg.dtype: tmp = (v*rate).to(v.dtype), then
+        # agg += tmp in promote_types(agg, tmp) (legal in place only if that is agg's dtype)
+        for c, r in zip(clients, rates):
+            c = _cpu(c)
+            if torch.promote_types(acc.dtype, c.dtype) != acc.dtype:
+                raise RuntimeError("result type can't be cast to the desired output type")
+            tmp = torch.empty(acc.shape, dtype=c.dtype)
+            reduce_tensor(tmp, [c], [r], init_first=True)
+            reduce_tensor(acc, [tmp.to(acc.dtype)], [1.0])
+        return
     n = len(clients)
-    cl = [_cpu(c).to(acc.dtype) if c.dtype != acc.dtype else _cpu(c) for c in clients]
+    cl = [_cpu(c) for c in clients]
     ptrs = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in cl])
     r32 = np.asarray([np.float32(r) for r in rates] or [0], dtype=np.float32)
     r64 = np.asarray([float(r) for r in rates] or [0], dtype=np.float64)
@@ -90,6 +101,9 @@ def fedopt_scalars(beta_1, beta_2, eta, tau):
 
 def adapt_tensor(sort, avg, cur, m, v, hyper):
     """Returns new cur; m and v (CPU fp32 contiguous) are updated in place."""
+    for t in (avg, cur, m, v):
+        if t.dtype != torch.float32:
+            raise TypeError("adapt_tensor: fp32 only (non-fp32 keys use the torch op sequence)")
     out = torch.empty_like(cur)
     lib().flame_oracle_fedopt_adapt(VARIANT[sort], _cpu(avg).data_ptr(), _cpu(cur).data_ptr(),
                                     m.data_ptr(), v.data_ptr(), out.data_ptr(), cur.numel(),
@@ -130,6 +144,7 @@ class OracleFedOPT(OracleFedAvg):
     def __init__(self, sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3):
         super().__init__()
         self.sort = sort
+        self.beta_1, self.beta_2, self.eta, self.tau = beta_1, beta_2, eta, tau
         self.hyper = fedopt_scalars(beta_1, beta_2, eta, tau)
         self.current_weights = None
         self.m_t = None
@@ -143,14 +158,37 @@ class OracleFedOPT(OracleFedAvg):
             self.current_weights = self.agg_weights
             return self.current_weights
         avg, cur = self.agg_weights, self.current_weights
-        if self.m_t is None:
-            self.m_t = {k: torch.zeros_like(avg[k], dtype=torch.float32) for k in avg}
-        if self.v_t is None:
-            self.v_t = {k: torch.zeros_like(avg[k], dtype=torch.float32) for k in avg}
-        self.current_weights = OrderedDict(
-            (k, adapt_tensor(self.sort, avg[k], cur[k], self.m_t[k], self.v_t[k], self.hyper))
-            for k in cur.keys())
+        first = self.m_t is None
+        if first:
+            self.m_t, self.v_t = {}, {}
+        new = OrderedDict()
+        for k in cur.keys():
+            if avg[k].dtype == torch.float32 and cur[k].dtype == torch.float32:
+                if first:
+                    self.m_t[k] = torch.zeros_like(avg[k])
+                    self.v_t[k] = torch.zeros_like(avg[k])
+                new[k] = adapt_tensor(self.sort, avg[k], cur[k], self.m_t[k], self.v_t[k], self.hyper)
+            else:
+                new[k] = self._adapt_torch(k, avg[k], cur[k], first)
+        self.current_weights = new
         return self.current_weights
+
+    def _adapt_torch(self, k, avg, cur, first):
+        """Non-fp32 keys: the reference's own torch op sequence (fedopt.py:106-129 and the
+        _delta_v variants), which carries its dtype promotions (int64 -> fp32, bf16 rounding)."""
+        b1, b2, eta, tau = self.beta_1, self.beta_2, self.eta, self.tau
+        d = avg - cur
+        m = torch.zeros_like(d) if first else self.m_t[k]
+        m = b1 * m + (1 - b1) * d
+        v = torch.zeros_like(d) if first else self.v_t[k]
+        if self.sort == "fedadam":
+            v = b2 * v + (1 - b2) * d**2
+        elif self.sort == "fedyogi":
+            v = v - (1 - b2) * d**2 * torch.sign(v - d**2)
+        else:
+            v = v + d**2
+        self.m_t[k], self.v_t[k] = m, v
+        return cur + eta * m / (torch.sqrt(v) + tau)
 
 
 class OracleFedBuff:

@@ -31,9 +31,10 @@ def tensor_to_np(t):
 
 
 def np_to_tensor(a, tag):
+    a = np.array(a, copy=True, order="C")          # keeps 0-d shapes (ascontiguousarray would not)
     if tag == "bf16":
-        return torch.from_numpy(np.ascontiguousarray(a).view(np.int16).copy()).view(torch.bfloat16)
-    return torch.from_numpy(np.ascontiguousarray(a).copy())
+        return torch.from_numpy(a.view(np.int16)).view(torch.bfloat16)
+    return torch.from_numpy(a)
 
 
 def digest(a: np.ndarray) -> str:

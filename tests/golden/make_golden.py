@@ -252,6 +252,41 @@ def fedopt_rounds(sort):
     print("wrote", sort)
 
 
+def fedopt_mixed_rounds():
+    """FedAdam over a BatchNorm-like model: fp32 weights, a bf16 tensor and an int64
+    num_batches_tracked buffer (which the reference silently promotes to fp32 in the
+    adaptive step, fedopt.py:125-129)."""
+    gen = torch.Generator().manual_seed(71)
+    shapes = {"w": ((40, 30), torch.float32), "bf": ((70,), torch.bfloat16), "nbt": ((), torch.int64)}
+    weights = small_weights(gen, shapes, 1.0)
+    opt = optimizer_provider.get("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    n, rounds = 5, 4
+    fw = FixtureWriter()
+    fw.put_weights("weights0", weights)
+    all_counts = []
+    for r in range(rounds):
+        clients = [small_weights(gen, shapes, 1e-2) for _ in range(n)]
+        for i, c in enumerate(clients):
+            c["nbt"] = torch.tensor(10 * r + i, dtype=torch.int64)
+        counts = [int(x) for x in torch.randint(1, 1001, (n,), generator=gen)]
+        all_counts.append(counts)
+        cache = Cache()
+        for i, (w, c) in enumerate(zip(clients, counts)):
+            cache[f"r{r}c{i}"] = TrainResult(w, c)
+        weights = opt.do(deepcopy(weights), cache, total=sum(counts), num_trainers=n)
+        for i, w in enumerate(clients):
+            fw.put_weights(f"r{r}/client{i}", w)
+        fw.put_weights(f"r{r}/avg", opt.agg_weights)
+        fw.put_weights(f"r{r}/cur", weights)
+        if opt.m_t is not None:
+            fw.put_weights(f"r{r}/m", opt.m_t)
+            fw.put_weights(f"r{r}/v", opt.v_t)
+    fw.meta.update({"kind": "fedopt_rounds", "sort": "fedadam", "n": n, "rounds": rounds,
+                    "counts": all_counts, "beta_1": 0.9, "beta_2": 0.99, "eta": 1e-2, "tau": 1e-3})
+    fw.save(os.path.join(HERE, "fedadam_mixed_rounds.npz"))
+    print("wrote fedadam_mixed_rounds.npz")
+
+
 def hier_fedbuff_small():
     """2 middle aggregators x 3 trainers -> top FedBuff (config 5 in miniature)."""
     gen = torch.Generator().manual_seed(61)
@@ -306,6 +341,7 @@ def main():
     for s in ("fedadam", "fedyogi", "fedadagrad"):
         fedopt_rounds(s)
     hier_fedbuff_small()
+    fedopt_mixed_rounds()
 
 
 if __name__ == "__main__":

@@ -237,7 +237,7 @@ BITWISE_FIXTURES = [
     ("fedbuff_seq_bf16.npz", run_fedbuff_seq),
     ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
 ]
-FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz"]
+FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz"]
 
 
 def delta_torch(a, b):
