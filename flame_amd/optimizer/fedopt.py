@@ -136,7 +136,12 @@ class FedOPT(FedAvg):
             v = torch.zeros_like(d) if state_zero or k not in self.v_t else self.v_t[k]
             v = self._delta_v_tensor(v, d)
             self.m_t[k], self.v_t[k] = m, v
-            out[k] = current[k] + self.eta * m / (torch.sqrt(v) + self.tau)
+            sq = torch.sqrt(v)
+            # torch-CPU adds a Python scalar to a bf16/fp16 tensor after rounding the scalar
+            # to that dtype (unlike mul/div, which use it in fp32); GPU torch keeps it fp32.
+            tau = float(torch.tensor(self.tau, dtype=sq.dtype)) if sq.dtype in (torch.bfloat16, torch.float16) \
+                else self.tau
+            out[k] = current[k] + self.eta * m / (sq + tau)
         return out
 
     @abstractmethod
