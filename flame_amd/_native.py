@@ -58,7 +58,7 @@ def lib() -> ctypes.CDLL:
     L.flame_agg_reduce.restype = ctypes.c_int
     L.flame_agg_reduce.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp, vp]
     L.flame_fedopt_reduce_adapt.restype = ctypes.c_int
-    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [f32] * 6 + [vp]
+    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [f32] * 6 + [vp]
     L.flame_fedbuff_scale_add.restype = ctypes.c_int
     L.flame_fedbuff_scale_add.argtypes = [ctypes.c_int, vp, i32, i64, i64, vp]
     L.flame_synth_fill.restype = ctypes.c_int

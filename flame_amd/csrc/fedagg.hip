@@ -369,33 +369,47 @@ __device__ __forceinline__ float sign_f(float x) {  // torch.sign: NaN -> 0, -0 
     return static_cast<float>((0.0f < x) - (x < 0.0f));
 }
 
-template <int VARIANT>
-__device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float& v, float& cur_out,
-                                           float b1, float omb1, float b2, float omb2, float eta, float tau) {
-    const float d = __fsub_rn(avg, cur);
-    const float mn = __fadd_rn(__fmul_rn(b1, m), __fmul_rn(omb1, d));
-    const float d2 = __fmul_rn(d, d);
-    float vn;
-    if constexpr (VARIANT == FLAME_FEDADAM) {
-        vn = __fadd_rn(__fmul_rn(b2, v), __fmul_rn(omb2, d2));
-    } else if constexpr (VARIANT == FLAME_FEDYOGI) {
-        vn = __fsub_rn(v, __fmul_rn(__fmul_rn(omb2, d2), sign_f(__fsub_rn(v, d2))));
-    } else {
-        vn = __fadd_rn(v, d2);
-    }
-    const float q = __fdiv_rn(__fmul_rn(eta, mn), __fadd_rn(__builtin_sqrtf(vn)  /* correctly rounded (the __fsqrt_rn builtin lowers to the 1-ulp v_sqrt_f32) */, tau));
-    m = mn;
-    v = vn;
-    cur_out = __fadd_rn(cur, q);
+// Per-dtype rounding after each reference op (identity for fp32; RNE to bf16 / fp16).
+template <int DT> __device__ __forceinline__ float rnd(float x) {
+    if constexpr (DT == FLAME_BF16) return bf16_round(x);
+    else if constexpr (DT == FLAME_F16) return f16_round(x);
+    else return x;
 }
 
-template <int VARIANT, int CU>
+// One element of fedopt.py:106-129 (+ the _delta_v variants), each torch op rounded in the
+// tensor's dtype.  `tau` arrives pre-rounded to the dtype for bf16/fp16 (torch-CPU rounds a
+// Python scalar to a reduced-precision tensor's dtype before + and -, not before * and /).
+template <int DT, int VARIANT>
+__device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float& v, float& cur_out,
+                                           float b1, float omb1, float b2, float omb2, float eta, float tau) {
+    const float d = rnd<DT>(__fsub_rn(avg, cur));
+    const float mn = rnd<DT>(__fadd_rn(rnd<DT>(__fmul_rn(b1, m)), rnd<DT>(__fmul_rn(omb1, d))));
+    const float d2 = rnd<DT>(__fmul_rn(d, d));
+    float vn;
+    if constexpr (VARIANT == FLAME_FEDADAM) {
+        vn = rnd<DT>(__fadd_rn(rnd<DT>(__fmul_rn(b2, v)), rnd<DT>(__fmul_rn(omb2, d2))));
+    } else if constexpr (VARIANT == FLAME_FEDYOGI) {
+        const float t = rnd<DT>(__fmul_rn(omb2, d2));
+        vn = rnd<DT>(__fsub_rn(v, rnd<DT>(__fmul_rn(t, sign_f(rnd<DT>(__fsub_rn(v, d2)))))));
+    } else {
+        vn = rnd<DT>(__fadd_rn(v, d2));
+    }
+    // __builtin_sqrtf is correctly rounded; the __fsqrt_rn builtin lowers to the 1-ulp v_sqrt_f32
+    const float den = rnd<DT>(__fadd_rn(rnd<DT>(__builtin_sqrtf(vn)), tau));
+    const float q = rnd<DT>(__fdiv_rn(rnd<DT>(__fmul_rn(eta, mn)), den));
+    m = mn;
+    v = vn;
+    cur_out = rnd<DT>(__fadd_rn(cur, q));
+}
+
+template <int DT, int VARIANT, int CU>
 __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                         const uint64_t* __restrict__ clients, int n_clients,
                                                         const float* __restrict__ r32, unsigned flags, float b1,
                                                         float omb1, float b2, float omb2, float eta, float tau) {
-    constexpr int DT = FLAME_F32;
-    constexpr int EPT = 4;
+    using X = Tr<DT>;
+    using T = typename X::T;
+    constexpr int EPT = X::EPT;
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
@@ -407,60 +421,65 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     float acc[kVPT][EPT];
-    const float* base = reinterpret_cast<const float*>(sg.in) + e0;
-    const float* curp = reinterpret_cast<const float*>(sg.cur) + e0;
-    float* mp = reinterpret_cast<float*>(sg.m) + e0;
-    float* vp = reinterpret_cast<float*>(sg.v) + e0;
-    float* ap = reinterpret_cast<float*>(sg.out);
-    float* cop = reinterpret_cast<float*>(sg.cur_out) + e0;
+    const T* base = reinterpret_cast<const T*>(sg.in) + e0;
+    const T* curp = reinterpret_cast<const T*>(sg.cur) + e0;
+    T* mp = reinterpret_cast<T*>(sg.m) + e0;
+    T* vp = reinterpret_cast<T*>(sg.v) + e0;
+    T* ap = sg.out ? reinterpret_cast<T*>(sg.out) + e0 : nullptr;
+    T* cop = reinterpret_cast<T*>(sg.cur_out) + e0;
     if (vec) {
 #pragma unroll
-        for (int v = 0; v < kVPT; ++v) unpack<float, EPT>(ld_v(base + v * VS), acc[v]);
+        for (int v = 0; v < kVPT; ++v) {
+            T b[EPT];
+            unpack<T, EPT>(ld_v(base + v * VS), b);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) acc[v][j] = X::ld(b[j]);
+        }
 #if FLAME_OPT_PREFETCH
-        float curs[kVPT][EPT], ms[kVPT][EPT], vs[kVPT][EPT];
+        T curs[kVPT][EPT], ms[kVPT][EPT], vs[kVPT][EPT];
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
-            unpack<float, EPT>(ld_v(curp + v * VS), curs[v]);
+            unpack<T, EPT>(ld_v(curp + v * VS), curs[v]);
             if (!zero_state) {
-                unpack<float, EPT>(ld_v(mp + v * VS), ms[v]);
-                unpack<float, EPT>(ld_v(vp + v * VS), vs[v]);
+                unpack<T, EPT>(ld_v(mp + v * VS), ms[v]);
+                unpack<T, EPT>(ld_v(vp + v * VS), vs[v]);
             }
         }
 #endif
         reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
-            float cur[EPT], m[EPT], vv[EPT], co[EPT];
+            T cur_t[EPT], m_t[EPT], v_t[EPT], avg_o[EPT], m_o[EPT], v_o[EPT], c_o[EPT];
 #if FLAME_OPT_PREFETCH
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) {
-                cur[j] = curs[v][j];
-                m[j] = zero_state ? 0.f : ms[v][j];
-                vv[j] = zero_state ? 0.f : vs[v][j];
-            }
+            for (int j = 0; j < EPT; ++j) { cur_t[j] = curs[v][j]; m_t[j] = ms[v][j]; v_t[j] = vs[v][j]; }
 #else
-            unpack<float, EPT>(ld_v(curp + v * VS), cur);
-            if (zero_state) {
-#pragma unroll
-                for (int j = 0; j < EPT; ++j) { m[j] = 0.f; vv[j] = 0.f; }
-            } else {
-                unpack<float, EPT>(ld_v(mp + v * VS), m);
-                unpack<float, EPT>(ld_v(vp + v * VS), vv);
+            unpack<T, EPT>(ld_v(curp + v * VS), cur_t);
+            if (!zero_state) {
+                unpack<T, EPT>(ld_v(mp + v * VS), m_t);
+                unpack<T, EPT>(ld_v(vp + v * VS), v_t);
             }
 #endif
 #pragma unroll
-            for (int j = 0; j < EPT; ++j)
-                adapt_elem<VARIANT>(acc[v][j], cur[j], m[j], vv[j], co[j], b1, omb1, b2, omb2, eta, tau);
-            if (ap) st_v(ap + e0 + v * VS, pack<float, EPT>(acc[v]));
-            st_v(mp + v * VS, pack<float, EPT>(m));
-            st_v(vp + v * VS, pack<float, EPT>(vv));
-            st_v(cop + v * VS, pack<float, EPT>(co));
+            for (int j = 0; j < EPT; ++j) {
+                float mj = zero_state ? 0.f : X::ld(m_t[j]), vj = zero_state ? 0.f : X::ld(v_t[j]), cj;
+                adapt_elem<DT, VARIANT>(acc[v][j], X::ld(cur_t[j]), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
+                avg_o[j] = X::st(acc[v][j]);
+                m_o[j] = X::st(mj);
+                v_o[j] = X::st(vj);
+                c_o[j] = X::st(cj);
+            }
+            if (ap) st_v(ap + v * VS, pack<T, EPT>(avg_o));
+            st_v(mp + v * VS, pack<T, EPT>(m_o));
+            st_v(vp + v * VS, pack<T, EPT>(v_o));
+            st_v(cop + v * VS, pack<T, EPT>(c_o));
         }
     } else {
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) acc[v][j] = (e0 + v * VS + j < sg.numel) ? ld1(base + v * VS + j) : 0.f;
+            for (int j = 0; j < EPT; ++j)
+                acc[v][j] = (e0 + v * VS + j < sg.numel) ? X::ld(ld1(base + v * VS + j)) : 0.f;
         reduce_clients<DT, 1, false>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
@@ -468,12 +487,12 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
             for (int j = 0; j < EPT; ++j) {
                 const int64_t o = v * VS + j;
                 if (e0 + o >= sg.numel) continue;
-                float mj = zero_state ? 0.f : ld1(mp + o), vj = zero_state ? 0.f : ld1(vp + o), cj;
-                adapt_elem<VARIANT>(acc[v][j], ld1(curp + o), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
-                if (ap) st1(ap + e0 + o, acc[v][j]);
-                st1(mp + o, mj);
-                st1(vp + o, vj);
-                st1(cop + o, cj);
+                float mj = zero_state ? 0.f : X::ld(ld1(mp + o)), vj = zero_state ? 0.f : X::ld(ld1(vp + o)), cj;
+                adapt_elem<DT, VARIANT>(acc[v][j], X::ld(ld1(curp + o)), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
+                if (ap) st1(ap + o, X::st(acc[v][j]));
+                st1(mp + o, X::st(mj));
+                st1(vp + o, X::st(vj));
+                st1(cop + o, X::st(cj));
             }
     }
 }
@@ -650,29 +669,41 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     return check_launch("flame_agg_reduce");
 }
 
-int flame_fedopt_reduce_adapt(int variant, unsigned flags, const flame_segment* segs, int32_t n_segs,
+int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flame_segment* segs, int32_t n_segs,
                               int64_t n_chunks, const void* const* clients, int32_t n_clients,
                               const float* rates32, float b1, float omb1, float b2, float omb2, float eta,
                               float tau, void* stream) {
     int rc = validate(segs, n_segs, n_chunks, n_clients, clients);
     if (rc) return rc;
     if (n_clients > 0 && !rates32) return set_err(FLAME_EINVAL, "rate array is NULL");
+    if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: unknown variant %d", variant);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-    switch (variant) {
-    case FLAME_FEDADAM:
-        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDADAM, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
-        break;
-    case FLAME_FEDYOGI:
-        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDYOGI, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
-        break;
-    case FLAME_FEDADAGRAD:
-        hipLaunchKernelGGL((fedopt_kernel<FLAME_FEDADAGRAD, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);
-        break;
-    default:
-        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: unknown variant %d", variant);
+#define FLAME_OPT_LAUNCH(DT, CUV)                                                                              \
+    switch (variant) {                                                                                         \
+    case FLAME_FEDADAM:                                                                                        \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAM, CUV>), grid, block, 0, st, segs, n_segs, cl,       \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        break;                                                                                                 \
+    case FLAME_FEDYOGI:                                                                                        \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDYOGI, CUV>), grid, block, 0, st, segs, n_segs, cl,       \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        break;                                                                                                 \
+    default:                                                                                                   \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAGRAD, CUV>), grid, block, 0, st, segs, n_segs, cl,    \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        break;                                                                                                 \
     }
+    switch (dtype) {
+    case FLAME_F32: FLAME_OPT_LAUNCH(FLAME_F32, kClientUnroll) break;
+    case FLAME_BF16: FLAME_OPT_LAUNCH(FLAME_BF16, kClientUnroll16) break;
+    case FLAME_F16: FLAME_OPT_LAUNCH(FLAME_F16, kClientUnroll16) break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: dtype %d not supported (f32, bf16, f16)", dtype);
+    }
+#undef FLAME_OPT_LAUNCH
     return check_launch("flame_fedopt_reduce_adapt");
 }
 

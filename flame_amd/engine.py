@@ -326,31 +326,41 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
                          cur: List[torch.Tensor], cur_out: List[torch.Tensor], m: List[torch.Tensor],
                          v: List[torch.Tensor], clients: List[List[torch.Tensor]], rates: Sequence[float],
                          hyper, state_zero: bool) -> None:
-    """Fused FedAvg + FedOPT step over fp32 segments (kernel: flame_fedopt_reduce_adapt)."""
+    """Fused FedAvg + FedOPT step (kernel: flame_fedopt_reduce_adapt), one launch per dtype
+    (fp32 / bf16 / fp16; every tensor of a segment shares its dtype)."""
     if not base:
         return
     device = base[0].device
     L = N.lib()
-    segs, keep = [], []
-    for s in range(len(base)):
-        for t in (base[s], cur[s], cur_out[s], m[s], v[s]):
-            assert t.dtype == torch.float32 and t.is_contiguous() and t.device == device
-        row, tstride = _client_row(clients[s], base[s], device, keep)
-        segs.append(Seg(base[s].numel(), out=avg_out[s].data_ptr() if avg_out[s] is not None else 0,
-                        inp=base[s].data_ptr(), cur=cur[s].data_ptr(), cur_out=cur_out[s].data_ptr(),
-                        m=m[s].data_ptr(), v=v[s].data_ptr(), clients=row, tile_stride=tstride))
-    p = plan(N.FLAME_F32, segs, rates)
-    dm = _staging.upload(p.meta, device)
-    segp, clp, r32p, _ = _device_ptrs(dm, p)
-    P = sum(s.numel for s in segs)
-    # clients + base + cur (+ m, v unless zero state) read; avg, m, v, cur_out written
-    nbytes = 4 * P * (p.n_clients + 2 + (0 if state_zero else 2) + 4)
-    with _timed("flame_fedopt_reduce_adapt", device, nbytes):
-        N.check(L.flame_fedopt_reduce_adapt(FEDOPT_VARIANT[variant], N.FLAME_OPT_STATE_ZERO if state_zero else 0,
-                                            segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
-                                            *[float(x) for x in hyper], _stream_ptr(device)))
-    keep.append(dm)
-    _keepalive(keep, device)
+    groups = collections.OrderedDict()
+    for s_, b in enumerate(base):
+        groups.setdefault(dtype_code(b.dtype), []).append(s_)
+    for code, idx in groups.items():
+        segs, keep = [], []
+        for s_ in idx:
+            for t in (base[s_], cur[s_], cur_out[s_], m[s_], v[s_]):
+                assert t.dtype == base[s_].dtype and t.is_contiguous() and t.device == device
+            row, tstride = _client_row(clients[s_], base[s_], device, keep)
+            segs.append(Seg(base[s_].numel(), out=avg_out[s_].data_ptr() if avg_out[s_] is not None else 0,
+                            inp=base[s_].data_ptr(), cur=cur[s_].data_ptr(), cur_out=cur_out[s_].data_ptr(),
+                            m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row, tile_stride=tstride))
+        p = plan(code, segs, rates)
+        dm = _staging.upload(p.meta, device)
+        segp, clp, r32p, _ = _device_ptrs(dm, p)
+        P = sum(sg.numel for sg in segs)
+        isz = ITEMSIZE[code]
+        # clients + base + cur (+ m, v unless zero state) read; avg, m, v, cur_out written
+        nbytes = isz * P * (p.n_clients + 2 + (0 if state_zero else 2) + 4)
+        h = list(hyper)
+        if code in (N.FLAME_BF16, N.FLAME_F16):  # torch-CPU rounds the scalar of `sqrt(v) + tau`
+            h[5] = float(torch.tensor(float(h[5]), dtype=base[idx[0]].dtype))
+        with _timed("flame_fedopt_reduce_adapt", device, nbytes):
+            N.check(L.flame_fedopt_reduce_adapt(code, FEDOPT_VARIANT[variant],
+                                                N.FLAME_OPT_STATE_ZERO if state_zero else 0,
+                                                segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
+                                                *[float(x) for x in h], _stream_ptr(device)))
+        keep.append(dm)
+        _keepalive(keep, device)
 
 
 def fedopt_scalars(beta_1, beta_2, eta, tau):

@@ -5,14 +5,15 @@ return ``current_weights``; round 1 -> ``current_weights = agg_weights`` (no
 adaptive step); afterwards the adaptive step of ``_adapt_pytorch``
 (:102-129) with the subclass's ``_delta_v``.
 
-From the second adaptive-capable round on, fp32 keys go through ONE fused
-kernel (``flame_fedopt_reduce_adapt``): the client reduction, ``d``, ``m_t``,
-``v_t`` and the new ``current`` are computed in registers, reading
-base/cur/m/v once and writing avg/m/v/cur once, instead of ~12 unfused
-torch passes.  Non-fp32 keys (e.g. BatchNorm's int64 ``num_batches_tracked``,
-whose dtype the reference silently promotes to fp32 here) are reduced by the
-same FedAvg kernel and then follow the reference op sequence with torch ops
-on the device.
+From the second adaptive-capable round on, fp32 / bf16 / fp16 keys go through
+ONE fused kernel per dtype (``flame_fedopt_reduce_adapt``): the client
+reduction, ``d``, ``m_t``, ``v_t`` and the new ``current`` are computed in
+registers with one rounding per reference op, reading base/cur/m/v once and
+writing avg/m/v/cur once, instead of ~12 unfused torch passes.  Other keys
+(BatchNorm's int64 ``num_batches_tracked``, which the reference silently
+promotes to fp32 in this step, and any key whose dtype changed) are reduced by
+the FedAvg kernel and then follow the reference op sequence with torch ops on
+the device.
 
 Ownership: ``base_weights`` is mutated in place into the
 FedAvg result (``self.agg_weights``); ``m_t``/``v_t`` persist across rounds on
@@ -81,11 +82,14 @@ class FedOPT(FedAvg):
         device = engine.pick_device(base_weights, current, *[w for w, _ in entries])
         keys = list(base_weights.keys())
         fused, generic = [], []
+        float_dts = (torch.float32, torch.bfloat16, torch.float16)
         for k in keys:
-            ok = (base_weights[k].dtype == torch.float32 and k in current
-                  and current[k].dtype == torch.float32 and current[k].shape == base_weights[k].shape
-                  and all(k in w and w[k].dtype == torch.float32 for w, _ in entries)
-                  and (self.m_t is None or (self.m_t[k].dtype == torch.float32 and self.v_t[k].dtype == torch.float32)))
+            dt = base_weights[k].dtype
+            ok = (dt in float_dts and k in current
+                  and current[k].dtype == dt and current[k].shape == base_weights[k].shape
+                  and all(k in w and w[k].dtype == dt for w, _ in entries)
+                  and (self.m_t is None or (k in self.m_t and self.m_t[k].dtype == dt
+                                            and self.v_t[k].dtype == dt)))
             (fused if ok else generic).append(k)
         for w, _ in entries:
             for k in w.keys():
@@ -99,12 +103,12 @@ class FedOPT(FedAvg):
         if fused:
             targets = [engine._Target(base_weights[k], device) for k in fused]
             curs = [engine._as_device(current[k], device) for k in fused]
-            outs = [torch.empty(base_weights[k].shape, dtype=torch.float32, device=device) for k in fused]
+            outs = [torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device) for k in fused]
             ms, vs = [], []
             for k in fused:
-                if state_zero:
-                    self.m_t[k] = torch.empty(base_weights[k].shape, dtype=torch.float32, device=device)
-                    self.v_t[k] = torch.empty(base_weights[k].shape, dtype=torch.float32, device=device)
+                if state_zero:  # zeros_like(d_t[k]) in the reference: d's dtype
+                    self.m_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
+                    self.v_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
                 else:
                     self.m_t[k] = engine._as_device(self.m_t[k], device)
                     self.v_t[k] = engine._as_device(self.v_t[k], device)

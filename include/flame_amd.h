@@ -123,16 +123,18 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment *segs, int32
                      const float *rates32, const double *rates64, void *stream);
 
 /*
- * Fused FedAvg + FedOPT adaptive step, fp32 only.  After the reduction above
- * (avg kept in registers, optionally written to seg.out), per element:
+ * Fused FedAvg + FedOPT adaptive step (dtype FLAME_F32, FLAME_BF16 or FLAME_F16; base,
+ * cur, m, v, outputs and clients all of that dtype).  After the reduction above (avg kept
+ * in registers, optionally written to seg.out), per element, every op rounded in dtype:
  *   d = avg - cur; m = b1*m + omb1*d;
  *   Adam: v = b2*v + omb2*(d*d);  Yogi: v = v - omb2*(d*d)*sign(v - d*d);  AdaGrad: v = v + d*d
  *   cur_out = cur + (eta*m) / (sqrt(v) + tau)
- * Scalars are the fp32 roundings torch applies to the Python floats:
- *   b1 = f32(beta_1), omb1 = f32(1 - beta_1), b2 = f32(beta_2), omb2 = f32(1 - beta_2),
- *   eta = f32(eta), tau = f32(tau).
+ * Scalars are the roundings torch applies to the Python floats: b1 = f32(beta_1),
+ * omb1 = f32(1 - beta_1), b2 = f32(beta_2), omb2 = f32(1 - beta_2), eta = f32(eta),
+ * tau = f32(tau) for fp32 but dtype(tau) for bf16/fp16 (torch-CPU rounds a scalar to a
+ * reduced-precision tensor's dtype before + / -).
  */
-int flame_fedopt_reduce_adapt(int variant, unsigned flags, const flame_segment *segs,
+int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flame_segment *segs,
                               int32_t n_segs, int64_t n_chunks, const void *const *clients,
                               int32_t n_clients, const float *rates32, float b1, float omb1,
                               float b2, float omb2, float eta, float tau, void *stream);

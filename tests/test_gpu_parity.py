@@ -494,3 +494,39 @@ def test_registered_shared_memory_payloads_zero_copy():
         O.reduce_tensor(exp, [w["w"] for w in ws], [(10 + i) / sum(10 + j for j in range(n)) for i in range(n)])
         S.assert_bitwise("registered", S.to_cpu(out), {"w": exp})
         del cache, msg
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_fedopt_fused_reduced_precision_vs_reference_ops(sort, dtype):
+    """bf16 / fp16 FedOPT keys take the fused kernel; compare with the reference's own torch-CPU
+    op sequence (oracle._adapt_torch) over 3 rounds: the reduction is bitwise, the adaptive step
+    agrees to within one ulp of the dtype (torch-CPU's fp32 sqrt is not correctly rounded)."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(17)
+    P, n = 20_011, 8
+    w0 = torch.randn(P, generator=g).to(dtype)
+    amd, ora = make_amd(sort), O.OracleFedOPT(sort)
+    wa, wo = {"w": w0.to(DEV)}, {"w": w0.clone()}
+    ulp = 2.0 ** -7 if dtype == torch.bfloat16 else 2.0 ** -10
+    for r in range(3):
+        cl = [(torch.randn(P, generator=g) * 1e-2).to(dtype) for _ in range(n)]
+        counts = [5 + 3 * i for i in range(n)]
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i in range(n):
+            ca[f"{i}"] = S.TR({"w": cl[i].to(DEV)}, counts[i])
+            co[f"{i}"] = S.TR({"w": cl[i].clone()}, counts[i])
+        wa = amd.do({"w": wa["w"].clone()}, ca, total=sum(counts))
+        wo = ora.do({"w": wo["w"].clone()}, co, total=sum(counts))
+        S.assert_bitwise(f"{sort}/{dtype}/r{r}/avg", S.to_cpu(amd.agg_weights), ora.agg_weights)
+        got, exp = wa["w"].cpu().double(), wo["w"].double()
+        assert got.dtype == exp.dtype and wa["w"].dtype == dtype
+        assert ((got - exp).abs() <= exp.abs() * ulp + 1e-30).all(), f"{sort}/{dtype}/r{r}"
+        if r >= 1:
+            assert amd.m_t["w"].dtype == dtype
+        wo = {"w": wa["w"].cpu().clone()}   # continue both from the same state
+        if ora.current_weights is not None:
+            ora.current_weights = {"w": wo["w"].clone()}
+        if amd.m_t is not None and ora.m_t is not None:
+            ora.m_t = {"w": amd.m_t["w"].cpu().clone()}
+            ora.v_t = {"w": amd.v_t["w"].cpu().clone()}

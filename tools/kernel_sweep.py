@@ -62,7 +62,8 @@ def load(name):
     L.flame_agg_reduce.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp, vp]
     L.flame_last_error.restype = ctypes.c_char_p
     L.flame_fedopt_reduce_adapt.restype = ctypes.c_int
-    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [ctypes.c_float] * 6 + [vp]
+    L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + \
+        [ctypes.c_float] * 6 + [vp]
     return L
 
 
@@ -150,7 +151,7 @@ def main():
             rc = libs[nm].flame_agg_reduce(code, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
                                            b + p.off_r32, b + p.off_r64, stream)
         else:
-            rc = libs[nm].flame_fedopt_reduce_adapt({"fedadam": 0, "fedyogi": 1}[args.kernel], 0, b, p.n_segs,
+            rc = libs[nm].flame_fedopt_reduce_adapt(code, {"fedadam": 0, "fedyogi": 1}[args.kernel], 0, b, p.n_segs,
                                                     p.n_chunks, b + p.off_clients, p.n_clients, b + p.off_r32,
                                                     *[float(x) for x in hyper], stream)
         if rc:
