@@ -360,7 +360,12 @@ def decode(payload, extra_globals: Dict[tuple, Any] = None):
         for v in extra_globals.values():
             if isinstance(v, type) and issubclass(v, enum.Enum):
                 _CALLABLE_ALLOW.add(v)
-    obj, _ = dec.load(0)
+    try:
+        obj, _ = dec.load(0)
+    except pickle.UnpicklingError:
+        raise
+    except (IndexError, KeyError, ValueError, TypeError, struct.error, UnicodeDecodeError) as e:
+        raise pickle.UnpicklingError(f"malformed update payload: {type(e).__name__}: {e}") from None
     return obj
 
 

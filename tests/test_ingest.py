@@ -101,3 +101,39 @@ def test_device_update_cache_host_placement_orders_and_pops():
     assert len(c) == 3 and list(c.iterkeys()) == ["a", "b", "c"] and "a" in c
     t = c.pop("a")
     assert t.count == 1 and len(c) == 2 and c.pop("zz") is None
+
+
+def test_decode_malformed_payloads_raise_unpickling_error():
+    payload = cloudpickle.dumps({"w": torch.randn(100)})
+    for bad in (payload[:len(payload) // 2], payload[:10], b"\x80\x05\xff", b""):
+        with pytest.raises(pickle.UnpicklingError):
+            ingest.decode(bad)
+
+
+def test_decode_property_random_messages():
+    """Property: for random update-like messages, decode == cloudpickle.loads (values, dtypes,
+    shapes, strides) -- hypothesis-generated dtypes, shapes, views and metadata."""
+    from hypothesis import given, settings, strategies as st
+
+    dts = st.sampled_from([torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64,
+                           torch.int32, torch.uint8, torch.bool])
+    shapes = st.lists(st.integers(0, 7), min_size=0, max_size=3)
+
+    @settings(max_examples=60, deadline=None)
+    @given(dts, shapes, st.integers(0, 3), st.dictionaries(st.text(max_size=5), st.integers() | st.floats(
+        allow_nan=False) | st.text(max_size=8) | st.none(), max_size=4), st.booleans())
+    def check(dt, shape, off, meta, transpose):
+        base = (torch.arange(int(np.prod(shape or [1])) + off) % 5).to(dt)
+        t = base[off:].reshape(shape) if shape else base[off:off + 1].reshape(())
+        if transpose and t.dim() >= 2:
+            t = t.transpose(0, 1)
+        payload = cloudpickle.dumps({"weights": {"t": t}, "meta": meta})
+        got = ingest.decode(payload)
+        ref = cloudpickle.loads(payload)
+        assert got["meta"] == ref["meta"]
+        g, r = got["weights"]["t"], ref["weights"]["t"]
+        assert g.dtype == r.dtype and g.shape == r.shape and g.stride() == r.stride()
+        if dt == torch.bfloat16:
+            g, r = g.view(torch.int16), r.view(torch.int16)
+        assert torch.equal(g, r)
+    check()
