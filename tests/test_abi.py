@@ -61,3 +61,15 @@ def test_segment_struct_size():
     fields = [ln for ln in body.split(";") if ln.strip()]
     from flame_amd import _native
     assert len(fields) == _native.SEGMENT_INT64S  # every field is 8 bytes
+
+
+def test_fedopt_and_host_entry_points_validate_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    args = [0, 0, 0, None, 0, 1, None, 0, None] + [0.0] * 6 + [None]
+    assert L.flame_fedopt_reduce_adapt(*args) == _native.FLAME_EINVAL
+    args[0] = 4  # int64 has no FedOPT kernel, but argument checks come first
+    assert L.flame_fedopt_reduce_adapt(*args) == _native.FLAME_EINVAL
+    assert L.flame_host_register(None, 0) == _native.FLAME_EINVAL
+    assert L.flame_host_unregister(None) == _native.FLAME_EINVAL
+    assert L.flame_host_device_pointer(None, None) == _native.FLAME_EINVAL
