@@ -4,10 +4,12 @@ from .fedadagrad import FedAdaGrad
 from .fedadam import FedAdam
 from .fedavg import FedAvg
 from .fedbuff import FedBuff
+from .feddyn import FedDyn
 from .fedopt import FedOPT
 from .fedprox import FedProx
 from .fedyogi import FedYogi
+from .scaffold import Scaffold
 from .train_result import TrainResult
 
 __all__ = ["AbstractOptimizer", "FedAvg", "FedOPT", "FedAdam", "FedYogi", "FedAdaGrad", "FedBuff",
-           "FedProx", "TrainResult"]
+           "FedProx", "FedDyn", "Scaffold", "TrainResult"]

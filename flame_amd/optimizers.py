@@ -4,11 +4,11 @@ flame's own provider so existing roles pick them up unchanged.
 
 ``OptimizerType`` is a closed enum validated by flame's config
 (config.py:55-70,121-123), so the drop-in re-registers the existing keys
-(``fedavg``, ``fedadagrad``, ``fedadam``, ``fedyogi``, ``fedbuff``, ``fedprox``)
-instead of adding new ones.  Keys the MI355X path does not cover (feddyn,
-scaffold, fedgft) keep flame's own classes.
+(``fedavg``, ``fedadagrad``, ``fedadam``, ``fedyogi``, ``fedbuff``, ``fedprox``,
+``feddyn``, ``scaffold``) instead of adding new ones.  ``fedgft`` (a different
+server computation, optimizer/fedgft.py) keeps flame's own class.
 """
-from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedProx, FedYogi
+from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedDyn, FedProx, FedYogi, Scaffold
 
 DROP_INS = {
     "fedavg": FedAvg,
@@ -17,6 +17,8 @@ DROP_INS = {
     "fedyogi": FedYogi,
     "fedbuff": FedBuff,
     "fedprox": FedProx,
+    "feddyn": FedDyn,
+    "scaffold": Scaffold,
 }
 
 

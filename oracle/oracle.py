@@ -11,6 +11,8 @@ References (``/root/reference/lib/python/flame/``):
   * FedAvg.do            optimizer/fedavg.py:49-87, _aggregate_pytorch :89-104
   * FedOPT.do            optimizer/fedopt.py:58-92, _adapt_pytorch :102-129
   * FedBuff.do           optimizer/fedbuff.py:59-99, scale_add :101-127, _aggregate :136-157
+  * FedDyn               optimizer/feddyn.py:51-62 (save_state), :64-115 (do), :125-139 (add_to_hist)
+  * Scaffold             optimizer/scaffold.py:58-90 (save_state), :92-139 (do), :141-150
 Parity of this oracle is pinned by ``tests/test_oracle_golden.py`` against
 vectors produced by the real reference (``tests/golden/make_golden.py``).
 """
@@ -220,6 +222,110 @@ class OracleFedBuff:
         for k in base_weights.keys():
             scale_add_tensor(base_weights[k], agg_goal_weights[k], agg_goal)
         return base_weights
+
+
+def _same_float(acc, *others):
+    return acc.is_floating_point() and all(o.dtype == acc.dtype for o in others)
+
+
+class OracleFedDyn(OracleFedAvg):
+    """feddyn.py:31-139.  Same-dtype float keys run through the C kernel
+    (``h + w`` == ``h + round(w*1.0)``; ``0.0 + Σ rate*h`` == a zero start);
+    keys whose dtypes differ or are integer keep the reference's torch ops."""
+
+    def __init__(self, alpha=0.01):
+        super().__init__()
+        self.alpha = alpha
+        self.local_param_dict = {}
+        self.cld_model = None
+
+    def save_state(self, state, **kwargs):
+        if getattr(state, "value", state) == "pre":
+            self.local_param_dict = {e: self.local_param_dict.get(e) for e in kwargs["active_ends"]}
+
+    def do(self, base_weights, cache, *, total=0, version=0, **kwargs):
+        assert base_weights is not None
+        self.agg_weights = base_weights
+        if len(cache) == 0 or total == 0:
+            return None
+        rate = 1 / len(cache)
+        for k in list(cache.iterkeys()):
+            tres = cache.pop(k)
+            self._add_to_hist(k, tres.weights)
+            for key, v in tres.weights.items():
+                reduce_tensor(self.agg_weights[key], [v], [rate])
+        avg = self.agg_weights
+        rate = 1 / len(self.local_param_dict)
+        hist = [h for h in self.local_param_dict.values() if h is not None]
+        self.cld_model = {}
+        for k in avg:
+            if _same_float(avg[k], *[h[k] for h in hist]):
+                mean = torch.zeros_like(avg[k])
+                reduce_tensor(mean, [h[k] for h in hist], [rate] * len(hist))
+                out = avg[k].clone()
+                reduce_tensor(out, [mean], [1.0])
+            else:
+                mean = 0.0
+                for h in hist:
+                    mean = mean + rate * h[k]
+                out = avg[k] + mean
+            self.cld_model[k] = out
+        return avg
+
+    def _add_to_hist(self, end, w):
+        h = self.local_param_dict.get(end)
+        if h is None:
+            self.local_param_dict[end] = {k: _cpu(v).clone() for k, v in w.items()}
+            return
+        for k in list(h.keys()):
+            if _same_float(h[k], w[k]):
+                reduce_tensor(h[k], [w[k]], [1.0])
+            else:
+                h[k] = h[k] + _cpu(w[k])
+
+
+class OracleScaffold(OracleFedAvg):
+    """scaffold.py:36-150: control variates folded into c_glob with rate 1/len(weight_dict),
+    then FedAvg with rate 1/len(cache)."""
+
+    def __init__(self, k=3):
+        super().__init__()
+        self.c_glob = None
+        self.weight_dict = None
+
+    def save_state(self, state, **kwargs):
+        if getattr(state, "value", state) != "pre":
+            return
+        if "dataset_sizes" in kwargs:
+            ds = kwargs["dataset_sizes"]
+            tot, n = sum(ds.values()), len(ds)
+            self.weight_dict = {e: (ds[e] / tot) * n for e in ds}
+        if "glob_weights" in kwargs and self.c_glob is None:
+            g = kwargs["glob_weights"]
+            self.c_glob = {k: torch.zeros(g[k].shape, dtype=g[k].dtype) for k in g}
+
+    def do(self, base_weights, cache, *, total=0, version=0, **kwargs):
+        assert base_weights is not None
+        if len(cache) == 0 or total == 0:
+            return None
+        control_cache = kwargs["control_cache"]
+        if len(control_cache) != len(cache):
+            return None
+        rate = 1 / len(self.weight_dict)
+        for k in list(control_cache.iterkeys()):
+            for key, v in control_cache.pop(k).weights.items():
+                c = self.c_glob[key]
+                if v.dtype == c.dtype:
+                    reduce_tensor(c, [v], [rate])
+                else:
+                    tmp = _cpu(v) * rate
+                    c += tmp.to(dtype=c.dtype)
+        self.agg_weights = base_weights
+        rate = 1 / len(cache)
+        for k in list(cache.iterkeys()):
+            for key, v in cache.pop(k).weights.items():
+                reduce_tensor(self.agg_weights[key], [v], [rate])
+        return self.agg_weights
 
 
 class ListCache:

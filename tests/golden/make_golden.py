@@ -18,6 +18,8 @@ Call patterns reproduced:
   * async FedBuff:         do(agg_goal_weights, cache(1 entry), total=count, version=round),
     then scale_add_agg_weights(weights, agg, goal)
                            -- lib/python/flame/mode/horizontal/asyncfl/top_aggregator.py:85-110
+  * FedDyn / SCAFFOLD:    save_state(PRE, ...) then do(deepcopy(...), cache, ...)
+                           -- lib/python/flame/mode/horizontal/{feddyn,scaffold}/top_aggregator.py
   * hierarchical middle:   delta = (weights after scale_add) - prev_weights
                            -- lib/python/flame/mode/horizontal/asyncfl/middle_aggregator.py:221-226,246
 """
@@ -38,6 +40,7 @@ from fixture_io import FixtureWriter  # noqa: E402
 
 from flame.optimizers import optimizer_provider  # noqa: E402  (reference, via PYTHONPATH)
 from flame.optimizer.train_result import TrainResult  # noqa: E402
+from flame.common.constants import TrainState  # noqa: E402
 from diskcache import Cache  # noqa: E402  (shim)
 
 from flame_amd import synth  # noqa: E402
@@ -324,7 +327,96 @@ def hier_fedbuff_small():
     print("wrote hier_fedbuff_small.npz")
 
 
+FEDDYN_SHAPES = {"w": ((40, 30), torch.float32), "b": ((30,), torch.float32),
+                 "bf": ((70,), torch.bfloat16), "nbt": ((), torch.int64)}
+
+
+def feddyn_rounds():
+    """FedDyn as its top aggregator drives it (feddyn/top_aggregator.py:101-107,140,163-165):
+    save_state(PRE, active_ends=all_ends); do(deepcopy(cld_weights), cache, ...);
+    cld_weights = optimizer.cld_model.  Ends drop out and come back (history kept,
+    None for never-seen ends) and one round has an end outside all_ends (untracked)."""
+    gen = torch.Generator().manual_seed(81)
+    all_ends = [f"e{i}" for i in range(6)]
+    rounds = [["e0", "e1", "e2", "e3"], ["e1", "e2", "e3", "e4", "e5"],
+              ["e0", "e2", "e4", "x9"], ["e5", "e3", "e1", "e0"]]
+    weights = small_weights(gen, FEDDYN_SHAPES, 1.0)
+    opt = optimizer_provider.get("feddyn", alpha=0.01)
+    fw = FixtureWriter()
+    fw.put_weights("weights0", weights)
+    cld = weights
+    all_counts, orders = [], []
+    for r, ends in enumerate(rounds):
+        opt.save_state(TrainState.PRE, active_ends=all_ends)
+        clients = [small_weights(gen, FEDDYN_SHAPES, 1e-2) for _ in ends]
+        for i, c in enumerate(clients):
+            c["nbt"] = torch.tensor(5 * r + i, dtype=torch.int64)
+        counts = [int(x) for x in torch.randint(1, 1001, (len(ends),), generator=gen)]
+        cache = Cache()
+        for e, w, c in zip(ends, clients, counts):
+            cache[e] = TrainResult(w, c)
+        orders.append(list(cache.iterkeys()))
+        all_counts.append(counts)
+        out = opt.do(deepcopy(cld), cache, total=sum(counts), num_trainers=len(ends))
+        cld = opt.cld_model if opt.cld_model is not None else out
+        for i, w in enumerate(clients):
+            fw.put_weights(f"r{r}/client{i}", w)
+        fw.put_weights(f"r{r}/avg", out)
+        fw.put_weights(f"r{r}/cld", opt.cld_model)
+    fw.meta.update({"kind": "feddyn_rounds", "alpha": 0.01, "all_ends": all_ends, "rounds": rounds,
+                    "orders": orders, "counts": all_counts})
+    fw.save(os.path.join(HERE, "feddyn_rounds.npz"))
+    print("wrote feddyn_rounds.npz")
+
+
+def scaffold_rounds():
+    """SCAFFOLD as its top aggregator drives it (scaffold/top_aggregator.py:115-126,160,177):
+    save_state(PRE, dataset_sizes=...) once, save_state(PRE, glob_weights=weights) every
+    round, do(deepcopy(weights), cache, ..., control_cache=control_cache).  The int64
+    buffer's control variate arrives as fp32 (the reference casts it back, scaffold.py:143-148)."""
+    gen = torch.Generator().manual_seed(82)
+    ends = [f"e{i}" for i in range(7)]
+    sizes = {e: int(x) for e, x in zip(ends, torch.randint(100, 5000, (len(ends),), generator=gen))}
+    rounds = [ends[:5], ends[2:], ends[::2]]
+    weights = small_weights(gen, FEDDYN_SHAPES, 1.0)
+    opt = optimizer_provider.get("scaffold", k=3)
+    opt.save_state(TrainState.PRE, dataset_sizes=sizes)
+    fw = FixtureWriter()
+    fw.put_weights("weights0", weights)
+    orders = []
+    for r, rends in enumerate(rounds):
+        opt.save_state(TrainState.PRE, glob_weights=weights)
+        clients = [small_weights(gen, FEDDYN_SHAPES, 1e-2) for _ in rends]
+        controls = [small_weights(gen, FEDDYN_SHAPES, 1e-3) for _ in rends]
+        for i, (c, cv) in enumerate(zip(clients, controls)):
+            c["nbt"] = torch.tensor(7 * r + i, dtype=torch.int64)
+            cv["nbt"] = torch.tensor(9.25 * (i + 1) + r, dtype=torch.float32)
+        cache, control_cache = Cache(), Cache()
+        for e, w, cv in zip(rends, clients, controls):
+            cache[e] = TrainResult(w, sizes[e])
+            control_cache[e] = TrainResult(cv)
+        orders.append(list(cache.iterkeys()))
+        weights = opt.do(deepcopy(weights), cache, total=sum(sizes[e] for e in rends),
+                         num_trainers=len(rends), control_cache=control_cache)
+        for i, (w, cv) in enumerate(zip(clients, controls)):
+            fw.put_weights(f"r{r}/client{i}", w)
+            fw.put_weights(f"r{r}/control{i}", cv)
+        fw.put_weights(f"r{r}/out", weights)
+        fw.put_weights(f"r{r}/c_glob", opt.c_glob)
+    fw.meta.update({"kind": "scaffold_rounds", "k": 3, "dataset_sizes": sizes, "rounds": rounds,
+                    "orders": orders})
+    fw.save(os.path.join(HERE, "scaffold_rounds.npz"))
+    print("wrote scaffold_rounds.npz")
+
+
+CASES = {"feddyn_rounds": feddyn_rounds, "scaffold_rounds": scaffold_rounds}
+
+
 def main():
+    if len(sys.argv) > 1:      # regenerate only the named cases
+        for name in sys.argv[1:]:
+            CASES[name]()
+        return
     fedavg_case("fedavg_small.npz",
                 {"w": ((1000, 37), torch.float32), "b": ((37,), torch.float32),
                  "k": ((5, 3, 3), torch.float32), "nbt": ((), torch.int64)}, 16, 1)

@@ -225,6 +225,52 @@ def run_hier(fx, make_opt, device, delta_fn):
     return res
 
 
+class _PRE:
+    """Stands in for flame.common.constants.TrainState.PRE (value "pre")."""
+    value = "pre"
+
+
+def run_feddyn(fx, make_opt, device):
+    """feddyn/top_aggregator.py:101-107,140,163-165 call pattern (make_golden.feddyn_rounds)."""
+    m = fx.meta
+    opt = make_opt("feddyn", alpha=m["alpha"])
+    cld = to_dev(fx.weights("weights0"), device)
+    res = []
+    for r, ends in enumerate(m["rounds"]):
+        opt.save_state(_PRE, active_ends=m["all_ends"])
+        cache = SortedCache()
+        for i, (e, c) in enumerate(zip(ends, m["counts"][r])):
+            cache[e] = TR(to_dev(fx.weights(f"r{r}/client{i}"), device), c)
+        assert list(cache.iterkeys()) == m["orders"][r]
+        out = opt.do(deepcopy(cld), cache, total=sum(m["counts"][r]), num_trainers=len(ends))
+        assert len(cache) == 0
+        cld = opt.cld_model
+        res.append((f"r{r}/avg", to_cpu(out), fx.weights(f"r{r}/avg")))
+        res.append((f"r{r}/cld", to_cpu(cld), fx.weights(f"r{r}/cld")))
+    return res
+
+
+def run_scaffold(fx, make_opt, device):
+    """scaffold/top_aggregator.py:115-126,160,177 call pattern (make_golden.scaffold_rounds)."""
+    m = fx.meta
+    opt = make_opt("scaffold", k=m["k"])
+    opt.save_state(_PRE, dataset_sizes=m["dataset_sizes"])
+    weights = to_dev(fx.weights("weights0"), device)
+    res = []
+    for r, ends in enumerate(m["rounds"]):
+        opt.save_state(_PRE, glob_weights=weights)
+        cache, control_cache = SortedCache(), SortedCache()
+        for i, e in enumerate(ends):
+            cache[e] = TR(to_dev(fx.weights(f"r{r}/client{i}"), device), m["dataset_sizes"][e])
+            control_cache[e] = TR(to_dev(fx.weights(f"r{r}/control{i}"), device))
+        weights = opt.do(deepcopy(weights), cache, total=sum(m["dataset_sizes"][e] for e in ends),
+                         num_trainers=len(ends), control_cache=control_cache)
+        assert len(cache) == 0 and len(control_cache) == 0
+        res.append((f"r{r}/out", to_cpu(weights), fx.weights(f"r{r}/out")))
+        res.append((f"r{r}/c_glob", to_cpu(opt.c_glob), fx.weights(f"r{r}/c_glob")))
+    return res
+
+
 BITWISE_FIXTURES = [
     ("fedavg_small.npz", run_fedavg),
     ("fedavg_dtypes.npz", run_fedavg),
@@ -236,6 +282,8 @@ BITWISE_FIXTURES = [
     ("fedbuff_seq_fp32.npz", run_fedbuff_seq),
     ("fedbuff_seq_bf16.npz", run_fedbuff_seq),
     ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
+    ("feddyn_rounds.npz", run_feddyn),
+    ("scaffold_rounds.npz", run_scaffold),
 ]
 FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz"]
 

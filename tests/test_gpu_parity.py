@@ -530,3 +530,93 @@ def test_fedopt_fused_reduced_precision_vs_reference_ops(sort, dtype):
         if amd.m_t is not None and ora.m_t is not None:
             ora.m_t = {"w": amd.m_t["w"].cpu().clone()}
             ora.v_t = {"w": amd.v_t["w"].cpu().clone()}
+
+
+def _dyn_model(g, P):
+    return {"w": torch.randn(P, generator=g), "m": torch.randn(31, 129, generator=g),
+            "bf": torch.randn(4099, generator=g).bfloat16(), "h": torch.randn(777, generator=g).half(),
+            "nbt": torch.tensor(3, dtype=torch.int64)}
+
+
+def _dyn_update(g, tmpl, i, scale=1e-2):
+    return {k: (torch.randn(v.shape, generator=g) * scale).to(v.dtype) if v.is_floating_point()
+            else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
+
+
+@pytest.mark.parametrize("placement", ["hbm", "slab"])
+def test_feddyn_vs_oracle_partial_participation(placement):
+    """FedDyn drop-in == oracle bitwise over 4 rounds with ends dropping out, returning and
+    one untracked end; updates device-resident or tiled UpdateSlab views (history copies
+    are untiled).  ~1M params x 24 ends."""
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(23)
+    tmpl = _dyn_model(g, 1_000_003)
+    all_ends = [f"e{i:02d}" for i in range(24)]
+    rounds = [all_ends[:16], all_ends[4:], all_ends[::3] + ["zz"], all_ends[1::2]]
+    slab = UpdateSlab(tmpl, capacity=48, device=DEV) if placement == "slab" else None
+    amd, ora = make_amd("feddyn", alpha=0.01), O.OracleFedDyn(alpha=0.01)
+    ca_w, co_w = {k: v.to(DEV) for k, v in tmpl.items()}, {k: v.clone() for k, v in tmpl.items()}
+    for r, ends in enumerate(rounds):
+        amd.save_state(S._PRE, active_ends=all_ends)
+        ora.save_state(S._PRE, active_ends=all_ends)
+        ws = [_dyn_update(g, tmpl, 10 * r + i) for i in range(len(ends))]
+        counts = [7 + i for i in range(len(ends))]
+        ca, co = S.SortedCache(), S.SortedCache()
+        for e, w, c in zip(ends, ws, counts):
+            dw = {k: v.to(DEV) for k, v in w.items()}
+            ca[e] = S.TR(slab.put(dw) if slab is not None else dw, c)
+            co[e] = S.TR({k: v.clone() for k, v in w.items()}, c)
+        a = amd.do({k: v.clone() for k, v in ca_w.items()}, ca, total=sum(counts))
+        o = ora.do({k: v.clone() for k, v in co_w.items()}, co, total=sum(counts))
+        S.assert_bitwise(f"feddyn/{placement}/r{r}/avg", S.to_cpu(a), o)
+        S.assert_bitwise(f"feddyn/{placement}/r{r}/cld", S.to_cpu(amd.cld_model), ora.cld_model)
+        ca_w, co_w = amd.cld_model, ora.cld_model
+        del ca, co
+    assert set(amd.local_param_dict) == set(ora.local_param_dict)
+    for e, h in ora.local_param_dict.items():
+        if h is not None:
+            S.assert_bitwise(f"feddyn/{placement}/hist/{e}", S.to_cpu(amd.local_param_dict[e]), h)
+
+
+def test_scaffold_vs_oracle_rounds():
+    """SCAFFOLD drop-in == oracle bitwise: c_glob (HBM-resident, updated in place) and the
+    model over 3 rounds, including an int buffer whose control variate arrives as fp32, and
+    the None results (empty cache; control/model cache length mismatch) leave state alone."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(29)
+    tmpl = _dyn_model(g, 500_009)
+    ends = [f"t{i:02d}" for i in range(20)]
+    sizes = {e: 100 + 37 * i for i, e in enumerate(ends)}
+    amd, ora = make_amd("scaffold", k=3), O.OracleScaffold(k=3)
+    for o in (amd, ora):
+        o.save_state(S._PRE, dataset_sizes=sizes)
+    wa, wo = {k: v.to(DEV) for k, v in tmpl.items()}, {k: v.clone() for k, v in tmpl.items()}
+    for r, rends in enumerate([ends[:12], ends[5:], ends[::2]]):
+        amd.save_state(S._PRE, glob_weights=wa)
+        ora.save_state(S._PRE, glob_weights=wo)
+        ws = [_dyn_update(g, tmpl, r + i) for i in range(len(rends))]
+        cs = [_dyn_update(g, tmpl, 0, 1e-3) for _ in rends]
+        for i, c in enumerate(cs):
+            c["nbt"] = torch.tensor(9.25 * (i + 1) + r)
+        caches = {}
+        for side in ("a", "o"):
+            mv = (lambda t: t.to(DEV)) if side == "a" else (lambda t: t.clone())
+            cache, cc = S.SortedCache(), S.SortedCache()
+            for e, w, c in zip(rends, ws, cs):
+                cache[e] = S.TR({k: mv(v) for k, v in w.items()}, sizes[e])
+                cc[e] = S.TR({k: mv(v) for k, v in c.items()})
+            caches[side] = (cache, cc)
+        total = sum(sizes[e] for e in rends)
+        if r == 1:   # mismatched control cache -> None before anything is consumed
+            extra = S.SortedCache()
+            assert amd.do(wa, caches["a"][0], total=total, control_cache=extra) is None
+            assert len(caches["a"][0]) == len(rends)
+            assert amd.do(wa, S.SortedCache(), total=total, control_cache=caches["a"][1]) is None
+        wa = amd.do({k: v.clone() for k, v in wa.items()}, caches["a"][0], total=total,
+                    control_cache=caches["a"][1])
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, caches["o"][0], total=total,
+                    control_cache=caches["o"][1])
+        S.assert_bitwise(f"scaffold/r{r}/out", S.to_cpu(wa), wo)
+        S.assert_bitwise(f"scaffold/r{r}/c_glob", S.to_cpu(amd.c_glob), ora.c_glob)
+        assert all(t.is_cuda for t in amd.c_glob.values())

@@ -86,11 +86,12 @@ def test_fedbuff_stale_errors_raise_before_launch():
 def test_provider_semantics():
     from flame_amd.optimizers import optimizer_provider, ObjectFactory, install, DROP_INS
     with pytest.raises(ValueError):
-        optimizer_provider.get("scaffold")
+        optimizer_provider.get("fedgft")
     f = ObjectFactory()
     install(f)
+    ctor = {"fedprox": {"mu": 0.01}, "feddyn": {"alpha": 0.01}, "scaffold": {"k": 3}}
     for k in DROP_INS:
-        kw = {"mu": 0.01} if k == "fedprox" else {}
+        kw = ctor.get(k, {})
         assert isinstance(f.create(k, **kw), DROP_INS[k])
     assert optimizer_provider.get("fedadam").regularizer.get_term() == 0.0
 
@@ -131,3 +132,42 @@ def test_fedprox_is_fedavg_with_regularizer():
     w = [torch.ones(3), torch.zeros(2)]
     wt = [torch.zeros(3), torch.zeros(2)]
     assert abs(float(opt.regularizer.get_term(w=w, w_t=wt)) - 0.15) < 1e-7
+
+
+def test_feddyn_save_state_tracks_active_ends():
+    """feddyn.py:51-62: history kept for active ends, None for new ones, others dropped."""
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("feddyn", alpha=0.1)
+    assert opt.alpha == 0.1 and opt.cld_model is None
+    opt.local_param_dict = {"a": {"w": torch.ones(2)}, "b": {"w": torch.zeros(2)}}
+    opt.save_state(S._PRE, active_ends=["b", "c"])
+    assert list(opt.local_param_dict) == ["b", "c"] and opt.local_param_dict["c"] is None
+    opt.save_state(type("S", (), {"value": "post"}), active_ends=[])
+    assert list(opt.local_param_dict) == ["b", "c"]
+    assert opt.do({"w": torch.zeros(2)}, S.SortedCache(), total=5) is None
+    with pytest.raises(AssertionError):
+        opt.do(None, S.SortedCache())
+
+
+def test_scaffold_weight_dict_and_none_paths():
+    """scaffold.py:58-79 weight_dict; do() returns None for an empty cache, total 0 or a
+    control cache whose length differs -- before consuming anything (:113-119)."""
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("scaffold", k=3)
+    opt.save_state(S._PRE, dataset_sizes={"a": 10, "b": 30})
+    assert opt.weight_dict == {"a": 0.5, "b": 1.5}
+    cache, cc = S.SortedCache(), S.SortedCache()
+    cache["a"] = S.TR({"w": torch.ones(2)}, 10)
+    assert opt.do({"w": torch.zeros(2)}, cache, total=10, control_cache=cc) is None
+    assert opt.do({"w": torch.zeros(2)}, cache, total=0, control_cache=cc) is None
+    assert opt.do({"w": torch.zeros(2)}, S.SortedCache(), total=10, control_cache=cc) is None
+    assert len(cache) == 1
+    with pytest.raises(KeyError):
+        opt.do({"w": torch.zeros(2)}, cache, total=10)   # control_cache is required
+
+
+def test_drop_in_keys_cover_reference_provider():
+    """Every key flame's provider registers (optimizers.py:37-48) except fedgft is a drop-in."""
+    from flame_amd.optimizers import DROP_INS
+    assert set(DROP_INS) == {"fedavg", "fedadagrad", "fedadam", "fedyogi", "fedbuff", "fedprox",
+                             "feddyn", "scaffold"}

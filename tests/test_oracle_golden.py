@@ -14,6 +14,10 @@ def make_oracle(sort, **kw):
         return O.OracleFedAvg()
     if sort == "fedbuff":
         return O.OracleFedBuff()
+    if sort == "feddyn":
+        return O.OracleFedDyn(**kw)
+    if sort == "scaffold":
+        return O.OracleScaffold(**kw)
     return O.OracleFedOPT(sort, **kw)
 
 
