@@ -86,7 +86,12 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
 __device__ __forceinline__ uint16_t f32_to_bf16_exact(float x) {  // x already bf16-representable
     return static_cast<uint16_t>(__float_as_uint(x) >> 16);
 }
+// The empty asm pins x as an fp32 VGPR value: without it the backend folds
+// fptrunc(fmul(a, r)) into v_fma_mixlo_f16, which rounds the exact product to
+// fp16 ONCE, while torch rounds the fp32 product to fp16 (two roundings; they
+// differ for an fp32 rate).
 __device__ __forceinline__ float f16_round(float x) {
+    asm volatile("" : "+v"(x));
     return static_cast<float>(static_cast<_Float16>(x));
 }
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
@@ -95,6 +100,7 @@ __device__ __forceinline__ float f16_to_f32(uint16_t h) {
     return static_cast<float>(v);
 }
 __device__ __forceinline__ uint16_t f32_to_f16_bits(float x) {
+    asm volatile("" : "+v"(x));
     _Float16 v = static_cast<_Float16>(x);
     uint16_t h;
     __builtin_memcpy(&h, &v, 2);

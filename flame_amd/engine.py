@@ -505,6 +505,18 @@ def logical_shape(weights, k):
     return weights[k].shape
 
 
+def logical_tensor(weights, k) -> torch.Tensor:
+    """``weights[k]`` in its logical shape (a tiled slab view is untiled into a copy)."""
+    v = weights[k]
+    shape = tuple(logical_shape(weights, k))
+    if tuple(v.shape) == shape:
+        return v
+    n = 1
+    for d in shape:
+        n *= d
+    return v.reshape(-1)[:n].reshape(shape)
+
+
 def first_tmp(weights: dict, rate: float, *, device=None) -> dict:
     """{k: round(v[k] * rate)} as new device tensors (fedbuff.py:139-140,154-155)."""
     device = device or pick_device(weights)

@@ -88,7 +88,7 @@ class FedDyn(FedAvg):
                     outs.append(v)
                     clients.append([w[k]])
                 else:  # reference op (keeps its dtype promotion)
-                    h[k] = v + w[k].to(v.device)
+                    h[k] = v + engine.logical_tensor(w, k).to(v.device)
         if outs:
             engine.reduce_(outs, outs, clients, [1.0])
 
@@ -121,12 +121,5 @@ class FedDyn(FedAvg):
 
 
 def _own_copy(weights, k, device):
-    """A private contiguous device copy of weights[k] (tiled slab views are untiled)."""
-    v = weights[k]
-    shape = engine.logical_shape(weights, k)
-    n = 1
-    for d in shape:
-        n *= d
-    if v.is_cuda and engine.tiled_stride(v, n):
-        return v.reshape(-1)[:n].reshape(shape).to(device, copy=True)
-    return v.to(device, copy=True).contiguous()
+    """A private contiguous device copy of weights[k] in its logical shape."""
+    return engine.logical_tensor(weights, k).to(device, copy=True).contiguous()

@@ -93,8 +93,8 @@ class Scaffold(FedAvg):
             engine.accumulate({k: c[k] for k in same}, [({k: w[k] for k in same}, rate) for w in controls],
                               device=device)
         for w in controls:   # keys with another dtype, in trainer order (reference ops)
-            for k, v in w.items():
+            for k in w.keys():
                 if k in same:
                     continue
-                tmp = v.to(device) * rate
+                tmp = engine.logical_tensor(w, k).to(device) * rate
                 c[k] += tmp.to(dtype=c[k].dtype) if tmp.dtype != c[k].dtype else tmp
