@@ -16,7 +16,9 @@ behind the reduction (flame_amd.shard.ShardedSliceFedAvg).
 Other workloads (DESIGN.md numbers; the driver's bench line is the default):
   --workload fedadam|fedyogi|fedadagrad   config 4 (fused FedOPT kernel, round >= 2)
   --workload hier_fedbuff                 config 5, one GPU's parameter shard
-                                          (4096 clients = 64 middles x 64, bf16)
+                                          (4096 clients = 64 middles x 64, bf16;
+                                          --hier-mode group batches the co-located
+                                          middles: 4 launches per step instead of 130)
   --e2e                                   host-resident updates: H2D + kernel + D2H
 """
 import argparse
@@ -53,6 +55,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--hier-mode", default="group", choices=["group", "serial"],
+                    help="hier_fedbuff: co-located middles in one launch (group) or one by one")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff"])
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
@@ -334,6 +338,7 @@ def bench_hier(args, world, rank, dev):
     Arrival batching (DeferredAggregate) turns each middle's 64 arrivals into one launch."""
     from flame_amd import engine, synth
     from flame_amd.optimizers import optimizer_provider
+    from flame_amd.optimizer.fedbuff import scale_add_many
     M = 64
     C = (args.clients or 4096) // M
     P = args.params or 125_000_000 // 8
@@ -355,7 +360,27 @@ def bench_hier(args, world, rank, dev):
     top_opt = optimizer_provider.get("fedbuff")
     torch.cuda.synchronize()
 
-    def step():
+    def step_group():
+        # the middles of this node queue their arrivals, then ONE launch reduces all of
+        # them (per-middle staleness rates, FLAME_AGG_SEG_RATES) and ONE launch does every
+        # middle's scale_add + delta; the top FedBuff then takes the 64 deltas in one launch
+        aggs = [None] * M
+        for m in range(M):
+            opt = mid_opts[m]
+            for t in range(C):
+                i = m * C + t
+                cache = Cache()
+                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
+                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        res = scale_add_many([({"model": mids[m]}, aggs[m]) for m in range(M)], C, with_delta=True)
+        top_agg = None
+        for m in range(M):
+            cache = Cache()
+            cache[f"mid{m:03d}"] = TR(res[m][1], C, rnd - (m % 2))
+            top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
+        top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
+
+    def step_serial():
         top_agg = None
         deltas = []
         for m in range(M):
@@ -373,6 +398,7 @@ def bench_hier(args, world, rank, dev):
             top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
 
+    step = step_group if args.hier_mode == "group" else step_serial
     elapsed, events = timed(world, args.steps, args.warmup, step)
     red = kernel_stats(events, "flame_agg_reduce")
     sa = kernel_stats(events, "flame_fedbuff_scale_add")
@@ -382,7 +408,8 @@ def bench_hier(args, world, rank, dev):
             "metric": "aggregated params/sec (device-resident), hierarchical FedBuff shard",
             "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
-            "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU"},
+            "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU",
+                                        "middles": args.hier_mode},
             "kernels": {"flame_agg_reduce": red, "flame_fedbuff_scale_add": sa,
                         "kernel_ms_per_step": per_step_kernel * 1e3,
                         "kernel_client_params_per_s": M * C * P / per_step_kernel},

@@ -331,6 +331,10 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const int64_t coff = client_offset<DT>(sg, chunk);
     const bool init_first = (flags & FLAME_AGG_INIT_FIRST) != 0;
+    if (flags & FLAME_AGG_SEG_RATES) {  // one rate row per segment
+        if (r32) r32 += static_cast<int64_t>(s) * n_clients;
+        if (r64) r64 += static_cast<int64_t>(s) * n_clients;
+    }
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     A acc[kVPT][EPT];
     const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
@@ -645,6 +649,8 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     if (rc) return rc;
     if ((flags & FLAME_AGG_INIT_FIRST) && n_clients < 1)
         return set_err(FLAME_EINVAL, "FLAME_AGG_INIT_FIRST needs at least one client");
+    if (flags & ~(FLAME_AGG_INIT_FIRST | FLAME_AGG_SEG_RATES))
+        return set_err(FLAME_EINVAL, "flame_agg_reduce: unknown flags 0x%x", flags);
     if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
         return set_err(FLAME_EINVAL, "rate array is NULL");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

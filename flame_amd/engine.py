@@ -89,12 +89,22 @@ class Plan:
     off_r64: int
 
 
-def plan(code: int, segs: Sequence[Seg], rates: Sequence[float], chunk: Optional[int] = None) -> Plan:
-    """Build the device metadata block for one launch (no GPU needed)."""
+def plan(code: int, segs: Sequence[Seg], rates: Sequence, chunk: Optional[int] = None,
+         seg_rates: bool = False) -> Plan:
+    """Build the device metadata block for one launch (no GPU needed).
+
+    ``rates`` holds one rate per client, or with ``seg_rates`` one row of rates per
+    segment (FLAME_AGG_SEG_RATES)."""
     n_segs = len(segs)
     if n_segs == 0:
         raise ValueError("empty segment list")
-    n = len(rates)
+    if seg_rates:
+        if len(rates) != n_segs or len({len(r) for r in rates}) > 1:
+            raise ValueError("seg_rates: one equal-length rate row per segment")
+        n = len(rates[0])
+        rates = [r for row in rates for r in row]
+    else:
+        n = len(rates)
     chunk = chunk or chunk_elems(code)
     words = []
     begin = 0
@@ -111,12 +121,13 @@ def plan(code: int, segs: Sequence[Seg], rates: Sequence[float], chunk: Optional
     for s in segs:
         words += list(s.clients)
     off_r32 = len(words) * 8
-    r32 = np.asarray([np.float32(r) for r in rates] + ([np.float32(0)] if n % 2 else []), dtype=np.float32)
+    r32 = np.asarray([np.float32(r) for r in rates] + ([np.float32(0)] if len(rates) % 2 else []),
+                     dtype=np.float32)
     words_arr = np.asarray([w if w < (1 << 63) else w - (1 << 64) for w in words], dtype=np.int64)
     r32w = r32.view(np.int64) if r32.size else np.zeros(0, np.int64)
     off_r64 = off_r32 + r32w.size * 8
     r64w = np.asarray([float(r) for r in rates], dtype=np.float64).view(np.int64)
-    meta = np.concatenate([words_arr, r32w, r64w]) if n else words_arr
+    meta = np.concatenate([words_arr, r32w, r64w]) if len(rates) else words_arr
     return Plan(code, meta, n_segs, begin, n, off_clients, off_r32, off_r64)
 
 
@@ -279,11 +290,14 @@ def host_device_pointer(host_ptr: int) -> int:
 
 
 def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients: List[List[torch.Tensor]],
-            rates: Sequence[float], *, init_first: bool = False) -> None:
+            rates: Optional[Sequence[float]], *, init_first: bool = False,
+            seg_rates: Optional[Sequence[Sequence[float]]] = None) -> None:
     """outs[s] = ins[s] (+)= Σ_i round(clients[s][i] * rates[i]) in order (kernel: flame_agg_reduce).
 
     ``outs`` are written in place (they must be contiguous device tensors);
     ``ins`` may be the same tensors (FedAvg mutates base_weights in place).
+    ``seg_rates`` (instead of ``rates``) gives every segment its own rate row:
+    independent reductions with equal client counts share one launch.
     """
     if not outs:
         return
@@ -307,14 +321,19 @@ def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients
                 assert i_t.is_contiguous() and i_t.device == device and i_t.numel() == o.numel()
                 inp = i_t.data_ptr()
             segs.append(Seg(o.numel(), out=o.data_ptr(), inp=inp, clients=row, tile_stride=tstride))
-        p = plan(code, segs, rates)
+        flags = N.FLAME_AGG_INIT_FIRST if init_first else 0
+        if seg_rates is not None:
+            p = plan(code, segs, [seg_rates[s] for s in idx], seg_rates=True)
+            flags |= N.FLAME_AGG_SEG_RATES
+        else:
+            p = plan(code, segs, rates)
         dm = _staging.upload(p.meta, device)
         segp, clp, r32p, r64p = _device_ptrs(dm, p)
         isz = ITEMSIZE[code]
         nbytes = sum(s.numel for s in segs) * isz * (p.n_clients + (1 if init_first else 2))
         with _timed("flame_agg_reduce", device, nbytes):
-            N.check(L.flame_agg_reduce(code, N.FLAME_AGG_INIT_FIRST if init_first else 0, segp, p.n_segs,
-                                       p.n_chunks, clp, p.n_clients, r32p, r64p, _stream_ptr(device)))
+            N.check(L.flame_agg_reduce(code, flags, segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, r64p,
+                                       _stream_ptr(device)))
         keep.append(dm)
     _keepalive(keep, device)
 

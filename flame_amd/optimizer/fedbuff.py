@@ -160,3 +160,70 @@ class FedBuff(AbstractOptimizer):
         for t in targets:
             t.writeback()
         return base_weights
+
+
+# ---------------------------------------------------------------- co-located middle aggregators
+def _uniform(agg: DeferredAggregate) -> bool:
+    """Every queued arrival carries every key in the aggregate's dtype (the one-launch case)."""
+    return all(k in w and w[k].dtype == agg._meta[k][1] for w, _ in agg._pending for k in agg._keys)
+
+
+def flush_aggregates(aggs):
+    """Reduce the queued arrivals of several independent FedBuff aggregates at once.
+
+    For middle aggregators that share a GPU (LIFL-style hierarchies,
+    asyncfl/middle_aggregator.py:164-256): every aggregate keeps its own arrival
+    order and staleness rates (FLAME_AGG_SEG_RATES gives each segment its own
+    rate row), so the result is bit-identical to flushing them one by one, but
+    all aggregates with the same number of queued arrivals and the same start
+    (None-start or accumulate) go in one launch per dtype.
+    """
+    groups = collections.OrderedDict()
+    for a in aggs:
+        if not isinstance(a, DeferredAggregate) or not a._pending:
+            continue
+        if not _uniform(a):
+            a.flush()
+            continue
+        groups.setdefault((a._data is None, len(a._pending)), []).append(a)
+    for (init, _), members in groups.items():
+        if len(members) == 1:
+            members[0].flush()
+            continue
+        device = engine.pick_device(*[w for a in members for w, _ in a._pending])
+        outs, clients, rows = [], [], []
+        for a in members:
+            if init:
+                a._data = collections.OrderedDict(
+                    (k, torch.empty(a._meta[k][0], dtype=a._meta[k][1], device=device)) for k in a._keys)
+            row = [r for _, r in a._pending]
+            for k in a._keys:
+                outs.append(a._data[k])
+                clients.append([w[k] for w, _ in a._pending])
+                rows.append(row)
+        engine.reduce_(outs, None if init else outs, clients, None, init_first=init, seg_rates=rows)
+        for a in members:
+            a._pending = []
+
+
+def scale_add_many(pairs, agg_goal: int, with_delta: bool = False):
+    """``scale_add_agg_weights`` (optionally fused with the middle's delta) for several
+    (base_weights, agg_goal_weights) pairs in one launch per dtype; bit-identical to
+    calling it pair by pair.  Returns the list of base_weights (or of (base, delta))."""
+    flush_aggregates([agg for _, agg in pairs])
+    device = engine.pick_device(*[b for b, _ in pairs], *[a for _, a in pairs])
+    targets, aggs, deltas, results = [], [], [], []
+    for base, agg in pairs:
+        delta = None
+        if with_delta:
+            delta = {k: torch.empty(base[k].shape, dtype=base[k].dtype, device=device) for k in base.keys()}
+        for k in base.keys():
+            targets.append(engine._Target(base[k], device))
+            aggs.append(agg[k])
+            if delta is not None:
+                deltas.append(delta[k])
+        results.append((base, delta) if with_delta else base)
+    engine.scale_add_([t.dev for t in targets], aggs, agg_goal, deltas if with_delta else None)
+    for t in targets:
+        t.writeback()
+    return results

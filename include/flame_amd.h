@@ -56,6 +56,9 @@ extern "C" {
 
 /* flame_agg_reduce flags */
 #define FLAME_AGG_INIT_FIRST 1u  /* no base: acc = tmp(client 0) (fedbuff.py:139-140,154-155) */
+#define FLAME_AGG_SEG_RATES 2u   /* rates are [n_segs][n_clients]: one rate row per segment
+                                    (independent reductions -- e.g. the middle aggregators of
+                                    a node, asyncfl/middle_aggregator.py:164-256 -- in one launch) */
 
 /* flame_fedopt_reduce_adapt variants and flags */
 #define FLAME_FEDADAM 0
@@ -113,6 +116,7 @@ int64_t flame_scale_add_chunk_elems(int dtype);
  *   rates32 : device [n_clients] fp32 rates (float(count/total) or
  *             float(1/sqrt(1+version-tres.version))), used for every dtype but f64.
  *   rates64 : device [n_clients] fp64 rates, used for FLAME_F64 (may be NULL otherwise).
+ *             With FLAME_AGG_SEG_RATES both are [n_segs][n_clients] and segment s uses row s.
  * Per element e of each segment:
  *   acc = in[e] (or tmp_0 with FLAME_AGG_INIT_FIRST);
  *   for i: tmp = round(v_i[e] * rate_i) (ints: trunc(float(v)*rate)); acc = round(acc + tmp)

@@ -1,4 +1,5 @@
 """The C-ABI library loads without a GPU and exports every symbol include/flame_amd.h declares."""
+import ctypes
 import os
 import re
 import subprocess
@@ -73,3 +74,11 @@ def test_fedopt_and_host_entry_points_validate_without_gpu():
     assert L.flame_host_register(None, 0) == _native.FLAME_EINVAL
     assert L.flame_host_unregister(None) == _native.FLAME_EINVAL
     assert L.flame_host_device_pointer(None, None) == _native.FLAME_EINVAL
+
+
+def test_agg_reduce_rejects_unknown_flags_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    fake = ctypes.c_void_p(4096)   # never dereferenced: flags are checked on the host first
+    assert L.flame_agg_reduce(0, 4, fake, 1, 1, None, 0, None, None, None) == _native.FLAME_EINVAL
+    assert b"unknown flags" in L.flame_last_error()

@@ -646,3 +646,56 @@ def test_f16_product_keeps_two_roundings():
     O.reduce_tensor(exp, [vs], [rate])
     S.assert_bitwise("f16 product", {"x": out}, {"x": exp})
     S.assert_bitwise("f16 product torch", {"x": out}, {"x": torch.zeros_like(vs) + vs * rate})
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_middle_group_flush_and_scale_add_many(dtype):
+    """Co-located middle aggregators: flush_aggregates + scale_add_many (FLAME_AGG_SEG_RATES,
+    one launch per group) == each middle's own FedBuff path, bitwise, and == the oracle.
+    Middles differ in staleness and arrival count; round 2 accumulates into round 1's
+    aggregate (non-None start)."""
+    from flame_amd.optimizer.fedbuff import flush_aggregates, scale_add_many
+    O = _oracle()
+    g = torch.Generator().manual_seed(37)
+    shapes = {"w": (3001,), "m": (17, 129)}
+    M, rnd = 6, 9
+    arrivals = [5, 5, 5, 3, 5, 3]
+    base0 = [{k: torch.randn(s, generator=g).to(dtype) for k, s in shapes.items()} for _ in range(M)]
+    ups = [[{k: (torch.randn(s, generator=g) * 1e-2).to(dtype) for k, s in shapes.items()}
+            for _ in range(arrivals[m])] for m in range(M)]
+    vers = [[rnd - ((m + t) % 4) for t in range(arrivals[m])] for m in range(M)]
+
+    def feed(opt, agg, m, t):
+        cache = S.SortedCache()
+        cache["a"] = S.TR({k: v.to(DEV) for k, v in ups[m][t].items()}, 1, vers[m][t])
+        return opt.do(agg, cache, total=1, version=rnd)
+
+    # group path: two rounds of arrivals into the same aggregates, then one group scale_add
+    gopts, gaggs = [make_amd("fedbuff") for _ in range(M)], [None] * M
+    iopts, iaggs = [make_amd("fedbuff") for _ in range(M)], [None] * M
+    oopts, oaggs = [O.OracleFedBuff() for _ in range(M)], [None] * M
+    half = [a // 2 + 1 for a in arrivals]
+    for lo, hi in ((0, None), (None, None)):
+        for m in range(M):
+            rng_t = range(0, half[m]) if lo == 0 else range(half[m], arrivals[m])
+            for t in rng_t:
+                gaggs[m] = feed(gopts[m], gaggs[m], m, t)
+                iaggs[m] = feed(iopts[m], iaggs[m], m, t)
+                cache = S.SortedCache()
+                cache["a"] = S.TR({k: v.clone() for k, v in ups[m][t].items()}, 1, vers[m][t])
+                oaggs[m] = oopts[m].do(oaggs[m], cache, total=1, version=rnd)
+        flush_aggregates(gaggs)
+        assert all(not a._pending for a in gaggs)
+    gb = [{k: v.to(DEV) for k, v in b.items()} for b in base0]
+    ib = [{k: v.to(DEV) for k, v in b.items()} for b in base0]
+    res = scale_add_many(list(zip(gb, gaggs)), 4, with_delta=True)
+    for m in range(M):
+        S.assert_bitwise(f"group agg m{m}", S.to_cpu(gaggs[m].materialize()), S.to_cpu(iaggs[m].materialize()))
+        S.assert_bitwise(f"oracle agg m{m}", S.to_cpu(gaggs[m].materialize()), oaggs[m])
+        _, idelta = iopts[m].scale_add_agg_weights_with_delta(ib[m], iaggs[m], 4)
+        assert res[m][0] is gb[m]
+        S.assert_bitwise(f"group base m{m}", S.to_cpu(gb[m]), S.to_cpu(ib[m]))
+        S.assert_bitwise(f"group delta m{m}", S.to_cpu(res[m][1]), S.to_cpu(idelta))
+        ob = {k: v.clone() for k, v in base0[m].items()}
+        O.OracleFedBuff().scale_add_agg_weights(ob, oaggs[m], 4)
+        S.assert_bitwise(f"oracle base m{m}", S.to_cpu(gb[m]), ob)

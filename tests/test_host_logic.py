@@ -171,3 +171,18 @@ def test_drop_in_keys_cover_reference_provider():
     from flame_amd.optimizers import DROP_INS
     assert set(DROP_INS) == {"fedavg", "fedadagrad", "fedadam", "fedyogi", "fedbuff", "fedprox",
                              "feddyn", "scaffold"}
+
+
+def test_plan_per_segment_rates_layout():
+    """FLAME_AGG_SEG_RATES: rates32/rates64 are [n_segs][n_clients] row-major."""
+    segs = [engine.Seg(10, out=64, inp=64, clients=[128, 256]), engine.Seg(5, out=64, inp=64, clients=[512, 1024])]
+    p = engine.plan(0, segs, [[0.5, 0.25], [1 / 3, 0.1]], seg_rates=True)
+    assert p.n_clients == 2 and p.n_segs == 2
+    r32 = p.meta.view(np.uint8)[p.off_r32:p.off_r32 + 16].view(np.float32)
+    assert list(r32) == [np.float32(0.5), np.float32(0.25), np.float32(1 / 3), np.float32(0.1)]
+    r64 = p.meta.view(np.uint8)[p.off_r64:p.off_r64 + 32].view(np.float64)
+    assert list(r64) == [0.5, 0.25, 1 / 3, 0.1]
+    with pytest.raises(ValueError):
+        engine.plan(0, segs, [[0.5, 0.25], [0.1]], seg_rates=True)
+    with pytest.raises(ValueError):
+        engine.plan(0, segs, [[0.5, 0.25]], seg_rates=True)
