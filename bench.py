@@ -119,15 +119,75 @@ def cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
         torch_cpu.fedavg_round(agg, ups, cts, tot)
         ts.append(time.perf_counter() - t0)
     t = statistics.median(ts)
-    try:
-        model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
-    except Exception:  # noqa: BLE001
-        model = "unknown"
+    model = _cpu_model()
     return {
         "value": n_cpu * P / t, "unit": "client-params/s", "cores": torch.get_num_threads(), "kind": "port",
         "sample": f"reference FedAvg op sequence (fedavg.py:84-104, torch CPU, oracle/torch_cpu.py) over "
                   f"{n_cpu} of the same synthetic clients x {P} fp32 params, median of {rounds} rounds "
                   f"({t:.3f} s/round), {torch.get_num_threads()} threads on {model}; diskcache I/O excluded",
+    }
+
+
+def _cpu_model():
+    try:
+        return [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
+    except Exception:  # noqa: BLE001
+        return "unknown"
+
+
+def cpu_baseline_fedopt(sort, host_row, n, P, base0, counts, n_cpu, rounds):
+    """FedAvg over a client sample + one adaptive step (fedopt.py:102-129), reference op
+    sequence on host cores; value = sampled client-params / time of that round."""
+    from oracle import torch_cpu
+    n_cpu = min(n_cpu, n)
+    ups = [{"model": host_row(i)} for i in range(n_cpu)]
+    cts = [int(c) for c in counts[:n_cpu]]
+    tot = sum(cts)
+    cur = {"model": base0.cpu()}
+    ts, ta = [], []
+    for r in range(rounds + 1):
+        agg = {"model": cur["model"].clone()}
+        t0 = time.perf_counter()
+        torch_cpu.fedavg_round(agg, ups, cts, tot)
+        t1 = time.perf_counter()
+        torch_cpu.fedopt_adapt(sort, agg, cur, {}, {}, 0.9, 0.99, 1e-2, 1e-3)
+        t2 = time.perf_counter()
+        if r:
+            ts.append(t2 - t0)
+            ta.append(t2 - t1)
+    t = statistics.median(ts)
+    return {
+        "value": n_cpu * P / t, "unit": "client-params/s", "cores": torch.get_num_threads(), "kind": "port",
+        "sample": f"reference {sort} op sequence (fedavg.py:84-104 + fedopt.py:102-129, torch CPU, "
+                  f"oracle/torch_cpu.py): FedAvg over {n_cpu} of the same synthetic clients x {P} fp32 params "
+                  f"+ one adaptive step, median of {rounds} ({t:.3f} s/round, of which adapt "
+                  f"{statistics.median(ta):.3f} s), {torch.get_num_threads()} threads on {_cpu_model()}",
+    }
+
+
+def cpu_baseline_hier(rows, P, stale, rnd, rounds):
+    """One middle aggregator of config 5 on host cores: FedBuff per arrival
+    (fedbuff.py:94-96,136-157) + scale_add (:122-127) + the middle's delta
+    (asyncfl/middle_aggregator.py:221-226, common/util.py:152-159)."""
+    from oracle import torch_cpu
+    C = len(rows)
+    ts = []
+    for _ in range(rounds):
+        base = {"model": rows[0].clone()}
+        t0 = time.perf_counter()
+        agg = None
+        for t in range(C):
+            agg = torch_cpu.fedbuff_step(agg, {"model": rows[t]}, rnd, rnd - stale[t])
+        prev = {"model": base["model"].clone()}
+        torch_cpu.fedbuff_scale_add(base, agg, C)
+        _ = {k: base[k] - prev[k] for k in base}
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    return {
+        "value": C * P / t, "unit": "client-params/s", "cores": torch.get_num_threads(), "kind": "port",
+        "sample": f"one middle aggregator: reference FedBuff op sequence over {C} arrivals x {P} bf16 params "
+                  f"+ scale_add + delta (torch CPU, oracle/torch_cpu.py), median of {rounds} ({t:.3f} s), "
+                  f"{torch.get_num_threads()} threads on {_cpu_model()}",
     }
 
 
@@ -286,6 +346,9 @@ def main():
         cpu = None
         if world == 1 and args.cpu_clients > 0 and args.workload == "fedavg":
             cpu = cpu_baseline(host_row, n, P, base0, counts, args.cpu_clients, args.cpu_rounds)
+        elif world == 1 and args.cpu_clients > 0:
+            cpu = cpu_baseline_fedopt(args.workload, host_row, n, P, base0, counts, args.cpu_clients,
+                                      args.cpu_rounds)
         ceiling = read_ceiling(slab_buf) if world == 1 else None
         # a piece-pipelined step has several launches: price the step's kernels as one
         launches_per_step = ks["launches"] / args.steps
@@ -356,6 +419,8 @@ def bench_hier(args, world, rank, dev):
     mids = [gw.clone() for _ in range(M)]
     stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
     rnd = 10
+    full = torch.empty(P * world, dtype=dt, device=dev) if world > 1 else None
+    full_cpu = torch.empty(P * world, dtype=dt) if world > 1 else None
     mid_opts = [optimizer_provider.get("fedbuff") for _ in range(M)]
     top_opt = optimizer_provider.get("fedbuff")
     torch.cuda.synchronize()
@@ -379,6 +444,16 @@ def bench_hier(args, world, rank, dev):
             cache[f"mid{m:03d}"] = TR(res[m][1], C, rnd - (m % 2))
             top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
+        gather()
+
+    def gather():
+        # config 5 is parameter-sharded: every rank reassembles the global bf16 model
+        if world > 1:
+            import torch.distributed as dist
+            if dist.get_backend() == "gloo":
+                dist.all_gather_into_tensor(full_cpu, gw.cpu())
+            else:
+                dist.all_gather_into_tensor(full, gw)
 
     def step_serial():
         top_agg = None
@@ -397,9 +472,14 @@ def bench_hier(args, world, rank, dev):
             cache[f"mid{m:03d}"] = TR(delta, C, rnd - (m % 2))
             top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
+        gather()
 
     step = step_group if args.hier_mode == "group" else step_serial
     elapsed, events = timed(world, args.steps, args.warmup, step)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_clients > 0:
+        cpu = cpu_baseline_hier([store.read(i, "model").cpu() for i in range(C)], P, stale[:C], rnd,
+                                args.cpu_rounds)
     red = kernel_stats(events, "flame_agg_reduce")
     sa = kernel_stats(events, "flame_fedbuff_scale_add")
     if rank == 0:
@@ -410,9 +490,13 @@ def bench_hier(args, world, rank, dev):
             "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
             "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU",
                                         "middles": args.hier_mode},
+            "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "flame_agg_reduce"},
             "kernels": {"flame_agg_reduce": red, "flame_fedbuff_scale_add": sa,
                         "kernel_ms_per_step": per_step_kernel * 1e3,
                         "kernel_client_params_per_s": M * C * P / per_step_kernel},
+            "cpu_baseline": cpu,
         }), flush=True)
 
 
