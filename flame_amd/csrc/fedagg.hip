@@ -50,12 +50,25 @@ namespace {
 #ifndef FLAME_NT
 #define FLAME_NT 1        // non-temporal client loads (read once)
 #endif
+#ifndef FLAME_ST_NT
+#define FLAME_ST_NT 4     // output store policy: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 sc0 sc1 nt (see st_v)
+#endif
+#ifndef FLAME_NOSTORE
+#define FLAME_NOSTORE 0   // DIAGNOSTIC sweep variant only: skip the reduction's output store
+#endif
+#ifndef FLAME_WGC
+#define FLAME_WGC 1       // chunks per workgroup of the reduction kernel
+#endif
+#ifndef FLAME_DEFER_ST
+#define FLAME_DEFER_ST 0  // 1: store a workgroup's FLAME_WGC output chunks together at its end
+#endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
 
 constexpr int kBlock = FLAME_BLOCK;
 constexpr int kVPT = FLAME_VPT;
+constexpr int kWGC = FLAME_WGC;
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -184,9 +197,23 @@ __device__ __forceinline__ V16 ld_v(const void* p) {
     V16 r; r.w[0] = x[0]; r.w[1] = x[1]; r.w[2] = x[2]; r.w[3] = x[3];
     return r;
 }
+// Output stores are write-through (sc0 sc1 nt): measured +2 % on config 3 and +4 % on
+// 64-client bf16 against plain / nt stores, whose dirty L2 lines are written back
+// interleaved with the client read stream (profiles/r01_scan5_*.log).  Inline asm
+// because no builtin sets sc0/sc1; `s_nop 1` covers the store-data hazard.
 __device__ __forceinline__ void st_v(void* p, const V16& v) {
     u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+#if FLAME_ST_NT == 1
+    __builtin_nontemporal_store(x, G(reinterpret_cast<u4*>(p)));
+#elif FLAME_ST_NT == 2
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#elif FLAME_ST_NT == 3
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#elif FLAME_ST_NT == 4
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#else
     *G(reinterpret_cast<u4*>(p)) = x;
+#endif
 }
 template <typename T> __device__ __forceinline__ T ld1(const T* p) { return *G(p); }
 template <typename T> __device__ __forceinline__ void st1(T* p, T x) { *G(p) = x; }
@@ -313,21 +340,24 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
     }
 }
 
+// One chunk of one segment: acc = base (or client 0), reduce every client in order.
+// Full, aligned chunks hand their output vectors back (ov / op) so the caller can
+// store them; tails and misaligned views store element-wise here.
 template <int DT, int CU>
-__global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment* __restrict__ segs, int n_segs,
-                                                            const uint64_t* __restrict__ clients, int n_clients,
-                                                            const float* __restrict__ r32,
-                                                            const double* __restrict__ r64, unsigned flags) {
+__device__ __forceinline__ bool reduce_chunk(const flame_segment* __restrict__ segs, int n_segs,
+                                             const uint64_t* __restrict__ clients, int n_clients,
+                                             const float* __restrict__ r32, const double* __restrict__ r64,
+                                             unsigned flags, int64_t chunk, V16 (&ov)[kVPT],
+                                             typename Tr<DT>::T*& op) {
     using X = Tr<DT>;
     using T = typename X::T;
     using A = typename X::A;
     constexpr int EPT = X::EPT;
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
-    const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
-    if (e0 >= sg.numel) return;
+    if (e0 >= sg.numel) return false;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const int64_t coff = client_offset<DT>(sg, chunk);
     const bool init_first = (flags & FLAME_AGG_INIT_FIRST) != 0;
@@ -338,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     A acc[kVPT][EPT];
     const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
-    T* op = reinterpret_cast<T*>(sg.out) + e0;
+    op = reinterpret_cast<T*>(sg.out) + e0;
     if (vec) {
         if (!init_first) {
 #pragma unroll
@@ -355,23 +385,71 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
             T o[EPT];
 #pragma unroll
             for (int j = 0; j < EPT; ++j) o[j] = X::st(acc[v][j]);
-            st_v(op + v * VS, pack<T, EPT>(o));
+            ov[v] = pack<T, EPT>(o);
         }
-    } else {
-        if (!init_first) {
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-                for (int j = 0; j < EPT; ++j)
-                    acc[v][j] = X::ld((e0 + v * VS + j < sg.numel) ? ld1(bp + v * VS + j) : T(0));
-        }
-        reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel, coff);
+        return true;
+    }
+    if (!init_first) {
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
             for (int j = 0; j < EPT; ++j)
-                if (e0 + v * VS + j < sg.numel) st1(op + v * VS + j, X::st(acc[v][j]));
+                acc[v][j] = X::ld((e0 + v * VS + j < sg.numel) ? ld1(bp + v * VS + j) : T(0));
     }
+    reduce_clients<DT, 1, false>(acc, init_first, cp, n_clients, r32, r64, e0, sg.numel, coff);
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+            if (e0 + v * VS + j < sg.numel) st1(op + v * VS + j, X::st(acc[v][j]));
+    return false;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_chunk(T* op, const V16 (&ov)[kVPT]) {
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * (16 / sizeof(T));
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v) {
+#if FLAME_NOSTORE
+        if (__builtin_expect(ov[v].w[0] == 0x12345u && ov[v].w[1] == 0x54321u, 0))   // keeps the math live
+#endif
+        st_v(op + v * VS, ov[v]);
+    }
+}
+
+// Workgroup w reduces chunks [w*kWGC, (w+1)*kWGC).  With FLAME_DEFER_ST the full
+// chunks' output vectors stay in registers and are stored together at the end.
+template <int DT, int CU>
+__global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                            const uint64_t* __restrict__ clients, int n_clients,
+                                                            const float* __restrict__ r32,
+                                                            const double* __restrict__ r64, unsigned flags,
+                                                            int64_t n_chunks) {
+    using T = typename Tr<DT>::T;
+#if FLAME_DEFER_ST
+    V16 ov[kWGC][kVPT];
+    T* op[kWGC];
+    bool full[kWGC];
+#pragma unroll
+    for (int k = 0; k < kWGC; ++k) {
+        const int64_t chunk = static_cast<int64_t>(blockIdx.x) * kWGC + k;
+        full[k] = chunk < n_chunks &&
+                  reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov[k], op[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kWGC; ++k)
+        if (full[k]) store_chunk(op[k], ov[k]);
+#else
+#pragma unroll 1
+    for (int k = 0; k < kWGC; ++k) {
+        const int64_t chunk = static_cast<int64_t>(blockIdx.x) * kWGC + k;
+        if (chunk >= n_chunks) break;
+        V16 ov[kVPT];
+        T* op;
+        if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov, op))
+            store_chunk(op, ov);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- fused FedOPT (fp32)
@@ -654,26 +732,26 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
         return set_err(FLAME_EINVAL, "rate array is NULL");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const dim3 grid(static_cast<unsigned>((n_chunks + kWGC - 1) / kWGC)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
     switch (dtype) {
     case FLAME_F32:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_BF16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_F16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_F64:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_I64:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_I32:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_agg_reduce: unsupported dtype %d", dtype);

@@ -39,6 +39,17 @@ VARIANTS = {
     "c16_2": {"FLAME_CU16": 2},
     "c16_4v2": {"FLAME_CU16": 4, "FLAME_VPT": 2},
     "cu16b128": {"FLAME_CU": 16, "FLAME_BLOCK": 128},
+    "stplain": {"FLAME_ST_NT": 0},
+    "stnt": {"FLAME_ST_NT": 1},
+    "nostore": {"FLAME_NOSTORE": 1},   # diagnostic: output not written (not checked)
+    "stsc1": {"FLAME_ST_NT": 2},
+    "stsc01": {"FLAME_ST_NT": 3},
+    "stsc01nt": {"FLAME_ST_NT": 4},
+    "wgc2": {"FLAME_WGC": 2},
+    "wgc4": {"FLAME_WGC": 4},
+    "wgc2d": {"FLAME_WGC": 2, "FLAME_DEFER_ST": 1},
+    "wgc4d": {"FLAME_WGC": 4, "FLAME_DEFER_ST": 1},
+    "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
 }
 
 
@@ -175,7 +186,7 @@ def main():
     for nm in names:
         launch(nm)
         torch.cuda.synchronize()
-        if args.kernel != "agg" or nm == "probe" or nm.endswith(":tiled"):
+        if args.kernel != "agg" or nm == "probe" or nm.endswith(":tiled") or nm.startswith("nostore"):
             continue
         if ref is None:
             ref = out.clone()
