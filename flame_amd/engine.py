@@ -61,6 +61,9 @@ def rate32(rate: float) -> float:
 
 
 # ------------------------------------------------------------------ planning (host only)
+SEG_WORDS = 10  # int64 words per flame_segment
+
+
 @dataclass
 class Seg:
     numel: int
@@ -106,28 +109,29 @@ def plan(code: int, segs: Sequence[Seg], rates: Sequence, chunk: Optional[int] =
     else:
         n = len(rates)
     chunk = chunk or chunk_elems(code)
-    words = []
+    head = np.zeros((n_segs, SEG_WORDS), dtype=np.uint64)
+    table = np.empty((n_segs, n), dtype=np.uint64)
     begin = 0
-    for s in segs:
+    for i, s in enumerate(segs):
         if len(s.clients) != n:
             raise ValueError("every segment needs one pointer per client")
-        unaligned = any(p % VEC_BYTES for p in s.pointers() if p)
-        words += [s.out, s.inp, s.cur, s.cur_out, s.m, s.v, s.numel, begin,
-                  N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride]
+        row = table[i]
+        row[:] = s.clients
+        fixed = (s.out, s.inp, s.cur, s.cur_out, s.m, s.v)
+        unaligned = bool(np.any(row % VEC_BYTES)) or any(p % VEC_BYTES for p in fixed if p)
+        head[i] = (*fixed, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride)
         begin += -(-s.numel // chunk) if s.numel > 0 else 0
     if begin == 0:
         begin = 1  # all segments empty: one (idle) chunk keeps the launch valid
-    off_clients = len(words) * 8
-    for s in segs:
-        words += list(s.clients)
-    off_r32 = len(words) * 8
-    r32 = np.asarray([np.float32(r) for r in rates] + ([np.float32(0)] if len(rates) % 2 else []),
-                     dtype=np.float32)
-    words_arr = np.asarray([w if w < (1 << 63) else w - (1 << 64) for w in words], dtype=np.int64)
-    r32w = r32.view(np.int64) if r32.size else np.zeros(0, np.int64)
-    off_r64 = off_r32 + r32w.size * 8
-    r64w = np.asarray([float(r) for r in rates], dtype=np.float64).view(np.int64)
-    meta = np.concatenate([words_arr, r32w, r64w]) if len(rates) else words_arr
+    off_clients = head.size * 8
+    off_r32 = off_clients + table.size * 8
+    r64 = np.asarray(rates, dtype=np.float64).reshape(-1)
+    r32 = r64.astype(np.float32)            # RNE, as torch rounds a Python float scalar
+    if r32.size % 2:
+        r32 = np.concatenate([r32, np.zeros(1, np.float32)])
+    off_r64 = off_r32 + r32.size * 4
+    meta = np.concatenate([head.view(np.int64).reshape(-1), table.view(np.int64).reshape(-1),
+                           r32.view(np.int64), r64.view(np.int64)])
     return Plan(code, meta, n_segs, begin, n, off_clients, off_r32, off_r64)
 
 
@@ -307,7 +311,6 @@ def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients
     groups = collections.OrderedDict()
     for s, o in enumerate(outs):
         groups.setdefault(dtype_code(o.dtype), []).append(s)
-    L = N.lib()
     keep = []
     for code, idx in groups.items():
         segs = []
@@ -321,21 +324,25 @@ def reduce_(outs: List[torch.Tensor], ins: Optional[List[torch.Tensor]], clients
                 assert i_t.is_contiguous() and i_t.device == device and i_t.numel() == o.numel()
                 inp = i_t.data_ptr()
             segs.append(Seg(o.numel(), out=o.data_ptr(), inp=inp, clients=row, tile_stride=tstride))
-        flags = N.FLAME_AGG_INIT_FIRST if init_first else 0
-        if seg_rates is not None:
-            p = plan(code, segs, [seg_rates[s] for s in idx], seg_rates=True)
-            flags |= N.FLAME_AGG_SEG_RATES
-        else:
-            p = plan(code, segs, rates)
-        dm = _staging.upload(p.meta, device)
-        segp, clp, r32p, r64p = _device_ptrs(dm, p)
-        isz = ITEMSIZE[code]
-        nbytes = sum(s.numel for s in segs) * isz * (p.n_clients + (1 if init_first else 2))
-        with _timed("flame_agg_reduce", device, nbytes):
-            N.check(L.flame_agg_reduce(code, flags, segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, r64p,
-                                       _stream_ptr(device)))
-        keep.append(dm)
+        _launch_reduce(code, segs, rates if seg_rates is None else [seg_rates[s] for s in idx], device, keep,
+                       init_first=init_first, seg_rates=seg_rates is not None)
     _keepalive(keep, device)
+
+
+def _launch_reduce(code, segs, rates, device, keep, *, init_first=False, seg_rates=False) -> None:
+    """One flame_agg_reduce launch over prepared segments (``keep`` holds what must outlive it)."""
+    L = N.lib()
+    flags = N.FLAME_AGG_INIT_FIRST if init_first else 0
+    if seg_rates:
+        flags |= N.FLAME_AGG_SEG_RATES
+    p = plan(code, segs, rates, seg_rates=seg_rates)
+    dm = _staging.upload(p.meta, device)
+    segp, clp, r32p, r64p = _device_ptrs(dm, p)
+    nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (p.n_clients + (1 if init_first else 2))
+    with _timed("flame_agg_reduce", device, nbytes):
+        N.check(L.flame_agg_reduce(code, flags, segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, r64p,
+                                   _stream_ptr(device)))
+    keep.append(dm)
 
 
 FEDOPT_VARIANT = {"fedadam": N.FLAME_FEDADAM, "fedyogi": N.FLAME_FEDYOGI, "fedadagrad": N.FLAME_FEDADAGRAD}
@@ -465,6 +472,8 @@ def accumulate(agg: dict, entries, *, device=None) -> None:
     if not entries:
         return
     device = device or pick_device(agg, *[w for w, _ in entries])
+    if _accumulate_slab(agg, entries, device):
+        return
     keys = list(agg.keys())
     per_key = collections.OrderedDict()
     for ci, (w, _) in enumerate(entries):
@@ -489,6 +498,46 @@ def accumulate(agg: dict, entries, *, device=None) -> None:
                 t.writeback()
         for k in mixed:
             _accumulate_promoted(agg, k, [entries[ci] for ci in cis], device)
+
+
+def _accumulate_slab(agg: dict, entries, device) -> bool:
+    """Fast path: every entry is the SlotWeights of ONE UpdateSlab whose keys and dtypes are
+    exactly agg's.  Pointer rows are computed from slot numbers (numpy), without touching
+    the per-client views; returns False (nothing done) when the case does not apply."""
+    slab = getattr(entries[0][0], "slab", None)
+    if slab is None or slab.device != device or len(slab.keys) != len(agg):
+        return False
+    nk = len(slab.keys)
+    for w, _ in entries:
+        if getattr(w, "slab", None) is not slab or len(w) != nk:
+            return False
+    layouts = {}
+    for k in agg.keys():
+        if k not in slab.meta:
+            return False
+        lay = slab.key_layout(k)
+        if lay[0] != agg[k].dtype or agg[k].numel() != lay[1]:
+            return False
+        layouts[k] = lay
+    slots = np.fromiter((w.slot for w, _ in entries), dtype=np.uint64, count=len(entries))
+    rates = [r for _, r in entries]
+    targets = {k: _Target(agg[k], device) for k in agg.keys()}
+    groups = collections.OrderedDict()
+    for k in agg.keys():
+        groups.setdefault(dtype_code(agg[k].dtype), []).append(k)
+    keep = []
+    for code, ks in groups.items():
+        segs = []
+        for k in ks:
+            _, n, base, slot_bytes, tile_bytes = layouts[k]
+            o = targets[k].dev
+            segs.append(Seg(n, out=o.data_ptr(), inp=o.data_ptr(),
+                            clients=np.uint64(base) + slots * np.uint64(slot_bytes), tile_stride=tile_bytes))
+        _launch_reduce(code, segs, rates, device, keep)
+    _keepalive(keep, device)
+    for t in targets.values():
+        t.writeback()
+    return True
 
 
 def _accumulate_promoted(agg: dict, k, entries, device) -> None:

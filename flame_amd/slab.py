@@ -37,7 +37,7 @@ class SlotWeights(dict):
     """The weights dict of one slab slot: {key: tiled view}; ``shapes`` holds the model
     shapes; releases the slot when dropped."""
 
-    __slots__ = ("__weakref__", "_release", "shapes")
+    __slots__ = ("__weakref__", "_release", "shapes", "slab", "slot")
 
     def __del__(self):
         rel = getattr(self, "_release", None)
@@ -98,7 +98,16 @@ class UpdateSlab:
             w[k] = self.storage[dt][tile0:tile0 + tiles, slot, :]
         w._release = lambda s=slot: self._release(s)
         w.shapes = {k: self.meta[k][1] for k in self.keys}
+        w.slab, w.slot = self, slot     # lets the engine compute pointer rows without touching views
         return w
+
+    def key_layout(self, key: str):
+        """(dtype, numel, address of slot 0's first tile, bytes between slots, bytes between tiles)."""
+        dt, _, n, tile0, _ = self.meta[key]
+        st = self.storage[dt]
+        T = st.shape[2]
+        isz = st.element_size()
+        return dt, n, st.data_ptr() + tile0 * self.capacity * T * isz, T * isz, self.capacity * T * isz
 
     def slot_view(self, slot: int, key: str) -> torch.Tensor:
         dt, _, _, tile0, tiles = self.meta[key]
