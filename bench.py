@@ -55,8 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--hier-mode", default="group", choices=["group", "serial"],
-                    help="hier_fedbuff: co-located middles in one launch (group) or one by one")
+    ap.add_argument("--hier-mode", default="fused", choices=["fused", "group", "serial"],
+                    help="hier_fedbuff: the node's middles AND the top in one pass (fused, "
+                         "flame_hier_fedbuff), co-located middles in one launch (group) or one by one")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff"])
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
@@ -474,16 +475,43 @@ def bench_hier(args, world, rank, dev):
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
         gather()
 
-    step = step_group if args.hier_mode == "group" else step_serial
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+
+    def step_fused():
+        # every middle's arrivals queue (DeferredAggregate); ONE launch then reduces each
+        # middle, applies its scale_add, feeds its delta to the top FedBuff and applies the
+        # top's scale_add -- the middle aggregates and deltas stay in registers
+        aggs = [None] * M
+        for m in range(M):
+            opt = mid_opts[m]
+            for t in range(C):
+                i = m * C + t
+                cache = Cache()
+                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
+                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        hierarchy_round([({"model": mids[m]}, aggs[m], C, rnd - (m % 2)) for m in range(M)], None,
+                        version=rnd, top_weights={"model": gw}, top_goal=M)
+        gather()
+
+    step = {"fused": step_fused, "group": step_group, "serial": step_serial}[args.hier_mode]
     elapsed, events = timed(world, args.steps, args.warmup, step)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_clients > 0:
         cpu = cpu_baseline_hier([store.read(i, "model").cpu() for i in range(C)], P, stale[:C], rnd,
                                 args.cpu_rounds)
-    red = kernel_stats(events, "flame_agg_reduce")
-    sa = kernel_stats(events, "flame_fedbuff_scale_add")
+    names = ("flame_hier_fedbuff",) if args.hier_mode == "fused" else ("flame_agg_reduce", "flame_fedbuff_scale_add")
+    kst = {nm: kernel_stats(events, nm) for nm in names}
+    red = kst[names[0]]
+    traffic = None
+    if rank == 0 and args.hier_mode == "fused":
+        try:
+            for tr in json.load(open(args.traffic))["entries"]:
+                if tr.get("kernel") == names[0] and tr.get("clients") == M * C and tr.get("params") == P:
+                    traffic = tr["hbm_bytes_per_launch"]
+        except Exception:  # noqa: BLE001
+            pass
     if rank == 0:
-        per_step_kernel = (red["avg_s"] * red["launches"] + sa["avg_s"] * sa["launches"]) / args.steps
+        per_step_kernel = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         print(json.dumps({
             "metric": "aggregated params/sec (device-resident), hierarchical FedBuff shard",
             "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
@@ -491,10 +519,9 @@ def bench_hier(args, world, rank, dev):
             "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU",
                                         "middles": args.hier_mode},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": None,
-                         "kernel": "flame_agg_reduce"},
-            "kernels": {"flame_agg_reduce": red, "flame_fedbuff_scale_add": sa,
-                        "kernel_ms_per_step": per_step_kernel * 1e3,
+                         "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": names[0]},
+            "kernels": {**kst, "kernel_ms_per_step": per_step_kernel * 1e3,
                         "kernel_client_params_per_s": M * C * P / per_step_kernel},
             "cpu_baseline": cpu,
         }), flush=True)

@@ -62,6 +62,15 @@ namespace {
 #ifndef FLAME_DEFER_ST
 #define FLAME_DEFER_ST 0  // 1: store a workgroup's FLAME_WGC output chunks together at its end
 #endif
+#ifndef FLAME_HCU16
+#define FLAME_HCU16 FLAME_CU16  // client unroll of the hierarchy kernel for 16-bit dtypes
+#endif
+#ifndef FLAME_HWPE
+#define FLAME_HWPE 0      // hierarchy kernel: minimum waves per SIMD to compile for (0 = compiler's choice)
+#endif
+#ifndef FLAME_HPF
+#define FLAME_HPF 0       // hierarchy kernel: load each middle's weights before its arrival loop
+#endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
@@ -230,7 +239,8 @@ __device__ __forceinline__ V16 pack(const T (&x)[EPT]) {
 }
 
 // Wave-uniform segment lookup: largest s with segs[s].chunk_begin <= chunk.
-__device__ __forceinline__ int find_segment(const flame_segment* __restrict__ segs, int n_segs, int64_t chunk) {
+template <typename SEG>
+__device__ __forceinline__ int find_segment(const SEG* __restrict__ segs, int n_segs, int64_t chunk) {
     int lo = 0, hi = n_segs - 1;
     while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
@@ -241,8 +251,8 @@ __device__ __forceinline__ int find_segment(const flame_segment* __restrict__ se
 
 // Byte offset of this lane's first element inside every client's data for the
 // workgroup's chunk: contiguous (e0 * sizeof) or tiled (chunk * client_tile_stride + lane).
-template <int DT>
-__device__ __forceinline__ int64_t client_offset(const flame_segment& sg, int64_t chunk) {
+template <int DT, typename SEG>
+__device__ __forceinline__ int64_t client_offset(const SEG& sg, int64_t chunk) {
     using T = typename Tr<DT>::T;
     const int64_t cl = chunk - sg.chunk_begin;
     const int64_t lane_elem = static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
@@ -658,6 +668,158 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
     }
 }
 
+// ---------------------------------------------------------------- co-located FedBuff hierarchy
+// One pass over a node's whole two-level asynchronous hierarchy:
+// for each middle m in the order the top receives their deltas --
+//   agg_m  = FedBuff None-start reduce of its C queued arrivals      (fedbuff.py:89-97,136-157)
+//   w_m'   = w_m + agg_m / goal_m,  delta_m = w_m' - w_m             (fedbuff.py:122-127,
+//                                     asyncfl/middle_aggregator.py:221-226,246, common/util.py:152-159)
+//   top    = tmp(delta_m, rate_m) [None start] or top + tmp(...)     (fedbuff.py:96,136-157, top role)
+// then top_w += top / top_goal (fedbuff.py:122-127).  Every op rounds in the tensor's
+// dtype exactly as the separate launches do, so results are bit-identical to them; the
+// middle aggregates and deltas never touch HBM (deltas are stored only if asked for).
+#if FLAME_HWPE
+#define FLAME_HIER_ATTR __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FLAME_HWPE, 8)))
+#else
+#define FLAME_HIER_ATTR __launch_bounds__(kBlock)
+#endif
+template <int DT, int CU>
+__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
+                                                              int n_mids, int n_clients,
+                                                              const uint64_t* __restrict__ mid_w,
+                                                              const uint64_t* __restrict__ mid_delta,
+                                                              const uint64_t* __restrict__ clients,
+                                                              const float* __restrict__ mid_rates,
+                                                              const float* __restrict__ mid_goal,
+                                                              const float* __restrict__ top_rates, float top_goal,
+                                                              unsigned flags) {
+    using X = Tr<DT>;
+    using S = SA<DT>;
+    using T = typename X::T;
+    using A = typename X::A;
+    constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_hier_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    const int64_t coff = client_offset<DT>(sg, chunk);
+    const uint64_t* wrow = mid_w + static_cast<int64_t>(s) * n_mids;
+    const uint64_t* drow = mid_delta ? mid_delta + static_cast<int64_t>(s) * n_mids : nullptr;
+    const uint64_t* crow = clients + static_cast<int64_t>(s) * n_mids * n_clients;
+    const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    A top[kVPT][EPT];
+    bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
+    const T* tin = reinterpret_cast<const T*>(sg.top_agg_in) + e0;
+    if (vec) {
+        if (have_top) {
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) {
+                T b[EPT];
+                unpack<T, EPT>(ld_v(tin + v * VS), b);
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) top[v][j] = X::ld(b[j]);
+            }
+        }
+#pragma unroll 1
+        for (int m = 0; m < n_mids; ++m) {
+            T* wp = reinterpret_cast<T*>(wrow[m]) + e0;
+#if FLAME_HPF
+            V16 wv[kVPT];
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) wv[v] = ld_v(wp + v * VS);
+#endif
+            A acc[kVPT][EPT];
+            reduce_clients<DT, CU, true>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+                                         mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
+                                         coff);
+            T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+            const float g = mid_goal[m], rt = top_rates[m];
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) {
+                T w[EPT], d[EPT];
+#if FLAME_HPF
+                unpack<T, EPT>(wv[v], w);
+#else
+                unpack<T, EPT>(ld_v(wp + v * VS), w);
+#endif
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) {
+                    S::op(w[j], X::st(acc[v][j]), g, static_cast<double>(g), &d[j]);
+                    const A t = X::tmp(d[j], rt, 0.0);
+                    top[v][j] = have_top ? X::add(top[v][j], t) : t;
+                }
+                st_v(wp + v * VS, pack<T, EPT>(w));
+                if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
+            }
+            have_top = true;
+        }
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            T o[EPT];
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) o[j] = X::st(top[v][j]);
+            if (sg.top_agg_out) st_v(reinterpret_cast<T*>(sg.top_agg_out) + e0 + v * VS, pack<T, EPT>(o));
+            if (flags & FLAME_HIER_TOP_APPLY) {
+                T* gp = reinterpret_cast<T*>(sg.top_w) + e0 + v * VS;
+                T gw[EPT];
+                unpack<T, EPT>(ld_v(gp), gw);
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) S::op(gw[j], o[j], top_goal, static_cast<double>(top_goal), nullptr);
+                st_v(gp, pack<T, EPT>(gw));
+            }
+        }
+        return;
+    }
+    // tails / misaligned views: element-wise, same op sequence
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int64_t o = v * VS + j;
+            if (have_top && e0 + o < sg.numel) top[v][j] = X::ld(ld1(tin + o));
+        }
+#pragma unroll 1
+    for (int m = 0; m < n_mids; ++m) {
+        A acc[kVPT][EPT];
+        reduce_clients<DT, 1, false>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+                                     mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel, coff);
+        T* wp = reinterpret_cast<T*>(wrow[m]) + e0;
+        T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+        const float g = mid_goal[m], rt = top_rates[m];
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                const int64_t o = v * VS + j;
+                if (e0 + o >= sg.numel) continue;
+                T w = ld1(wp + o), d;
+                S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
+                st1(wp + o, w);
+                if (dp) st1(dp + o, d);
+                const A t = X::tmp(d, rt, 0.0);
+                top[v][j] = have_top ? X::add(top[v][j], t) : t;
+            }
+        have_top = true;
+    }
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int64_t o = v * VS + j;
+            if (e0 + o >= sg.numel) continue;
+            const T t = X::st(top[v][j]);
+            if (sg.top_agg_out) st1(reinterpret_cast<T*>(sg.top_agg_out) + e0 + o, t);
+            if (flags & FLAME_HIER_TOP_APPLY) {
+                T* gp = reinterpret_cast<T*>(sg.top_w) + e0 + o;
+                T gw = ld1(gp);
+                S::op(gw, t, top_goal, static_cast<double>(top_goal), nullptr);
+                st1(gp, gw);
+            }
+        }
+}
+
 // ---------------------------------------------------------------- synthetic generator
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -680,6 +842,7 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 
 constexpr int kClientUnroll = FLAME_CU;
 constexpr int kClientUnroll16 = FLAME_CU16;
+constexpr int kHierUnroll16 = FLAME_HCU16;
 
 int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
     if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
@@ -815,6 +978,42 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs
         return set_err(FLAME_ENOTSUP, "flame_fedbuff_scale_add: dtype %d not supported (integer tensors raise in the reference)", dtype);
     }
     return check_launch("flame_fedbuff_scale_add");
+}
+
+int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs, int32_t n_segs, int64_t n_chunks,
+                       int32_t n_mids, int32_t n_clients, const void* const* mid_w, const void* const* mid_delta,
+                       const void* const* clients, const float* mid_rates, const float* mid_goal,
+                       const float* top_rates, float top_goal, void* stream) {
+    if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
+    if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
+    if (n_mids < 1 || n_clients < 1) return set_err(FLAME_EINVAL, "flame_hier_fedbuff: need >= 1 middle and >= 1 arrival per middle");
+    if (!mid_w || !clients || !mid_rates || !mid_goal || !top_rates)
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff: NULL table");
+    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff: unknown flags 0x%x", flags);
+    if ((flags & FLAME_HIER_TOP_APPLY) && top_goal == 0.f) return set_err(FLAME_EINVAL, "top agg_goal must be nonzero");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    auto w = reinterpret_cast<const uint64_t*>(mid_w);
+    auto d = reinterpret_cast<const uint64_t*>(mid_delta);
+    auto cl = reinterpret_cast<const uint64_t*>(clients);
+    switch (dtype) {
+    case FLAME_F32:
+        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, n_mids,
+                           n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+        break;
+    case FLAME_BF16:
+        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_BF16, kHierUnroll16>), grid, block, 0, st, segs, n_segs,
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+        break;
+    case FLAME_F16:
+        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_F16, kHierUnroll16>), grid, block, 0, st, segs, n_segs,
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+        break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
+    }
+    return check_launch("flame_hier_fedbuff");
 }
 
 int flame_host_register(void* host, uint64_t nbytes) {

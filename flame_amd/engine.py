@@ -431,6 +431,108 @@ def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
     _keepalive(keep, device)
 
 
+# ------------------------------------------------------------------ co-located FedBuff hierarchy
+HSEG_WORDS = N.HIER_SEGMENT_INT64S
+
+
+@dataclass
+class HierSeg:
+    """One tensor of the hierarchy: the top's pointers + per-middle weight / delta pointers
+    and the [n_mids * n_clients] arrival pointers (middle-major, arrival order)."""
+    numel: int
+    mid_w: Sequence[int]
+    clients: Sequence[int]
+    mid_delta: Optional[Sequence[int]] = None
+    top_w: int = 0
+    top_in: int = 0
+    top_out: int = 0
+    tile_stride: int = 0
+
+
+@dataclass
+class HierPlan:
+    code: int
+    meta: np.ndarray
+    n_segs: int
+    n_chunks: int
+    n_mids: int
+    n_clients: int
+    offs: dict            # byte offsets of the tables inside the device copy of ``meta``
+
+
+def _f32_words(x) -> np.ndarray:
+    a = np.asarray(x, dtype=np.float64).reshape(-1).astype(np.float32)   # RNE, as torch rounds scalars
+    if a.size % 2:
+        a = np.concatenate([a, np.zeros(1, np.float32)])
+    return a.view(np.int64)
+
+
+def plan_hier(code: int, segs: Sequence[HierSeg], mid_rates, mid_goals, top_rates) -> HierPlan:
+    """Device metadata of one flame_hier_fedbuff launch (no GPU needed):
+    [segments (8 words)] [mid_w S x M] [mid_delta S x M] [clients S x M x C]
+    [mid_rates f32 M x C] [mid_goal f32 M] [top_rates f32 M]."""
+    S = len(segs)
+    if S == 0:
+        raise ValueError("empty segment list")
+    M = len(mid_goals)
+    if M == 0 or len(top_rates) != M or len(mid_rates) != M:
+        raise ValueError("one goal, one top rate and one rate row per middle")
+    C = len(mid_rates[0])
+    if C == 0 or any(len(r) != C for r in mid_rates):
+        raise ValueError("every middle needs the same (>= 1) number of arrivals")
+    chunk = chunk_elems(code)
+    head = np.zeros((S, HSEG_WORDS), dtype=np.uint64)
+    wtab = np.empty((S, M), dtype=np.uint64)
+    dtab = np.zeros((S, M), dtype=np.uint64)
+    ctab = np.empty((S, M * C), dtype=np.uint64)
+    begin = 0
+    for i, s in enumerate(segs):
+        if len(s.mid_w) != M or len(s.clients) != M * C or (s.mid_delta is not None and len(s.mid_delta) != M):
+            raise ValueError("segment tables must be [n_mids] and [n_mids * n_clients]")
+        wtab[i] = s.mid_w
+        ctab[i] = s.clients
+        if s.mid_delta is not None:
+            dtab[i] = s.mid_delta
+        fixed = [s.top_w, s.top_in, s.top_out]
+        unaligned = (bool(np.any(ctab[i] % VEC_BYTES)) or bool(np.any(wtab[i] % VEC_BYTES))
+                     or bool(np.any(dtab[i] % VEC_BYTES)) or any(p % VEC_BYTES for p in fixed if p))
+        head[i] = (*fixed, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride, 0)
+        begin += -(-s.numel // chunk) if s.numel > 0 else 0
+    if begin == 0:
+        begin = 1
+    parts = [head.view(np.int64).reshape(-1), wtab.view(np.int64).reshape(-1), dtab.view(np.int64).reshape(-1),
+             ctab.view(np.int64).reshape(-1), _f32_words(mid_rates), _f32_words(mid_goals), _f32_words(top_rates)]
+    names = ["segs", "mid_w", "mid_delta", "clients", "mid_rates", "mid_goal", "top_rates"]
+    offs, o = {}, 0
+    for nm, p in zip(names, parts):
+        offs[nm] = o
+        o += p.size * 8
+    return HierPlan(code, np.concatenate(parts), S, begin, M, C, offs)
+
+
+def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_rates, *, top_accum: bool,
+                  top_goal: Optional[int], device, keep: list) -> None:
+    """One flame_hier_fedbuff launch (the caller checked dtypes / devices / contiguity)."""
+    L = N.lib()
+    p = plan_hier(code, segs, mid_rates, mid_goals, top_rates)
+    dm = _staging.upload(p.meta, device)
+    b = dm.data_ptr()
+    flags = (N.FLAME_HIER_TOP_ACCUM if top_accum else 0) | (N.FLAME_HIER_TOP_APPLY if top_goal is not None else 0)
+    with_delta = any(s.mid_delta is not None for s in segs)
+    P = sum(s.numel for s in segs)
+    isz = ITEMSIZE[code]
+    M, C = p.n_mids, p.n_clients
+    # arrivals + middle weights (read, write) [+ deltas] + top (in) + top out [+ top weights r/w]
+    nbytes = isz * P * (M * C + 2 * M + (M if with_delta else 0) + (1 if top_accum else 0) + 1
+                        + (2 if top_goal is not None else 0))
+    with _timed("flame_hier_fedbuff", device, nbytes):
+        N.check(L.flame_hier_fedbuff(code, flags, b + p.offs["segs"], p.n_segs, p.n_chunks, M, C,
+                                     b + p.offs["mid_w"], b + p.offs["mid_delta"] if with_delta else None,
+                                     b + p.offs["clients"], b + p.offs["mid_rates"], b + p.offs["mid_goal"],
+                                     b + p.offs["top_rates"], float(top_goal or 0), _stream_ptr(device)))
+    keep.append(dm)
+
+
 def synth_fill_(out: torch.Tensor, seed: int, stream_id: int, start: int, sigma: float) -> None:
     """Fill a device tensor with flame_amd.synth values (bench / test inputs)."""
     from .synth import scale_for_sigma

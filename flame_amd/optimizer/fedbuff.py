@@ -25,6 +25,7 @@ import copy
 import logging
 import math
 
+import numpy as np
 import torch
 
 from .. import engine
@@ -227,3 +228,144 @@ def scale_add_many(pairs, agg_goal: int, with_delta: bool = False):
     for t in targets:
         t.writeback()
     return results
+
+
+# ---------------------------------------------------------------- co-located hierarchy, one pass
+class _OneEntryCache(dict):
+    def iterkeys(self):
+        return iter(list(self.keys()))
+
+
+def _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta):
+    """The reference's op sequence with the separate launches (fallback of hierarchy_round)."""
+    from .train_result import TrainResult
+    top = FedBuff()
+    deltas = []
+    for w, agg, goal, mv in middles:
+        _, d = FedBuff().scale_add_agg_weights_with_delta(w, agg, goal)
+        deltas.append(d)
+        cache = _OneEntryCache(mid=TrainResult(d, 1, mv))
+        top_agg = top.do(top_agg, cache, total=1, version=version)
+    if top_weights is not None:
+        top.scale_add_agg_weights(top_weights, top_agg, top_goal)
+    return top_agg, (deltas if with_delta else None)
+
+
+def _hier_rows(aggs, keys, device):
+    """Per key: (arrival pointers middle-major, tile stride), or None if no single stride fits."""
+    first = aggs[0]._pending[0][0]
+    slab = getattr(first, "slab", None)
+    if (slab is not None and slab.device == device
+            and all(getattr(w, "slab", None) is slab for a in aggs for w, _ in a._pending)
+            and all(k in slab.meta for k in keys)):
+        slots = np.fromiter((w.slot for a in aggs for w, _ in a._pending), dtype=np.uint64)
+        rows = {}
+        for k in keys:
+            _, _, base, slot_bytes, tile_bytes = slab.key_layout(k)
+            rows[k] = (np.uint64(base) + slots * np.uint64(slot_bytes), tile_bytes)
+        return rows, []
+    rows, keep = {}, []
+    for k in keys:
+        shape, dt = aggs[0]._meta[k]
+        ref = torch.empty(shape, dtype=dt, device="meta")   # numel / dtype of the aggregate
+        ptrs, stride = [], None
+        for a in aggs:
+            row, ts = engine._client_row([w[k] for w, _ in a._pending], ref, device, keep)
+            if stride is None:
+                stride = ts
+            elif ts != stride:
+                return None, keep
+            ptrs.extend(row)
+        rows[k] = (np.asarray(ptrs, dtype=np.uint64), stride)
+    return rows, keep
+
+
+def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, top_goal=None,
+                    with_delta: bool = False):
+    """A node's co-located two-level FedBuff hierarchy in ONE pass per dtype.
+
+    ``middles``: sequence of ``(mid_weights, mid_agg, mid_goal, mid_version)`` in the order
+    the top aggregator receives their deltas.  ``mid_agg`` is the middle's FedBuff aggregate
+    (normally the :class:`DeferredAggregate` its ``do()`` calls returned).  Equivalent to,
+    for each middle: ``scale_add_agg_weights_with_delta(mid_weights, mid_agg, mid_goal)``
+    (fedbuff.py:101-127 + asyncfl/middle_aggregator.py:221-226,246), then the top's
+    ``top_agg = FedBuff.do(top_agg, {delta, version=mid_version}, version=version)``
+    (asyncfl/top_aggregator.py:85-92, rate 1/sqrt(1+version-mid_version), fedbuff.py:96);
+    finally, if ``top_weights`` is given, ``scale_add_agg_weights(top_weights, top_agg,
+    top_goal)``.  Bit-identical to that sequence; the middle aggregates and (unless
+    ``with_delta``) the deltas never reach HBM.  Middle weights and ``top_weights`` are
+    updated in place.  Returns ``(top_agg, deltas or None)``.
+
+    The middle aggregates stay valid: their queued arrivals are kept and reduced again
+    if anything reads them later.
+    """
+    middles = list(middles)
+    if not middles:
+        raise ValueError("hierarchy_round: no middles")
+    if top_weights is not None and not top_goal:
+        raise ValueError("hierarchy_round: top_goal must be nonzero")
+    # the top's rates, computed as FedBuff.do does (stale versions raise here, fedbuff.py:96)
+    top_rates = [1 / math.sqrt(1 + version - mv) for *_, mv in middles]
+    aggs = [a for _, a, _, _ in middles]
+    keys = list(middles[0][0].keys())
+    fusable = (all(isinstance(a, DeferredAggregate) and a._data is None and a._pending and _uniform(a)
+                   for a in aggs)
+               and len({len(a._pending) for a in aggs}) == 1
+               and all(list(w.keys()) == keys and a._keys == keys for w, a, _, _ in middles))
+    device = None
+    if fusable:
+        device = engine.pick_device(middles[0][0])
+        for k in keys:
+            shape, dt = aggs[0]._meta[k]
+            n = middles[0][0][k].numel()
+            tensors = [w[k] for w, _, _, _ in middles]
+            if isinstance(top_agg, collections.abc.Mapping):
+                tensors.append(top_agg[k])
+            if top_weights is not None:
+                tensors.append(top_weights[k] if k in top_weights else None)
+            if (engine.dtype_code(dt) not in (engine.N.FLAME_F32, engine.N.FLAME_BF16, engine.N.FLAME_F16)
+                    or any(t is None or t.dtype != dt or t.numel() != n or t.device != device
+                           or not t.is_contiguous() for t in tensors)
+                    or any(a._meta[k][1] != dt for a in aggs)):
+                fusable = False
+                break
+    if fusable:
+        rows, keep = _hier_rows(aggs, keys, device)
+        fusable = rows is not None
+    if not fusable:
+        return _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta)
+
+    top_accum = top_agg is not None
+    if isinstance(top_agg, DeferredAggregate):
+        top_agg.flush()
+        top_out = top_agg._data
+        result = top_agg
+    elif top_agg is not None:
+        top_out, result = top_agg, top_agg
+    else:
+        top_out = collections.OrderedDict(
+            (k, torch.empty(aggs[0]._meta[k][0], dtype=aggs[0]._meta[k][1], device=device)) for k in keys)
+        result = top_out
+    deltas = None
+    if with_delta:
+        deltas = [{k: torch.empty(w[k].shape, dtype=w[k].dtype, device=device) for k in keys}
+                  for w, _, _, _ in middles]
+    mid_rates = [[r for _, r in a._pending] for a in aggs]
+    mid_goals = [g for _, _, g, _ in middles]
+    groups = collections.OrderedDict()
+    for k in keys:
+        groups.setdefault(engine.dtype_code(aggs[0]._meta[k][1]), []).append(k)
+    for code, ks in groups.items():
+        segs = []
+        for k in ks:
+            ptrs, stride = rows[k]
+            t_out = top_out[k]
+            segs.append(engine.HierSeg(
+                numel=t_out.numel(), mid_w=[w[k].data_ptr() for w, _, _, _ in middles], clients=ptrs,
+                mid_delta=[d[k].data_ptr() for d in deltas] if deltas is not None else None,
+                top_w=top_weights[k].data_ptr() if top_weights is not None else 0,
+                top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride))
+        engine.hier_fedbuff_(segs, code, mid_rates, mid_goals, top_rates, top_accum=top_accum,
+                             top_goal=top_goal if top_weights is not None else None, device=device, keep=keep)
+    engine._keepalive(keep, device)
+    return result, deltas

@@ -14,6 +14,11 @@
  *   flame_fedbuff_scale_add     optimizer/fedbuff.py:101-127 (scale_add_agg_weights), fused with
  *                               common/util.py:152-159 (delta_weights_pytorch) as used by
  *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246
+ *   flame_hier_fedbuff          a node's co-located two-level FedBuff hierarchy in one pass:
+ *                               per middle optimizer/fedbuff.py:89-97,136-157 (None-start
+ *                               arrivals) + :101-127 (scale_add) + the delta of
+ *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246,
+ *                               fed to the top's FedBuff (asyncfl/top_aggregator.py:85-109)
  *   flame_synth_fill            (bench/test plumbing: counter-based synthetic updates)
  *
  * Conventions
@@ -150,6 +155,47 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
  */
 int flame_fedbuff_scale_add(int dtype, const flame_segment *segs, int32_t n_segs,
                             int64_t n_chunks, int64_t goal, void *stream);
+
+/* flame_hier_fedbuff flags */
+#define FLAME_HIER_TOP_ACCUM 1u  /* the top aggregate exists (not None): start from seg.top_agg_in */
+#define FLAME_HIER_TOP_APPLY 2u  /* finish with the top's scale-add into seg.top_w */
+
+/* One contiguous run of elements of the hierarchy (one state_dict tensor). */
+typedef struct flame_hier_segment {
+    void *top_w;              /* top model weights, in/out (FLAME_HIER_TOP_APPLY) */
+    const void *top_agg_in;   /* top aggregate before this batch (FLAME_HIER_TOP_ACCUM) */
+    void *top_agg_out;        /* top aggregate after this batch (NULL = not stored; may == top_agg_in) */
+    int64_t numel;
+    int64_t chunk_begin;      /* prefix sum of ceil(numel / flame_chunk_elems(dtype)) */
+    int64_t flags;            /* FLAME_SEG_UNALIGNED */
+    int64_t client_tile_stride;  /* as flame_segment.client_tile_stride, shared by every arrival */
+    int64_t reserved;
+} flame_hier_segment;
+
+/*
+ * Co-located two-level FedBuff hierarchy (LIFL-style: n_mids middle aggregators on this
+ * GPU feeding one top aggregator), one launch.  Per element, for m = 0 .. n_mids-1 (the
+ * order the top receives the middles' deltas), every op rounded in dtype:
+ *   a   = tmp(c_{m,0}, r_{m,0}); a = a + tmp(c_{m,i}, r_{m,i}) for i >= 1     (None-start FedBuff)
+ *   w_m' = w_m + a / mid_goal[m];  d_m = w_m' - w_m;  w_m := w_m'          (scale_add + delta)
+ *   top = tmp(d_0, top_rates[0]) (or top_agg_in + ...), top = top + tmp(d_m, top_rates[m])
+ * then top_agg_out = top and, with FLAME_HIER_TOP_APPLY, top_w = top_w + top / top_goal.
+ * tmp(v, r) = round(v * r).  Bit-identical to flame_agg_reduce (INIT_FIRST) per middle +
+ * flame_fedbuff_scale_add with delta + one flame_agg_reduce per delta on the top aggregate +
+ * flame_fedbuff_scale_add; the middle aggregates never reach HBM.
+ *   mid_w     : device [n_segs][n_mids] pointers to each middle's weights (in/out)
+ *   mid_delta : device [n_segs][n_mids] pointers for the deltas (NULL table or NULL entries:
+ *               not stored)
+ *   clients   : device [n_segs][n_mids][n_clients] arrival pointers, arrival order per middle
+ *   mid_rates : device [n_mids][n_clients] fp32 staleness rates float(1/sqrt(1+version-v))
+ *   mid_goal  : device [n_mids] float(agg_goal) of each middle; top_rates: device [n_mids]
+ * dtype FLAME_F32, FLAME_BF16 or FLAME_F16.
+ */
+int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment *segs, int32_t n_segs,
+                       int64_t n_chunks, int32_t n_mids, int32_t n_clients, const void *const *mid_w,
+                       const void *const *mid_delta, const void *const *clients,
+                       const float *mid_rates, const float *mid_goal, const float *top_rates,
+                       float top_goal, void *stream);
 
 /*
  * Host buffers the kernels read zero-copy over PCIe (ingest; flame_amd/ingest.py).

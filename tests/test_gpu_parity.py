@@ -699,3 +699,114 @@ def test_middle_group_flush_and_scale_add_many(dtype):
         ob = {k: v.clone() for k, v in base0[m].items()}
         O.OracleFedBuff().scale_add_agg_weights(ob, oaggs[m], 4)
         S.assert_bitwise(f"oracle base m{m}", S.to_cpu(gb[m]), ob)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("placement", ["slab", "tensors"])
+@pytest.mark.parametrize("top_start", ["none", "existing"])
+def test_hierarchy_round_one_pass(dtype, placement, top_start):
+    """flame_hier_fedbuff (the co-located middles + top in ONE launch) == the separate
+    launches (scale_add_agg_weights_with_delta per middle, top FedBuff.do per delta,
+    top scale_add) == the oracle's op sequence, bitwise: top aggregate, top weights,
+    middle weights and deltas."""
+    from flame_amd.optimizer.fedbuff import hierarchy_round, _compose_hierarchy
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(41)
+    shapes = {"w": (3001,), "m": (17, 129), "b": (5,)}
+    M, C, rnd = 5, 4, 12
+    ups = [[{k: (torch.randn(s, generator=g) * 1e-2).to(dtype) for k, s in shapes.items()} for _ in range(C)]
+           for _ in range(M)]
+    vers = [[rnd - ((m + t) % 4) for t in range(C)] for m in range(M)]
+    mid0 = [{k: torch.randn(s, generator=g).to(dtype) for k, s in shapes.items()} for _ in range(M)]
+    top_w0 = {k: torch.randn(s, generator=g).to(dtype) for k, s in shapes.items()}
+    top_prev = {k: (torch.randn(s, generator=g) * 1e-3).to(dtype) for k, s in shapes.items()}
+    mid_ver = [rnd - (m % 3) for m in range(M)]
+    goals = [C, C + 1, C, 3, C]
+    slab = UpdateSlab({k: torch.empty(s, dtype=dtype) for k, s in shapes.items()}, capacity=M * C, device=DEV) \
+        if placement == "slab" else None
+
+    def arrivals():
+        opts, aggs = [make_amd("fedbuff") for _ in range(M)], [None] * M
+        for m in range(M):
+            for t in range(C):
+                w = {k: v.to(DEV) for k, v in ups[m][t].items()}
+                cache = S.SortedCache()
+                cache["a"] = S.TR(slab.put(w) if slab is not None else w, 1, vers[m][t])
+                aggs[m] = opts[m].do(aggs[m], cache, total=1, version=rnd)
+        return aggs
+
+    def run(fn):
+        mids = [{k: v.to(DEV) for k, v in b.items()} for b in mid0]
+        tw = {k: v.to(DEV) for k, v in top_w0.items()}
+        tprev = {k: v.to(DEV) for k, v in top_prev.items()} if top_start == "existing" else None
+        mids_in = [(mids[m], a, goals[m], mid_ver[m]) for m, a in enumerate(arrivals())]
+        agg, deltas = fn(mids_in, tprev, rnd, tw, 7, True)
+        return S.to_cpu(dict(agg)), [S.to_cpu(d) for d in deltas], [S.to_cpu(x) for x in mids], S.to_cpu(tw)
+
+    fused = run(lambda mi, ta, v, tw, tg, wd: hierarchy_round(mi, ta, version=v, top_weights=tw, top_goal=tg,
+                                                               with_delta=wd))
+    sep = run(_compose_hierarchy)
+    for lbl, a, b in zip(("top agg", "deltas", "mids", "top w"), fused, sep):
+        if isinstance(a, list):
+            for m, (x, y) in enumerate(zip(a, b)):
+                S.assert_bitwise(f"{lbl} m{m}", x, y)
+        else:
+            S.assert_bitwise(lbl, a, b)
+    # oracle: the reference's op sequence on CPU
+    top_o, top_agg_o = O.OracleFedBuff(), ({k: v.clone() for k, v in top_prev.items()}
+                                             if top_start == "existing" else None)
+    for m in range(M):
+        mo, agg_o = O.OracleFedBuff(), None
+        for t in range(C):
+            cache = S.SortedCache()
+            cache["a"] = S.TR({k: v.clone() for k, v in ups[m][t].items()}, 1, vers[m][t])
+            agg_o = mo.do(agg_o, cache, total=1, version=rnd)
+        w = {k: v.clone() for k, v in mid0[m].items()}
+        d = {k: O.scale_add_tensor(w[k], agg_o[k], goals[m], want_delta=True) for k in w}
+        S.assert_bitwise(f"oracle mid m{m}", fused[2][m], w)
+        S.assert_bitwise(f"oracle delta m{m}", fused[1][m], d)
+        cache = S.SortedCache()
+        cache["d"] = S.TR(d, 1, mid_ver[m])
+        top_agg_o = top_o.do(top_agg_o, cache, total=1, version=rnd)
+    S.assert_bitwise("oracle top agg", fused[0], top_agg_o)
+    tw = {k: v.clone() for k, v in top_w0.items()}
+    top_o.scale_add_agg_weights(tw, top_agg_o, 7)
+    S.assert_bitwise("oracle top w", fused[3], tw)
+
+
+def test_hierarchy_round_launch_count_and_fallback():
+    """Uniform middles take ONE flame_hier_fedbuff launch per dtype; ragged arrival counts
+    fall back to the separate launches with the same results; stale versions raise as
+    FedBuff.do does (fedbuff.py:96)."""
+    from flame_amd import engine
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    g = torch.Generator().manual_seed(43)
+    rnd = 5
+
+    def middles(counts):
+        out = []
+        for m, c in enumerate(counts):
+            opt, agg = make_amd("fedbuff"), None
+            for t in range(c):
+                cache = S.SortedCache()
+                cache["a"] = S.TR({"x": (torch.randn(777, generator=g) * 1e-2).to(DEV)}, 1, rnd - t % 2)
+                agg = opt.do(agg, cache, total=1, version=rnd)
+            out.append(({"x": torch.randn(777, generator=g).to(DEV)}, agg, c, rnd))
+        return out
+
+    engine.kernel_events = []
+    try:
+        hierarchy_round(middles([3, 3, 3]), None, version=rnd)
+        names = [e[0] for e in engine.kernel_events]
+        assert names == ["flame_hier_fedbuff"], names
+        engine.kernel_events = []
+        hierarchy_round(middles([3, 2]), None, version=rnd)
+        names = [e[0] for e in engine.kernel_events]
+        assert "flame_hier_fedbuff" not in names and "flame_fedbuff_scale_add" in names, names
+    finally:
+        engine.kernel_events = None
+    mids = middles([2, 2])
+    mids[1] = (mids[1][0], mids[1][1], 2, rnd + 1)
+    with pytest.raises(ZeroDivisionError):
+        hierarchy_round(mids, None, version=rnd)

@@ -186,3 +186,33 @@ def test_plan_per_segment_rates_layout():
         engine.plan(0, segs, [[0.5, 0.25], [0.1]], seg_rates=True)
     with pytest.raises(ValueError):
         engine.plan(0, segs, [[0.5, 0.25]], seg_rates=True)
+
+
+def test_plan_hier_layout():
+    """flame_hier_fedbuff metadata: 8-word segments, [S][M] weight / delta tables,
+    [S][M*C] arrival table, fp32 rate rows, goals and top rates at the recorded offsets."""
+    M, C = 3, 2
+    segs = [engine.HierSeg(3000, mid_w=[16 * (i + 1) for i in range(M)], clients=[4096 * (i + 1) for i in range(M * C)],
+                           mid_delta=[0, 32, 48], top_w=64, top_in=0, top_out=80, tile_stride=8192),
+            engine.HierSeg(5, mid_w=[96, 112, 8], clients=[1024] * (M * C), top_out=128)]   # mid_w 8: unaligned
+    rates = [[0.5, 1 / 3], [1.0, 0.25], [0.7, 0.1]]
+    p = engine.plan_hier(N.FLAME_F32, segs, rates, [2, 3, 4], [1.0, 0.5, 1 / 3])
+    w = p.meta
+    assert (p.n_segs, p.n_mids, p.n_clients) == (2, M, C)
+    chunk = engine.chunk_elems(N.FLAME_F32)
+    assert p.n_chunks == -(-3000 // chunk) + 1
+    assert list(w[0:8]) == [64, 0, 80, 3000, 0, 0, 8192, 0]
+    assert list(w[8:16]) == [0, 0, 128, 5, -(-3000 // chunk), N.FLAME_SEG_UNALIGNED, 0, 0]
+    o = p.offs
+    assert o["mid_w"] == 16 * 8 and o["mid_delta"] == o["mid_w"] + 2 * M * 8
+    assert list(w[o["mid_w"] // 8:o["mid_w"] // 8 + M]) == [16, 32, 48]
+    assert list(w[o["mid_delta"] // 8:o["mid_delta"] // 8 + 2 * M]) == [0, 32, 48, 0, 0, 0]
+    assert list(w[o["clients"] // 8:o["clients"] // 8 + M * C]) == [4096 * (i + 1) for i in range(M * C)]
+    f = w.view(np.float32)
+    assert list(f[o["mid_rates"] // 4:o["mid_rates"] // 4 + M * C]) == [np.float32(r) for row in rates for r in row]
+    assert list(f[o["mid_goal"] // 4:o["mid_goal"] // 4 + M]) == [2.0, 3.0, 4.0]
+    assert list(f[o["top_rates"] // 4:o["top_rates"] // 4 + M]) == [np.float32(x) for x in (1.0, 0.5, 1 / 3)]
+    with pytest.raises(ValueError):
+        engine.plan_hier(N.FLAME_F32, segs, [[0.5, 0.1], [0.2]], [2, 3], [1.0, 1.0])
+    with pytest.raises(ValueError):
+        engine.plan_hier(N.FLAME_F32, segs, rates, [2, 3], [1.0, 1.0])

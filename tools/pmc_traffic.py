@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--layout", default="slab")
+    ap.add_argument("--itemsize", type=int, default=4, help="bytes per element (bf16: 2)")
     ap.add_argument("--extra-arrays", type=int, default=2,
                     help="P-sized arrays besides the N clients in the algorithmic bytes (FedAvg 2, FedOPT 8)")
     a = ap.parse_args()
@@ -48,7 +49,7 @@ def main():
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     read_b = 2.0 * f_kb * 1024
     write_b = w_kb * 1024
-    algo = (a.clients + a.extra_arrays) * a.params * 4
+    algo = (a.clients + a.extra_arrays) * a.params * a.itemsize
     res = {
         "kernel": a.name, "clients": a.clients, "params": a.params, "layout": a.layout,
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb, "dispatches": [len(fetch), len(write)],
