@@ -65,6 +65,9 @@ def parse():
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--force-shard", action="store_true",
+                    help="run the N>1 code path (process group + sharded FedAvg + all-gather) even at N=1 "
+                         "(rehearses the RCCL path on a one-GPU box under torchrun)")
     ap.add_argument("--layout", default="slab", choices=["slab", "row"],
                     help="slab: updates in the tiled UpdateSlab (what DeviceUpdateCache produces); "
                          "row: one contiguous tensor per client (weights_to_model_device layout)")
@@ -80,7 +83,7 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(force_group=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,7 +93,7 @@ def setup_dist():
     if backend != "nccl":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or force_group:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -100,7 +103,8 @@ def setup_dist():
 
 
 def barrier(world):
-    if world > 1:
+    import torch.distributed as dist
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         import torch.distributed as dist
         dist.barrier()
 
@@ -263,7 +267,7 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5):
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    world, rank, local = setup_dist(args.force_shard)
     dev = torch.device("cuda", local)
     from flame_amd import _native, engine, synth
     from flame_amd.optimizers import optimizer_provider
@@ -303,7 +307,7 @@ def main():
     keys = [f"{i:05d}" for i in range(n)]
     torch.cuda.synchronize()
 
-    if world > 1 and args.workload == "fedavg":
+    if (world > 1 or args.force_shard) and args.workload == "fedavg":
         from flame_amd.shard import ShardedSliceFedAvg
         opt = ShardedSliceFedAvg(fracs=(1.0,) if args.no_overlap else (0.75, 0.20, 0.05))
     else:
@@ -390,8 +394,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

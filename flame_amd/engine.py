@@ -642,6 +642,36 @@ def _accumulate_slab(agg: dict, entries, device) -> bool:
     return True
 
 
+def reduce_slab_range(out: torch.Tensor, entries, key: str, lo: int, hi: int) -> bool:
+    """``out += Σ_i round(w_i[key][lo:hi] * rate_i)`` in order, for ``entries`` = (SlotWeights,
+    rate) of ONE UpdateSlab: the pointer row is computed from slot numbers (numpy) instead of
+    slicing every client's view (the sharded FedAvg's per-piece launches).  ``out`` is the
+    contiguous device slice [lo, hi) of the aggregate; ``lo`` must start a slab tile.
+    Returns False (nothing launched) when the case does not apply."""
+    if not entries:
+        return False
+    slab = getattr(entries[0][0], "slab", None)
+    if (slab is None or not out.is_cuda or slab.device != out.device or key not in slab.meta
+            or not out.is_contiguous()):
+        return False
+    if any(getattr(w, "slab", None) is not slab for w, _ in entries):
+        return False
+    dt, n, base, slot_bytes, tile_bytes = slab.key_layout(key)
+    code = dtype_code(dt)
+    T = chunk_elems(code)
+    if dt != out.dtype or not (0 <= lo <= hi <= n) or lo % T or out.numel() != hi - lo:
+        return False
+    if hi == lo:
+        return True
+    slots = np.fromiter((w.slot for w, _ in entries), dtype=np.uint64, count=len(entries))
+    ptrs = np.uint64(base + (lo // T) * tile_bytes) + slots * np.uint64(slot_bytes)
+    keep = []
+    _launch_reduce(code, [Seg(hi - lo, out=out.data_ptr(), inp=out.data_ptr(), clients=ptrs,
+                              tile_stride=tile_bytes)], [r for _, r in entries], out.device, keep)
+    _keepalive(keep, out.device)
+    return True
+
+
 def _accumulate_promoted(agg: dict, k, entries, device) -> None:
     """agg[k] += tmp_i where tmp_i = (v_i * rate_i).to(v_i.dtype) has another dtype.
 

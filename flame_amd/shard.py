@@ -174,11 +174,13 @@ class ShardedSliceFedAvg:
         rates = [r for _, r in entries]
         works = []
         staged = base.is_cuda and self.dist.get_backend(self.group) == "gloo"  # gloo: host collectives
+        from . import engine
         for lo, hi in piece_bounds(P, self.fracs, align):
             piece = base[lo:hi]
-            from . import engine
-            self.reducer(piece, [engine.slice_elems(w[key], lo, hi, P) if w[key].is_cuda else w[key][lo:hi]
-                                 for w, _ in entries], rates)
+            # slab-resident updates: pointer rows from slot numbers, no per-client views
+            if not (self.reducer is hip_reducer and engine.reduce_slab_range(piece, entries, key, lo, hi)):
+                self.reducer(piece, [engine.slice_elems(w[key], lo, hi, P) if w[key].is_cuda else w[key][lo:hi]
+                                     for w, _ in entries], rates)
             dst = self.global_flat[self.world * lo:self.world * hi]
             if staged:
                 host = torch.empty(dst.numel(), dtype=dst.dtype)
