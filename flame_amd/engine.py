@@ -171,27 +171,35 @@ class _Staging:
 
 _staging = _Staging()
 
-# Optional kernel timing hook (bench.py): when set to a list, every native
-# launch appends (name, start_event, end_event, algorithmic_bytes).  Events are
-# recorded on the stream the kernel is launched on (torch's current stream).
+# Optional kernel timing hooks: when ``kernel_events`` is a list (bench.py), or while a
+# flame_amd.metrics.KernelRecorder is active (``_recorders``), every native launch
+# appends (name, start_event, end_event, algorithmic_bytes).  Events are recorded on
+# the stream the kernel is launched on (torch's current stream).
 kernel_events = None
+_recorders = []
 
 
 class _timed:
     def __init__(self, name, device, nbytes):
         self.name, self.device, self.nbytes = name, device, nbytes
+        self.on = False
 
     def __enter__(self):
-        if kernel_events is not None:
+        self.on = kernel_events is not None or bool(_recorders)
+        if self.on:
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e0.record(torch.cuda.current_stream(self.device))
         return self
 
     def __exit__(self, *exc):
-        if kernel_events is not None and exc[0] is None:
+        if self.on and exc[0] is None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(torch.cuda.current_stream(self.device))
-            kernel_events.append((self.name, self.e0, e1, self.nbytes))
+            ev = (self.name, self.e0, e1, self.nbytes)
+            if kernel_events is not None:
+                kernel_events.append(ev)
+            for r in _recorders:
+                r.append(ev)
         return False
 
 

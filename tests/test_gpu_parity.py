@@ -836,3 +836,31 @@ def test_reduce_slab_range_pieces_equal_full_reduce():
     assert not engine.reduce_slab_range(pieced[100:200], entries, "a", 100, 200)      # not tile-aligned
     assert not engine.reduce_slab_range(pieced[:10], [({"a": base}, 1.0)], "a", 0, 10)  # not slab slots
     assert not engine.reduce_slab_range(pieced[:21], entries, "zz", 0, 21)             # unknown key
+
+
+def test_metric_collector_receives_kernel_metrics():
+    """optimizer.metric_collector gets runtime / hbm_GBps / launches per kernel of each call
+    (saved once the kernels are done; metrics.flush() waits for them)."""
+    from flame_amd import metrics
+
+    class MC:
+        def __init__(self):
+            self.state_dict = {}
+
+        def save(self, mtype, alias, value):
+            self.state_dict[f"{alias}.{mtype}"] = value
+
+    opt = make_amd("fedadam")
+    opt.metric_collector = MC()
+    g = torch.Generator().manual_seed(53)
+    w = {"x": torch.randn(100_003, generator=g).to(DEV)}
+    for rnd in range(2):
+        cache = S.SortedCache()
+        for i in range(4):
+            cache[f"e{i}"] = S.TR({"x": (torch.randn(100_003, generator=g) * 1e-2).to(DEV)}, 10 + i)
+        w = opt.do({k: v.clone() for k, v in w.items()}, cache, total=46)
+    metrics.flush()
+    sd = opt.metric_collector.state_dict
+    assert sd["fedadam.flame_fedopt_reduce_adapt.launches"] == 1, sd
+    assert sd["fedadam.flame_fedopt_reduce_adapt.runtime"] > 0
+    assert sd["fedadam.flame_fedopt_reduce_adapt.hbm_GBps"] > 0

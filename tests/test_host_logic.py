@@ -216,3 +216,28 @@ def test_plan_hier_layout():
         engine.plan_hier(N.FLAME_F32, segs, [[0.5, 0.1], [0.2]], [2, 3], [1.0, 1.0])
     with pytest.raises(ValueError):
         engine.plan_hier(N.FLAME_F32, segs, rates, [2, 3], [1.0, 1.0])
+
+
+class _MC:
+    """MetricCollector surface (monitor/metric_collector.py:117-121)."""
+
+    def __init__(self):
+        self.state_dict = {}
+
+    def save(self, mtype, alias, value):
+        self.state_dict[f"{alias}.{mtype}"] = value
+
+
+def test_metric_collector_hook_without_launches():
+    """An instrumented do() that launches nothing saves nothing and keeps the contract."""
+    from flame_amd import metrics
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedavg")
+    opt.metric_collector = _MC()
+    assert opt.do({"w": torch.zeros(3)}, S.SortedCache(), total=0) is None
+    metrics.flush()
+    assert opt.metric_collector.state_dict == {}
+    # every drop-in's entry points are wrapped
+    from flame_amd.optimizers import DROP_INS
+    for sort, cls in DROP_INS.items():
+        assert getattr(cls.do, "__wrapped__", None) is not None, sort
