@@ -73,9 +73,11 @@ def parse():
                          "row: one contiguous tensor per client (weights_to_model_device layout)")
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--e2e-mode", default="zerocopy",
-                    choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference"],
+                    choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference", "eager"],
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
                          "stream overlapped with the reduction; pageable: reference weights_to_model_device")
+    ap.add_argument("--e2e-placement", default="slab", choices=["slab", "hbm"],
+                    help="eager mode: DeviceUpdateCache placement of the arriving updates")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-rounds", type=int, default=3)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -540,6 +542,9 @@ def bench_e2e(args, n, P, dev):
               with the reduction of the previous batch;
     pageable: the reference convention (weights_to_model_device: per-tensor .to(device)
               from pageable memory), then one FedAvg;
+    eager:    the eager top aggregator (eager_syncfl/top_aggregator.py:36-90): every arrival
+              goes into a DeviceUpdateCache (H2D on its side stream) and FedAvg.do runs
+              per arrival with the running total, so the reduction trails the transfers;
     wire*:    starts from the channel's serialized payloads (cloudpickle of
               {weights, dataset_size}, channel.py:203-218): wire = flame_amd.ingest.decode
               (zero-copy views into the payload bytes) + H2D; wire_pinned = payloads sit in
@@ -550,7 +555,7 @@ def bench_e2e(args, n, P, dev):
     n = min(n, 64)
     batch = 8
     mode = args.e2e_mode
-    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode in ("zerocopy", "copy")))
+    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode in ("zerocopy", "copy", "eager")))
     tmp = torch.empty(P, dtype=torch.float32, device=dev)
     for i in range(n):
         engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
@@ -579,6 +584,9 @@ def bench_e2e(args, n, P, dev):
     if mode == "copy":
         dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
         copy_stream = torch.cuda.Stream(dev)
+    if mode == "eager":
+        from flame_amd.ingest import DeviceUpdateCache
+        ecache = DeviceUpdateCache(device=dev, placement=args.e2e_placement, capacity=n)
     torch.cuda.synchronize()
 
     def step():
@@ -599,6 +607,13 @@ def bench_e2e(args, n, P, dev):
                     w = msg["weights"]
                 cache[f"{i:05d}"] = TR(w, msg["dataset_size"])
             opt.do({"model": base}, cache, total=total)
+        elif mode == "eager":
+            base_w = {"model": base}
+            running = 0
+            for i in range(n):   # arrival i: receive -> cache (H2D on the side stream) -> do()
+                running += int(counts[i])
+                ecache[f"{i:05d}"] = TR({"model": host[i]}, int(counts[i]))
+                opt.do(base_w, ecache, total=running, num_trainers=n)
         elif mode == "pageable":
             cache = Cache()
             for i in range(n):  # weights_to_model_device (common/util.py:198-208)

@@ -448,11 +448,13 @@ class DeviceUpdateCache:
             self.device = torch.device("cuda", torch.cuda.current_device())
         return self.device
 
-    def _side_stream(self):
+    def _side_stream(self, after_current: bool = True):
         dev = self._dev()
         if self._stream is None:
             self._stream = torch.cuda.Stream(dev)
-        self._stream.wait_stream(torch.cuda.current_stream(dev))
+        if after_current:
+            # device-resident sources may still be being produced on the caller's stream
+            self._stream.wait_stream(torch.cuda.current_stream(dev))
         return self._stream
 
     def _fits_slab(self, w):
@@ -468,7 +470,10 @@ class DeviceUpdateCache:
         w = getattr(tres, "weights", None)
         ev = None
         if isinstance(w, dict) and w and self.placement in ("slab", "hbm"):
-            st = self._side_stream()
+            # host-resident updates (the channel's case) need no ordering behind the caller's
+            # stream, so back-to-back arrivals keep the copy engine busy while the
+            # reductions of earlier arrivals run on the caller's stream
+            st = self._side_stream(any(isinstance(v, torch.Tensor) and v.is_cuda for v in w.values()))
             if self.placement == "slab" and self._fits_slab(w):
                 tres.weights = self.slab.put(w, stream=st)
             else:
