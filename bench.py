@@ -73,7 +73,8 @@ def parse():
                          "row: one contiguous tensor per client (weights_to_model_device layout)")
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--e2e-mode", default="zerocopy",
-                    choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference", "eager"],
+                    choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference", "eager",
+                             "shm", "shm_reference"],
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
                          "stream overlapped with the reduction; pageable: reference weights_to_model_device")
     ap.add_argument("--e2e-placement", default="slab", choices=["slab", "hbm"],
@@ -549,7 +550,11 @@ def bench_e2e(args, n, P, dev):
               {weights, dataset_size}, channel.py:203-218): wire = flame_amd.ingest.decode
               (zero-copy views into the payload bytes) + H2D; wire_pinned = payloads sit in
               pinned receive buffers, decode gives device-addressable views the kernel streams
-              directly; wire_reference = cloudpickle.loads + .to(device) (the reference ingest)."""
+              directly; wire_reference = cloudpickle.loads + .to(device) (the reference ingest);
+    shm*:     payloads sit in per-sender POSIX shared-memory segments (the LIFL SHM backend,
+              backend/shm.py:386-403): shm = flame_amd.ingest.ShmReceiver (segments registered
+              once, decoded in place, the kernel streams the views); shm_reference = the
+              backend's bytes(buf[:size]) copy + cloudpickle.loads + .to(device)."""
     from flame_amd import engine, synth
     from flame_amd.optimizers import optimizer_provider
     n = min(n, 64)
@@ -581,6 +586,22 @@ def bench_e2e(args, n, P, dev):
             else:
                 payloads.append(b)
         del host
+    shm_segs = []
+    if mode.startswith("shm"):
+        import cloudpickle
+        from multiprocessing import shared_memory
+        from flame_amd import ingest
+        sizes = []
+        tag = f"flamebench{os.getpid()}"
+        for i in range(n):
+            b = cloudpickle.dumps({"weights": {"model": host[i].clone()}, "dataset_size": int(counts[i])})
+            seg = shared_memory.SharedMemory(name=f"{tag}_t{i}-agg", create=True, size=len(b))
+            seg.buf[:len(b)] = b
+            shm_segs.append(seg)
+            sizes.append(len(b))
+            del b
+        del host
+        rx = ingest.ShmReceiver("agg", untrack=False)
     if mode == "copy":
         dslab = torch.empty((2, batch, P), dtype=torch.float32, device=dev)
         copy_stream = torch.cuda.Stream(dev)
@@ -607,6 +628,22 @@ def bench_e2e(args, n, P, dev):
                     w = msg["weights"]
                 cache[f"{i:05d}"] = TR(w, msg["dataset_size"])
             opt.do({"model": base}, cache, total=total)
+        elif mode.startswith("shm"):
+            cache = Cache()
+            for i in range(n):
+                if mode == "shm_reference":   # backend/shm.py:386-391 + channel.py:321-325 + util.py:198-208
+                    buf = shared_memory.SharedMemory(f"{tag}_t{i}-agg")
+                    data = bytes(buf.buf[:sizes[i]])
+                    buf.close()
+                    msg = cloudpickle.loads(data)
+                    w = {k: v.to(dev) for k, v in msg["weights"].items()}
+                else:
+                    msg = rx.loads(f"{tag}_t{i}", sizes[i])
+                    w = msg["weights"]
+                cache[f"{i:05d}"] = TR(w, msg["dataset_size"])
+                del msg
+            opt.do({"model": base}, cache, total=total)
+            del cache, w
         elif mode == "eager":
             base_w = {"model": base}
             running = 0
@@ -640,7 +677,14 @@ def bench_e2e(args, n, P, dev):
                 done[slot].record(cur)
         out_h.copy_(base, non_blocking=True)
 
-    elapsed, events = timed(1, args.steps, args.warmup, step)
+    try:
+        elapsed, events = timed(1, args.steps, args.warmup, step)
+    finally:
+        if shm_segs:
+            rx.close()
+            for seg in shm_segs:
+                seg.close()
+                seg.unlink()
     ks = kernel_stats(events, "flame_agg_reduce")
     print(json.dumps({
         "metric": "aggregated params/sec, END-TO-END (host-resident updates -> global model in host memory)",

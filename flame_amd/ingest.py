@@ -402,6 +402,7 @@ class RegisteredBuffer:
             engine._staging.drain()
             N.check(N.lib().flame_host_unregister(self.ptr))
             self._open = False
+            self.arr = self.buf = None   # release the exported buffer (lets an mmap / shm close)
 
     def __enter__(self):
         return self
@@ -409,6 +410,77 @@ class RegisteredBuffer:
     def __exit__(self, *exc):
         self.close()
         return False
+
+
+# ------------------------------------------------------------------ LIFL shared-memory receive
+class ShmReceiver:
+    """Zero-copy stand-in for the LIFL SHM backend's receive (``backend/shm.py:386-391``).
+
+    The reference opens ``SharedMemory(other + "-" + self_id)`` on every message and
+    copies ``msg_size`` bytes out of it (``bytes(read_buf.buf[:msg_size])``), after
+    which the channel runs ``cloudpickle.loads`` on the copy (``channel.py:321-325``).
+    Here each sender's segment is opened once and (with ``register=True``, the
+    default on a GPU host) page-locked and mapped for the device with
+    ``flame_host_register``; :meth:`get_data` returns a memoryview of the message in
+    place and :meth:`loads` decodes it with :func:`decode` -- the update's tensors are
+    views into the shared segment that the reduction kernel streams over PCIe, or that
+    :class:`DeviceUpdateCache` copies to HBM, without any host copy.
+
+    Lifetime: the sender rewrites its segment for its next message
+    (``backend/shm.py:393-403``), so a message's views are valid until that sender
+    writes again -- hand them to a DeviceUpdateCache (which copies to HBM as they
+    arrive) or aggregate before acknowledging the sender.  A segment that grew is
+    re-opened (and re-registered) transparently.
+    """
+
+    def __init__(self, self_id: str, register: bool = True, untrack: bool = True):
+        self.self_id = self_id
+        self.register = register
+        self.untrack = untrack     # the writer owns (and unlinks) its segment
+        self._segs = {}   # name -> (SharedMemory, RegisteredBuffer | None)
+
+    def _segment(self, other: str, msg_size: int):
+        from multiprocessing import shared_memory
+        name = other + "-" + self.self_id
+        seg = self._segs.get(name)
+        if seg is not None and seg[0].size < msg_size:
+            self._close_one(name)
+            seg = None
+        if seg is None:
+            shm = shared_memory.SharedMemory(name)
+            if self.untrack:   # python < 3.13 tracks attached segments too and unlinks them at exit
+                try:
+                    from multiprocessing import resource_tracker
+                    resource_tracker.unregister(shm._name, "shared_memory")  # noqa: SLF001
+                except Exception:  # noqa: BLE001
+                    pass
+            reg = RegisteredBuffer(shm.buf) if self.register else None
+            seg = (shm, reg)
+            self._segs[name] = seg
+        return seg
+
+    def get_data(self, other: str, msg_size: int) -> memoryview:
+        """The message bytes in place (the reference returns a copy)."""
+        shm, _ = self._segment(other, msg_size)
+        return shm.buf[:msg_size]
+
+    def loads(self, other: str, msg_size: int):
+        """get_data + zero-copy decode (falls back to cloudpickle for non-update messages)."""
+        return loads(self.get_data(other, msg_size))
+
+    def _close_one(self, name):
+        shm, reg = self._segs.pop(name)
+        if reg is not None:
+            reg.close()
+        del reg
+        try:
+            shm.close()
+        except BufferError:
+            pass   # views still exported; the mapping goes when they do
+
+    def close(self):
+        for name in list(self._segs):
+            self._close_one(name)
 
 
 # ------------------------------------------------------------------ device-resident cache

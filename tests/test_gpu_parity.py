@@ -22,6 +22,7 @@ def _native_loaded():
     from flame_amd import _native
     _native.lib()  # fail loudly if the HIP library is missing
     assert torch.cuda.is_available()
+    torch.empty(1, device=DEV)   # torch's HIP context: is_pinned() of registered memory needs it
 
 
 def make_amd(sort, **kw):
@@ -864,3 +865,42 @@ def test_metric_collector_receives_kernel_metrics():
     assert sd["fedadam.flame_fedopt_reduce_adapt.launches"] == 1, sd
     assert sd["fedadam.flame_fedopt_reduce_adapt.runtime"] > 0
     assert sd["fedadam.flame_fedopt_reduce_adapt.hbm_GBps"] > 0
+
+
+@pytest.mark.parametrize("where", ["zero_copy", "device_cache"])
+def test_shm_receiver_registered_segment_to_fedavg(where):
+    """LIFL SHM receive without host copies (flame_amd.ingest.ShmReceiver): each sender's
+    segment is registered once; updates are either streamed by the kernel straight out of
+    the shared segment or copied to HBM by DeviceUpdateCache; FedAvg bitwise == oracle."""
+    import cloudpickle
+    from multiprocessing import shared_memory
+    from flame_amd import ingest
+    O = _oracle()
+    g = torch.Generator().manual_seed(59)
+    n, P = 5, 70_001
+    ws = [{"w": torch.randn(P, generator=g) * 1e-2} for _ in range(n)]
+    counts = [20 + 3 * i for i in range(n)]
+    segs, rx = [], ingest.ShmReceiver("agg", untrack=False)
+    try:
+        cache = ingest.DeviceUpdateCache(device=DEV, placement="hbm") if where == "device_cache" else S.SortedCache()
+        for i, w in enumerate(ws):
+            blob = cloudpickle.dumps({"weights": w, "dataset_size": counts[i]})
+            seg = shared_memory.SharedMemory(name=f"flametest_t{i}-agg", create=True, size=len(blob))
+            seg.buf[:len(blob)] = blob
+            segs.append(seg)
+            msg = rx.loads(f"flametest_t{i}", len(blob))
+            assert msg["weights"]["w"].is_pinned()
+            cache[f"t{i}"] = S.TR(msg["weights"], msg["dataset_size"])
+            del msg
+        base = torch.randn(P, generator=g)
+        out = make_amd("fedavg").do({"w": base.to(DEV)}, cache, total=sum(counts))
+        torch.cuda.synchronize()
+        exp = base.clone()
+        O.reduce_tensor(exp, [w["w"] for w in ws], [c / sum(counts) for c in counts])
+        S.assert_bitwise("shm", S.to_cpu(out), {"w": exp})
+        del cache, out
+    finally:
+        rx.close()
+        for seg in segs:
+            seg.close()
+            seg.unlink()

@@ -137,3 +137,28 @@ def test_decode_property_random_messages():
             g, r = g.view(torch.int16), r.view(torch.int16)
         assert torch.equal(g, r)
     check()
+
+
+def test_shm_receiver_decodes_in_place():
+    """ShmReceiver (backend/shm.py:386-391 stand-in) decodes a message in the sender's
+    segment without copying: the tensors alias the shared memory."""
+    import numpy as np
+    from multiprocessing import shared_memory
+    w = {"w": torch.arange(1000, dtype=torch.float32), "b": torch.ones(3, dtype=torch.bfloat16)}
+    blob = cloudpickle.dumps({"weights": w, "dataset_size": 77})
+    seg = shared_memory.SharedMemory(name="flametest_a-agg", create=True, size=len(blob) + 64)
+    try:
+        seg.buf[:len(blob)] = blob
+        rx = ingest.ShmReceiver("agg", register=False, untrack=False)   # same process as the writer
+        msg = rx.loads("flametest_a", len(blob))
+        assert msg["dataset_size"] == 77
+        assert torch.equal(msg["weights"]["w"], w["w"]) and torch.equal(msg["weights"]["b"], w["b"])
+        mapping = rx._segs["flametest_a-agg"][0].buf
+        base = np.frombuffer(mapping, dtype=np.uint8).ctypes.data
+        assert base <= msg["weights"]["w"].data_ptr() < base + len(mapping)   # a view, not a copy
+        del mapping
+        del msg
+        rx.close()
+    finally:
+        seg.close()
+        seg.unlink()
