@@ -313,3 +313,33 @@ def fedopt_identical_state_rounds(fx, device):
         exp = {"cur": fx.weights(f"r{r}/cur"), "m": fx.weights(f"r{r}/m"), "v": fx.weights(f"r{r}/v"),
                "avg": fx.weights(f"r{r}/avg")}
         yield r, clients, counts, state, exp
+
+
+def nonfinite_case(dtype, n=5, P=4099, seed=61):
+    """Client updates with NaN, +-inf and values whose weighted sum overflows (a diverged
+    trainer): base, clients, counts."""
+    g = torch.Generator().manual_seed(seed)
+    big = {torch.float32: 3.0e38, torch.bfloat16: 3.0e38, torch.float16: 6.0e4, torch.float64: 1.7e308}[dtype]
+    base = torch.randn(P, generator=g, dtype=torch.float64).to(dtype)
+    cl = []
+    for i in range(n):
+        c = (torch.randn(P, generator=g, dtype=torch.float64) * 1e-2).to(dtype)
+        c[i::97] = float("nan")
+        c[(i + 11)::89] = float("inf")
+        c[(i + 23)::83] = -float("inf")
+        c[(i + 37)::79] = big            # sums of several of these overflow to inf
+        c[(i + 41)::73] = -big
+        cl.append(c)
+    base[::101] = float("nan")
+    base[7::103] = float("inf")
+    return base, cl, [100 + 7 * i for i in range(n)]
+
+
+def assert_same_nonfinite(label, got, exp):
+    """Equal where finite or infinite (bitwise), NaN in exactly the same places.  NaN sign /
+    payload bits are not pinned: IEEE 754 leaves them open and torch-CPU's depend on the ISA."""
+    g = got.detach().cpu().double()
+    e = exp.detach().cpu().double()
+    gn, en = torch.isnan(g), torch.isnan(e)
+    assert torch.equal(gn, en), f"{label}: NaN positions differ ({int((gn ^ en).sum())} elements)"
+    assert torch.equal(g[~gn], e[~en]), f"{label}: non-NaN values differ"

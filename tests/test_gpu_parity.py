@@ -904,3 +904,35 @@ def test_shm_receiver_registered_segment_to_fedavg(where):
         for seg in segs:
             seg.close()
             seg.unlink()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_nonfinite_updates_match_oracle(dtype):
+    """A diverged trainer (NaN, +-inf, overflowing sums): FedAvg and FedBuff + scale_add put
+    NaN and +-inf exactly where the oracle (== the reference's torch-CPU ops) does, and
+    every other element bitwise."""
+    O = _oracle()
+    base, cl, counts = S.nonfinite_case(dtype)
+    tot = sum(counts)
+    cache = S.SortedCache()
+    for i, c in enumerate(cl):
+        cache[f"e{i}"] = S.TR({"w": c.to(DEV)}, counts[i])
+    got = make_amd("fedavg").do({"w": base.to(DEV)}, cache, total=tot)["w"]
+    exp = base.clone()
+    O.reduce_tensor(exp, cl, [c / tot for c in counts])
+    assert torch.isnan(exp).sum() > 10 and torch.isinf(exp).sum() > 10
+    S.assert_same_nonfinite(f"fedavg {dtype}", got, exp)
+    if dtype == torch.float64:
+        return
+    fb, agg, ofb, oagg = make_amd("fedbuff"), None, O.OracleFedBuff(), None
+    for i, c in enumerate(cl):
+        c1, c2 = S.SortedCache(), S.SortedCache()
+        c1["a"] = S.TR({"w": c.to(DEV)}, 1, 9 - i % 3)
+        c2["a"] = S.TR({"w": c.clone()}, 1, 9 - i % 3)
+        agg = fb.do(agg, c1, total=1, version=9)
+        oagg = ofb.do(oagg, c2, total=1, version=9)
+    w = {"w": base.to(DEV)}
+    fb.scale_add_agg_weights(w, agg, len(cl))
+    ow = {"w": base.clone()}
+    ofb.scale_add_agg_weights(ow, oagg, len(cl))
+    S.assert_same_nonfinite(f"fedbuff {dtype}", w["w"], ow["w"])

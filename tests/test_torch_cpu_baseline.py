@@ -2,6 +2,7 @@
 sequence: replayed through the golden drivers it reproduces the reference's
 outputs bitwise -- FedOPT included, since it is the same torch-CPU sqrt."""
 import pytest
+import torch
 
 import scenarios as S
 from oracle import torch_cpu
@@ -67,3 +68,18 @@ def _make(sort, **kw):
 def test_torch_cpu_matches_golden(golden, name, driver):
     for label, got, exp in driver(golden(name), _make, "cpu"):
         S.assert_bitwise(f"{name}:{label}", got, exp)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_oracle_nonfinite_matches_reference_ops(dtype):
+    """NaN / inf / overflowing client updates: the C oracle puts NaN and +-inf exactly where
+    the reference's torch-CPU op sequence (fedavg.py:84-104) does."""
+    from oracle import oracle as O
+    base, cl, counts = S.nonfinite_case(dtype)
+    tot = sum(counts)
+    exp = {"w": base.clone()}
+    torch_cpu.fedavg_round(exp, [{"w": c} for c in cl], counts, tot)
+    got = base.clone()
+    O.reduce_tensor(got, cl, [c / tot for c in counts])
+    assert torch.isinf(exp["w"]).sum() > 10 and torch.isnan(exp["w"]).sum() > 10
+    S.assert_same_nonfinite(str(dtype), got, exp["w"])
