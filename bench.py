@@ -59,7 +59,7 @@ def parse():
                     help="hier_fedbuff: the node's middles AND the top in one pass (fused, "
                          "flame_hier_fedbuff), co-located middles in one launch (group) or one by one")
     ap.add_argument("--workload", default="fedavg",
-                    choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff"])
+                    choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff", "feddyn", "scaffold"])
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
     ap.add_argument("--params", type=int, default=None,
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
@@ -268,6 +268,72 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5):
     return nbytes / statistics.median(ts) / 1e9
 
 
+def make_clients(args, n, P, rank, dev):
+    """n synthetic fp32 client updates of P params in HBM (tiled slab or one row each)."""
+    from flame_amd import engine
+    if args.layout == "slab":
+        from flame_amd.slab import UpdateSlab
+        store = UpdateSlab({"model": torch.empty(P, dtype=torch.float32)}, capacity=n, device=dev)
+        tmp = torch.empty(P, dtype=torch.float32, device=dev)
+        client_w = []
+        for i in range(n):
+            engine.synth_fill_(tmp, args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+            client_w.append(store.put({"model": tmp}))        # tiled slot views, held for the run
+        del tmp
+        return client_w, store.storage[torch.float32], (lambda i: store.read(i, "model").cpu())
+    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
+    for i in range(n):
+        engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+    return [{"model": slab[i]} for i in range(n)], slab, (lambda i: slab[i].cpu())
+
+
+def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
+    """FedDyn (feddyn.py:70-139) / SCAFFOLD (scaffold.py:92-150) server rounds through the
+    drop-ins: every trainer active each round, updates (and SCAFFOLD control variates)
+    resident in HBM.  Reports the round's kernels priced by their algorithmic bytes."""
+    from flame_amd.optimizers import optimizer_provider
+    keys = [f"{i:05d}" for i in range(n)]
+    if args.workload == "feddyn":
+        opt = optimizer_provider.get("feddyn", alpha=0.01)
+    else:
+        opt = optimizer_provider.get("scaffold", k=3)
+        opt.save_state("pre", dataset_sizes={k: int(c) for k, c in zip(keys, counts)},
+                       glob_weights={"model": base})
+    state = {"weights": {"model": base}}
+
+    def step():
+        cache = Cache()
+        for i, k in enumerate(keys):
+            cache[k] = TR(client_w[i], int(counts[i]))
+        if args.workload == "feddyn":
+            opt.save_state("pre", active_ends=keys)   # the role's per-round call (feddyn top_aggregator)
+            state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=n)
+        else:
+            ctl = Cache()
+            for i, k in enumerate(keys):    # control variates: the same synthetic tensors stand in
+                ctl[k] = TR(client_w[n - 1 - i], 1)
+            state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=n,
+                                      control_cache=ctl)
+
+    step()  # FedDyn: the first round copies every trainer's history (untimed, as FedOPT's round 1)
+    elapsed, events = timed(world, args.steps, args.warmup, step)
+    ks = kernel_stats(events, "flame_agg_reduce")
+    if rank == 0:
+        k_time = ks["avg_s"] * ks["launches"] / args.steps
+        k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
+        print(json.dumps({
+            "metric": f"aggregated params/sec (device-resident), {args.workload} server round",
+            "value": n * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32",
+            "config": {"workload": f"{args.workload}: {n} clients x {P} fp32 params, {args.layout} layout"},
+            "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": "flame_agg_reduce",
+                         "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
+                         "algorithmic_bytes_per_step": k_bytes,
+                         "bytes_per_client_param": k_bytes / (n * P * 4)},
+        }), flush=True)
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args.force_shard)
@@ -279,33 +345,18 @@ def main():
     if args.workload == "hier_fedbuff":
         return bench_hier(args, world, rank, dev)
 
-    n = args.clients or 1024
+    n = args.clients or (512 if args.workload in ("feddyn", "scaffold") else 1024)
     P = args.params or 25_000_000
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
         return bench_e2e(args, n, P, dev)
-    if args.layout == "slab":
-        from flame_amd.slab import UpdateSlab
-        store = UpdateSlab({"model": torch.empty(P, dtype=torch.float32)}, capacity=n, device=dev)
-        tmp = torch.empty(P, dtype=torch.float32, device=dev)
-        client_w = []
-        for i in range(n):
-            engine.synth_fill_(tmp, args.seed, 1 + i + rank * 100_000, 0, 1e-2)
-            client_w.append(store.put({"model": tmp}))        # tiled slot views, held for the run
-        del tmp
-        slab_buf = store.storage[torch.float32]
-        host_row = lambda i: store.read(i, "model").cpu()    # noqa: E731
-    else:
-        slab = torch.empty((n, P), dtype=torch.float32, device=dev)
-        for i in range(n):
-            engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
-        client_w = [{"model": slab[i]} for i in range(n)]
-        slab_buf = slab
-        host_row = lambda i: slab[i].cpu()                   # noqa: E731
+    client_w, slab_buf, host_row = make_clients(args, n, P, rank, dev)
     base = torch.empty(P, dtype=torch.float32, device=dev)
     engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
-    base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
     counts = synth.counts(args.seed, n)
+    if args.workload in ("feddyn", "scaffold"):
+        return bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts)
+    base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
     total = int(counts.sum())
     keys = [f"{i:05d}" for i in range(n)]
     torch.cuda.synchronize()
