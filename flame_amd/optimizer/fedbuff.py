@@ -257,7 +257,8 @@ def _hier_rows(aggs, keys, device):
     slab = getattr(first, "slab", None)
     if (slab is not None and slab.device == device
             and all(getattr(w, "slab", None) is slab for a in aggs for w, _ in a._pending)
-            and all(k in slab.meta for k in keys)):
+            and all(k in slab.meta and slab.meta[k][0] == aggs[0]._meta[k][1]
+                    and slab.meta[k][2] == math.prod(aggs[0]._meta[k][0]) for k in keys)):
         slots = np.fromiter((w.slot for a in aggs for w, _ in a._pending), dtype=np.uint64)
         rows = {}
         for k in keys:
@@ -326,7 +327,7 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
             if (engine.dtype_code(dt) not in (engine.N.FLAME_F32, engine.N.FLAME_BF16, engine.N.FLAME_F16)
                     or any(t is None or t.dtype != dt or t.numel() != n or t.device != device
                            or not t.is_contiguous() for t in tensors)
-                    or any(a._meta[k][1] != dt for a in aggs)):
+                    or any(a._meta[k][1] != dt or math.prod(a._meta[k][0]) != n for a in aggs)):
                 fusable = False
                 break
     if fusable:

@@ -811,6 +811,10 @@ def test_hierarchy_round_launch_count_and_fallback():
     mids[1] = (mids[1][0], mids[1][1], 2, rnd + 1)
     with pytest.raises(ZeroDivisionError):
         hierarchy_round(mids, None, version=rnd)
+    mids = middles([2, 2])
+    mids[0] = ({"x": torch.zeros(776, device=DEV)}, mids[0][1], 2, rnd)   # weights / arrivals numel differ
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        hierarchy_round(mids, None, version=rnd)
 
 
 def test_reduce_slab_range_pieces_equal_full_reduce():
