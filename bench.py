@@ -238,8 +238,11 @@ def kernel_stats(events, name):
 
 
 def read_ceiling(buf: torch.Tensor, reps: int = 5):
-    """Same-device HBM streaming-read ceiling (tools/hbm_probe.hip, best measured config:
-    16,384 workgroups, 16 nt dwordx4 loads in flight per lane) over an existing buffer."""
+    """Same-device HBM streaming-read ceiling over an existing buffer (tools/hbm_probe.hip):
+    the best of a grid-stride read (16,384 workgroups, 16 nt dwordx4 loads in flight per
+    lane) and a region-streaming read (each workgroup one contiguous 1 MiB region, 16 loads
+    per lane -- the product kernel's access pattern with the fastest region size measured).
+    Returns (best GB/s, {probe: GB/s})."""
     import ctypes
     import subprocess
     so = os.path.join(ROOT, "build", "hbm_probe.so")
@@ -249,23 +252,33 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5):
             subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
                                    "-o", so, os.path.join(ROOT, "tools", "hbm_probe.hip")])
         L = ctypes.CDLL(so)
+        L.probe_read_region.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
     except Exception:  # noqa: BLE001
-        return None
+        return None, {}
     L.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                              ctypes.c_void_p]
-    nbytes = buf.numel() * buf.element_size() // 4096 * 4096
+    nbytes = buf.numel() * buf.element_size() // (1 << 20) * (1 << 20)
     out = torch.zeros(4, dtype=torch.int32, device=buf.device)
     st = torch.cuda.current_stream(buf.device).cuda_stream
-    ts = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        if L.probe_read(buf.data_ptr(), nbytes, out.data_ptr(), 16384, 2, st) != 0:
-            return None
-        e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1) / 1e3)
-    return nbytes / statistics.median(ts) / 1e9
+    probes = {
+        "grid_stride_16384wg_16ld": lambda: L.probe_read(buf.data_ptr(), nbytes, out.data_ptr(), 16384, 2, st),
+        "region_1MiB_16ld": lambda: L.probe_read_region(buf.data_ptr(), nbytes, out.data_ptr(), 1 << 20, 1 << 20,
+                                                        16, st),
+    }
+    res = {}
+    for name, launch in probes.items():
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if launch() != 0:
+                return None, {}
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 1e3)
+        res[name] = nbytes / statistics.median(ts) / 1e9
+    return max(res.values()), res
 
 
 def make_clients(args, n, P, rank, dev):
@@ -408,7 +421,7 @@ def main():
         elif world == 1 and args.cpu_clients > 0:
             cpu = cpu_baseline_fedopt(args.workload, host_row, n, P, base0, counts, args.cpu_clients,
                                       args.cpu_rounds)
-        ceiling = read_ceiling(slab_buf) if world == 1 else None
+        ceiling, probes = read_ceiling(slab_buf) if world == 1 else (None, {})
         # a piece-pipelined step has several launches: price the step's kernels as one
         launches_per_step = ks["launches"] / args.steps
         k_time = ks["avg_s"] * launches_per_step
@@ -442,7 +455,7 @@ def main():
                 "kernel": name, "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
                 "launches_per_step": launches_per_step,
                 # same device, same buffer: plain streaming-read probe (tools/hbm_probe.hip)
-                "measured_read_ceiling_GBps": ceiling,
+                "measured_read_ceiling_GBps": ceiling, "read_probes_GBps": probes,
                 "frac_of_measured_ceiling": (achieved / ceiling) if ceiling else None,
             },
             "cpu_baseline": cpu,

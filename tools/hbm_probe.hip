@@ -58,3 +58,39 @@ extern "C" int probe_read_lds(const void* p, int64_t bytes, int blocks, int nt, 
     else hipLaunchKernelGGL(read_lds_kernel<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, pieces);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Region-streaming read: workgroup w reads ONE contiguous region [w*R, (w+1)*R) in 4 KiB
+// steps (256 lanes x 16 B), UN steps in flight -- the access pattern of the product
+// kernel over the tiled UpdateSlab (each workgroup streams its N x 4 KiB tile column).
+template <int UN>
+__global__ __launch_bounds__(256) void read_region_kernel(const uint8_t* __restrict__ p, int64_t region,
+                                                          int64_t pitch, int64_t bytes, uint32_t* out) {
+    const int64_t b0 = (int64_t)blockIdx.x * pitch;
+    const int64_t b1 = b0 + region < bytes ? b0 + region : bytes;
+    uint32_t acc = 0;
+    int64_t off = b0 + threadIdx.x * 16;
+    for (; off + (UN - 1) * 4096 + 16 <= b1; off += UN * 4096) {
+        u4 v[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(p + off + u * 4096));
+#pragma unroll
+        for (int u = 0; u < UN; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    for (; off + 16 <= b1; off += 4096) {
+        u4 v = *(const u4*)(p + off);
+        acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// pitch = bytes between consecutive regions' starts (>= region; the gap is not read).
+extern "C" int probe_read_region(const void* p, int64_t bytes, void* out, int64_t region, int64_t pitch, int un,
+                                 void* stream) {
+    if (region < 4096 || region % 4096 || pitch < region || pitch % 16) return 2;
+    const int64_t blocks = bytes / pitch;
+    if (blocks < 1 || blocks > 0x7FFFFFFF) return 2;
+    if (un == 16) hipLaunchKernelGGL((read_region_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, region, pitch, bytes, (uint32_t*)out);
+    else hipLaunchKernelGGL((read_region_kernel<8>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, region, pitch, bytes, (uint32_t*)out);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -43,6 +43,26 @@ def main():
             res[f"blocks{blocks}_nt{nt}"] = {"ms": t, "GBps": nbytes / t / 1e6}
             print(f"blocks {blocks:6d} nt {nt} (2: nt + 16 loads/lane): {t:8.3f} ms  {nbytes / t / 1e6:8.1f} GB/s",
                   flush=True)
+    L.probe_read_region.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int, ctypes.c_void_p]
+    regions = [(1 << 20, 0), (4 << 20, 0), (16 << 20, 0), (4 << 20, 4096), (4 << 20, 1024), (4 << 20, 65536),
+               (4 << 20, 256), (16 << 20, 4096), (1 << 20, 4096)]
+    for region, pad in regions:
+        for un in (16,):
+            ts = []
+            pitch = region + pad
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                assert L.probe_read_region(buf.data_ptr(), nbytes, out.data_ptr(), region, pitch, un, st) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            t = statistics.median(ts)
+            rb = (nbytes // pitch) * region
+            res[f"region{region >> 20}M_pad{pad}_un{un}"] = {"ms": t, "GBps": rb / t / 1e6}
+            print(f"region {region >> 20:3d} MiB + pad {pad:6d} B per WG, {un} loads/lane: {t:8.3f} ms  "
+                  f"{rb / t / 1e6:8.1f} GB/s", flush=True)
     L.probe_read_lds.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     for blocks in (1024, 2048, 4096):
         for nt in (0, 1):
