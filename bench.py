@@ -58,6 +58,11 @@ def parse():
     ap.add_argument("--hier-mode", default="fused", choices=["fused", "group", "serial"],
                     help="hier_fedbuff: the node's middles AND the top in one pass (fused, "
                          "flame_hier_fedbuff), co-located middles in one launch (group) or one by one")
+    ap.add_argument("--hier-middles", default="own", choices=["own", "fetched"],
+                    help="hier_fedbuff fused: own = every middle keeps its own weights, updated in place; "
+                         "fetched = the middles hold the top model they fetched this round (one shared "
+                         "tensor, read-only: their updated weights only feed the upload delta and are "
+                         "replaced at the next fetch, asyncfl/middle_aggregator.py:119-120,244-246)")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff", "feddyn", "scaffold"])
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
@@ -489,6 +494,7 @@ def bench_hier(args, world, rank, dev):
     gw = torch.empty(P, dtype=dt, device=dev)
     engine.synth_fill_(gw, args.seed + 4, rank * 100_000, 0, 1.0)
     mids = [gw.clone() for _ in range(M)]
+    gw_fetched = gw.clone()   # --hier-middles fetched: the model every middle fetched from the top
     stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
     rnd = 10
     full = torch.empty(P * world, dtype=dt, device=dev) if world > 1 else None
@@ -560,8 +566,10 @@ def bench_hier(args, world, rank, dev):
                 cache = Cache()
                 cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
                 aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
-        hierarchy_round([({"model": mids[m]}, aggs[m], C, rnd - (m % 2)) for m in range(M)], None,
-                        version=rnd, top_weights={"model": gw}, top_goal=M)
+        fetched = args.hier_middles == "fetched"
+        hierarchy_round([({"model": gw_fetched if fetched else mids[m]}, aggs[m], C, rnd - (m % 2))
+                         for m in range(M)], None, version=rnd, top_weights={"model": gw}, top_goal=M,
+                        update_middle_weights=not fetched)
         gather()
 
     step = {"fused": step_fused, "group": step_group, "serial": step_serial}[args.hier_mode]
@@ -577,7 +585,8 @@ def bench_hier(args, world, rank, dev):
     if rank == 0 and args.hier_mode == "fused":
         try:
             for tr in json.load(open(args.traffic))["entries"]:
-                if tr.get("kernel") == names[0] and tr.get("clients") == M * C and tr.get("params") == P:
+                if (tr.get("kernel") == names[0] and tr.get("clients") == M * C and tr.get("params") == P
+                        and tr.get("middle_weights", "own") == args.hier_middles):
                     traffic = tr["hbm_bytes_per_launch"]
         except Exception:  # noqa: BLE001
             pass
@@ -588,7 +597,7 @@ def bench_hier(args, world, rank, dev):
             "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
             "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU",
-                                        "middles": args.hier_mode},
+                                        "middles": args.hier_mode, "middle_weights": args.hier_middles},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,
                          "kernel": names[0]},

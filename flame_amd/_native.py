@@ -21,6 +21,7 @@ FLAME_OPT_STATE_ZERO = 1
 FLAME_SEG_UNALIGNED = 1
 FLAME_HIER_TOP_ACCUM = 1
 FLAME_HIER_TOP_APPLY = 2
+FLAME_HIER_MID_READONLY = 4
 HIER_SEGMENT_INT64S = 8  # sizeof(flame_hier_segment) / 8
 SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
 

@@ -71,6 +71,12 @@ namespace {
 #ifndef FLAME_HPF
 #define FLAME_HPF 0       // hierarchy kernel: load each middle's weights before its arrival loop
 #endif
+#ifndef FLAME_HDIAG
+#define FLAME_HDIAG 0     // DIAGNOSTIC sweep variants only: 1 = skip middle-weight stores, 2 = also skip their loads
+#endif
+#ifndef FLAME_HST
+#define FLAME_HST FLAME_ST_NT  // hierarchy kernel: store policy of the middle weights (encoding of FLAME_ST_NT)
+#endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
@@ -223,6 +229,24 @@ __device__ __forceinline__ void st_v(void* p, const V16& v) {
 #else
     *G(reinterpret_cast<u4*>(p)) = x;
 #endif
+}
+// Store with an explicit policy (same encoding as FLAME_ST_NT).
+template <int POL>
+__device__ __forceinline__ void st_pol(void* p, const V16& v) {
+    u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+    if constexpr (POL == 1) {
+        __builtin_nontemporal_store(x, G(reinterpret_cast<u4*>(p)));
+    } else if constexpr (POL == 2) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 3) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 4) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 5) {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else {
+        *G(reinterpret_cast<u4*>(p)) = x;
+    }
 }
 template <typename T> __device__ __forceinline__ T ld1(const T* p) { return *G(p); }
 template <typename T> __device__ __forceinline__ void st1(T* p, T x) { *G(p) = x; }
@@ -741,6 +765,9 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                 T w[EPT], d[EPT];
 #if FLAME_HPF
                 unpack<T, EPT>(wv[v], w);
+#elif FLAME_HDIAG == 2
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) w[j] = T(0);
 #else
                 unpack<T, EPT>(ld_v(wp + v * VS), w);
 #endif
@@ -750,7 +777,10 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                     const A t = X::tmp(d[j], rt, 0.0);
                     top[v][j] = have_top ? X::add(top[v][j], t) : t;
                 }
-                st_v(wp + v * VS, pack<T, EPT>(w));
+#if FLAME_HDIAG
+                if (__builtin_expect(w[0] == T(0x1234) && w[1] == T(0x4321), 0))   // keeps the math live
+#endif
+                if (!(flags & FLAME_HIER_MID_READONLY)) st_pol<FLAME_HST>(wp + v * VS, pack<T, EPT>(w));
                 if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
             }
             have_top = true;
@@ -796,7 +826,7 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                 if (e0 + o >= sg.numel) continue;
                 T w = ld1(wp + o), d;
                 S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
-                st1(wp + o, w);
+                if (!(flags & FLAME_HIER_MID_READONLY)) st1(wp + o, w);
                 if (dp) st1(dp + o, d);
                 const A t = X::tmp(d, rt, 0.0);
                 top[v][j] = have_top ? X::add(top[v][j], t) : t;
@@ -989,7 +1019,7 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     if (n_mids < 1 || n_clients < 1) return set_err(FLAME_EINVAL, "flame_hier_fedbuff: need >= 1 middle and >= 1 arrival per middle");
     if (!mid_w || !clients || !mid_rates || !mid_goal || !top_rates)
         return set_err(FLAME_EINVAL, "flame_hier_fedbuff: NULL table");
-    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY))
+    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY | FLAME_HIER_MID_READONLY))
         return set_err(FLAME_EINVAL, "flame_hier_fedbuff: unknown flags 0x%x", flags);
     if ((flags & FLAME_HIER_TOP_APPLY) && top_goal == 0.f) return set_err(FLAME_EINVAL, "top agg_goal must be nonzero");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -519,20 +519,23 @@ def plan_hier(code: int, segs: Sequence[HierSeg], mid_rates, mid_goals, top_rate
 
 
 def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_rates, *, top_accum: bool,
-                  top_goal: Optional[int], device, keep: list) -> None:
+                  top_goal: Optional[int], device, keep: list, mid_readonly: bool = False) -> None:
     """One flame_hier_fedbuff launch (the caller checked dtypes / devices / contiguity)."""
     L = N.lib()
     p = plan_hier(code, segs, mid_rates, mid_goals, top_rates)
     dm = _staging.upload(p.meta, device)
     b = dm.data_ptr()
-    flags = (N.FLAME_HIER_TOP_ACCUM if top_accum else 0) | (N.FLAME_HIER_TOP_APPLY if top_goal is not None else 0)
+    flags = ((N.FLAME_HIER_TOP_ACCUM if top_accum else 0) | (N.FLAME_HIER_TOP_APPLY if top_goal is not None else 0)
+             | (N.FLAME_HIER_MID_READONLY if mid_readonly else 0))
     with_delta = any(s.mid_delta is not None for s in segs)
     P = sum(s.numel for s in segs)
     isz = ITEMSIZE[code]
     M, C = p.n_mids, p.n_clients
     # arrivals + middle weights (read, write) [+ deltas] + top (in) + top out [+ top weights r/w]
-    nbytes = isz * P * (M * C + 2 * M + (M if with_delta else 0) + (1 if top_accum else 0) + 1
-                        + (2 if top_goal is not None else 0))
+    # distinct middle-weight tensors (read-only middles may share one base: it is read once)
+    wsum = sum(s.numel * len(set(int(p) for p in s.mid_w)) for s in segs)
+    nbytes = isz * (P * (M * C + (M if with_delta else 0) + (1 if top_accum else 0) + 1
+                         + (2 if top_goal is not None else 0)) + wsum * (1 if mid_readonly else 2))
     with _timed("flame_hier_fedbuff", device, nbytes):
         N.check(L.flame_hier_fedbuff(code, flags, b + p.offs["segs"], p.n_segs, p.n_chunks, M, C,
                                      b + p.offs["mid_w"], b + p.offs["mid_delta"] if with_delta else None,

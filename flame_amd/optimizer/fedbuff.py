@@ -236,12 +236,14 @@ class _OneEntryCache(dict):
         return iter(list(self.keys()))
 
 
-def _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta):
+def _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta, update_middle_weights=True):
     """The reference's op sequence with the separate launches (fallback of hierarchy_round)."""
     from .train_result import TrainResult
     top = FedBuff()
     deltas = []
     for w, agg, goal, mv in middles:
+        if not update_middle_weights:
+            w = {k: v.clone() for k, v in w.items()}
         _, d = FedBuff().scale_add_agg_weights_with_delta(w, agg, goal)
         deltas.append(d)
         cache = _OneEntryCache(mid=TrainResult(d, 1, mv))
@@ -282,7 +284,7 @@ def _hier_rows(aggs, keys, device):
 
 
 def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, top_goal=None,
-                    with_delta: bool = False):
+                    with_delta: bool = False, update_middle_weights: bool = True):
     """A node's co-located two-level FedBuff hierarchy in ONE pass per dtype.
 
     ``middles``: sequence of ``(mid_weights, mid_agg, mid_goal, mid_version)`` in the order
@@ -299,6 +301,12 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
 
     The middle aggregates stay valid: their queued arrivals are kept and reduced again
     if anything reads them later.
+
+    ``update_middle_weights=False`` leaves the middles' weights untouched (nothing is
+    written back; the same tensor may then serve several middles).  That is the async
+    hierarchy as the reference composes it: a middle's updated weights only feed its
+    upload delta (asyncfl/middle_aggregator.py:244-246) and are replaced by the top's
+    model at its next fetch (:119-120) -- here the delta goes straight to the top.
     """
     middles = list(middles)
     if not middles:
@@ -330,11 +338,15 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
                     or any(a._meta[k][1] != dt or math.prod(a._meta[k][0]) != n for a in aggs)):
                 fusable = False
                 break
+    if fusable and update_middle_weights:
+        # middles updated in place must not share tensors (the separate calls would chain them)
+        fusable = all(len({w[k].data_ptr() for w, _, _, _ in middles}) == len(middles) for k in keys)
     if fusable:
         rows, keep = _hier_rows(aggs, keys, device)
         fusable = rows is not None
     if not fusable:
-        return _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta)
+        return _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta,
+                                  update_middle_weights)
 
     top_accum = top_agg is not None
     if isinstance(top_agg, DeferredAggregate):
@@ -367,6 +379,7 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
                 top_w=top_weights[k].data_ptr() if top_weights is not None else 0,
                 top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride))
         engine.hier_fedbuff_(segs, code, mid_rates, mid_goals, top_rates, top_accum=top_accum,
-                             top_goal=top_goal if top_weights is not None else None, device=device, keep=keep)
+                             top_goal=top_goal if top_weights is not None else None, device=device, keep=keep,
+                             mid_readonly=not update_middle_weights)
     engine._keepalive(keep, device)
     return result, deltas

@@ -159,6 +159,10 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment *segs, int32_t n_segs
 /* flame_hier_fedbuff flags */
 #define FLAME_HIER_TOP_ACCUM 1u  /* the top aggregate exists (not None): start from seg.top_agg_in */
 #define FLAME_HIER_TOP_APPLY 2u  /* finish with the top's scale-add into seg.top_w */
+#define FLAME_HIER_MID_READONLY 4u  /* do not write w_m' back: the middles' weights are only the
+                                      base of their deltas (the async middle role replaces them with
+                                      the top's model at its next fetch,
+                                      asyncfl/middle_aggregator.py:119-120); mid_w may then alias */
 
 /* One contiguous run of elements of the hierarchy (one state_dict tensor). */
 typedef struct flame_hier_segment {
@@ -183,7 +187,8 @@ typedef struct flame_hier_segment {
  * tmp(v, r) = round(v * r).  Bit-identical to flame_agg_reduce (INIT_FIRST) per middle +
  * flame_fedbuff_scale_add with delta + one flame_agg_reduce per delta on the top aggregate +
  * flame_fedbuff_scale_add; the middle aggregates never reach HBM.
- *   mid_w     : device [n_segs][n_mids] pointers to each middle's weights (in/out)
+ *   mid_w     : device [n_segs][n_mids] pointers to each middle's weights (in/out; in only with
+ *               FLAME_HIER_MID_READONLY)
  *   mid_delta : device [n_segs][n_mids] pointers for the deltas (NULL table or NULL entries:
  *               not stored)
  *   clients   : device [n_segs][n_mids][n_clients] arrival pointers, arrival order per middle

@@ -776,6 +776,47 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start):
     S.assert_bitwise("oracle top w", fused[3], tw)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hierarchy_round_readonly_middles(dtype):
+    """update_middle_weights=False (FLAME_HIER_MID_READONLY): middle weights untouched, the
+    same tensor may serve every middle, and the top aggregate / top weights / deltas equal
+    those of the in-place run with private copies, bitwise."""
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    g = torch.Generator().manual_seed(67)
+    M, C, rnd, P = 4, 3, 8, 5000
+    ups = [[(torch.randn(P, generator=g) * 1e-2).to(dtype) for _ in range(C)] for _ in range(M)]
+    fetched = torch.randn(P, generator=g).to(dtype)
+    top0 = torch.randn(P, generator=g).to(dtype)
+
+    def aggs():
+        out = []
+        for m in range(M):
+            opt, a = make_amd("fedbuff"), None
+            for t in range(C):
+                cache = S.SortedCache()
+                cache["a"] = S.TR({"x": ups[m][t].to(DEV)}, 1, rnd - (m + t) % 3)
+                a = opt.do(a, cache, total=1, version=rnd)
+            out.append(a)
+        return out
+
+    shared = fetched.to(DEV)
+    tw_ro = {"x": top0.to(DEV)}
+    agg_ro, d_ro = hierarchy_round([({"x": shared}, a, C, rnd - m % 2) for m, a in enumerate(aggs())], None,
+                                   version=rnd, top_weights=tw_ro, top_goal=M, with_delta=True,
+                                   update_middle_weights=False)
+    own = [{"x": fetched.to(DEV)} for _ in range(M)]
+    tw = {"x": top0.to(DEV)}
+    agg, d = hierarchy_round([(own[m], a, C, rnd - m % 2) for m, a in enumerate(aggs())], None,
+                             version=rnd, top_weights=tw, top_goal=M, with_delta=True)
+    torch.cuda.synchronize()
+    assert torch.equal(shared.cpu().view(torch.int16 if dtype != torch.float32 else torch.int32),
+                       fetched.view(torch.int16 if dtype != torch.float32 else torch.int32))
+    S.assert_bitwise("top agg", S.to_cpu(dict(agg_ro)), S.to_cpu(dict(agg)))
+    S.assert_bitwise("top w", S.to_cpu(tw_ro), S.to_cpu(tw))
+    for m in range(M):
+        S.assert_bitwise(f"delta m{m}", S.to_cpu(d_ro[m]), S.to_cpu(d[m]))
+
+
 def test_hierarchy_round_launch_count_and_fallback():
     """Uniform middles take ONE flame_hier_fedbuff launch per dtype; ragged arrival counts
     fall back to the separate launches with the same results; stale versions raise as
