@@ -91,6 +91,38 @@ def test_golden_hier_fused_delta(golden):
         S.assert_bitwise(f"m{mid}/delta", delta, fx.weights(f"m{mid}/delta"))
 
 
+@pytest.mark.parametrize("update_middle_weights", [True, False])
+def test_golden_hier_one_pass(golden, update_middle_weights):
+    """The whole 2-middle x 3-arrival hierarchy of the reference-generated fixture in ONE
+    flame_hier_fedbuff launch (hierarchy_round): middle deltas and the top model bitwise
+    equal the reference's (make_golden.py drove flame's own FedBuff + delta_weights)."""
+    from flame_amd import engine
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    fx = golden("hier_fedbuff_small.npz")
+    rnd = fx.meta["round"]
+    top_w0 = fx.weights("top_w0")
+    middles = []
+    shared = S.to_dev(top_w0, DEV)
+    for mid in range(2):
+        opt, agg = make_amd("fedbuff"), None
+        for t in range(3):
+            c = S.SortedCache()
+            c[f"m{mid}t{t}"] = S.TR(S.to_dev(fx.weights(f"m{mid}/update{t}"), DEV), 10 + t, rnd - t % 2)
+            agg = opt.do(agg, c, total=10 + t, version=rnd)
+        middles.append((S.to_dev(top_w0, DEV) if update_middle_weights else shared, agg, 3, rnd - mid))
+    top = S.to_dev(top_w0, DEV)
+    engine.kernel_events = []
+    try:
+        _, deltas = hierarchy_round(middles, None, version=rnd, top_weights=top, top_goal=2, with_delta=True,
+                                    update_middle_weights=update_middle_weights)
+        assert [e[0] for e in engine.kernel_events] == ["flame_hier_fedbuff"] * len({v.dtype for v in top.values()})
+    finally:
+        engine.kernel_events = None
+    for mid in range(2):
+        S.assert_bitwise(f"m{mid}/delta", S.to_cpu(deltas[mid]), fx.weights(f"m{mid}/delta"))
+    S.assert_bitwise("top_out", S.to_cpu(top), fx.weights("top_out"))
+
+
 # ------------------------------------------------------------------ oracle comparisons
 def _oracle():
     from oracle import oracle as O
