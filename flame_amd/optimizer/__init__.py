@@ -5,6 +5,7 @@ from .fedadam import FedAdam
 from .fedavg import FedAvg
 from .fedbuff import FedBuff
 from .feddyn import FedDyn
+from .fedgft import FedGFT
 from .fedopt import FedOPT
 from .fedprox import FedProx
 from .fedyogi import FedYogi
@@ -12,4 +13,4 @@ from .scaffold import Scaffold
 from .train_result import TrainResult
 
 __all__ = ["AbstractOptimizer", "FedAvg", "FedOPT", "FedAdam", "FedYogi", "FedAdaGrad", "FedBuff",
-           "FedProx", "FedDyn", "Scaffold", "TrainResult"]
+           "FedProx", "FedDyn", "FedGFT", "Scaffold", "TrainResult"]

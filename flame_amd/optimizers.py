@@ -5,10 +5,10 @@ flame's own provider so existing roles pick them up unchanged.
 ``OptimizerType`` is a closed enum validated by flame's config
 (config.py:55-70,121-123), so the drop-in re-registers the existing keys
 (``fedavg``, ``fedadagrad``, ``fedadam``, ``fedyogi``, ``fedbuff``, ``fedprox``,
-``feddyn``, ``scaffold``) instead of adding new ones.  ``fedgft`` (a different
-server computation, optimizer/fedgft.py) keeps flame's own class.
+``feddyn``, ``scaffold``, ``fedgft`` -- every key flame registers) instead of
+adding new ones.
 """
-from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedDyn, FedProx, FedYogi, Scaffold
+from .optimizer import FedAdaGrad, FedAdam, FedAvg, FedBuff, FedDyn, FedGFT, FedProx, FedYogi, Scaffold
 
 DROP_INS = {
     "fedavg": FedAvg,
@@ -19,6 +19,7 @@ DROP_INS = {
     "fedprox": FedProx,
     "feddyn": FedDyn,
     "scaffold": Scaffold,
+    "fedgft": FedGFT,
 }
 
 

@@ -140,6 +140,30 @@ class OracleFedAvg:
         return self.agg_weights
 
 
+class OracleFedGFT(OracleFedAvg):
+    """fedgft.py:27-58: FedAvg.do unchanged; update_bias restates bias.py:74-106 (server side)."""
+
+    def __init__(self, fair, gamma, reg="l2"):
+        super().__init__()
+        self.fair = fair
+        self.a = self.b = self.c = self.d = self.val = self.sign = 0.0
+
+    def update_bias(self, dataset_sizes, local_biases):
+        n = sum(dataset_sizes.values())
+        wm = {t: sum([getattr(local_biases[e], t) * dataset_sizes[e] / n for e in local_biases])
+              for t in ("a", "b", "c", "d", "val")}
+        self.a, self.b, self.c, self.d = wm["a"], wm["b"], wm["c"], wm["d"]
+        if self.fair in ("SP", "EOP"):
+            self.val = wm["val"]
+        self.sign = 0.0 if self.val == 0 else (1.0 if self.val > 0 else -1.0)
+
+    def bias_terms(self):
+        return [self.a, self.b, self.c, self.d, self.val, self.sign]
+
+    def get_bias(self):
+        return self.val
+
+
 class OracleFedOPT(OracleFedAvg):
     """fedopt.py:58-129 with the three _delta_v variants."""
 

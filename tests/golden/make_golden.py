@@ -409,7 +409,55 @@ def scaffold_rounds():
     print("wrote scaffold_rounds.npz")
 
 
-CASES = {"feddyn_rounds": feddyn_rounds, "scaffold_rounds": scaffold_rounds}
+def fedgft_rounds():
+    """FedGFT as its top aggregator drives it (fedgft/top_aggregator.py:52-86 + syncfl
+    aggregate): do(deepcopy(weights), cache, total=...) -- inherited FedAvg.do
+    (fedgft.py:27) -- then update_bias(dataset_sizes, local_biases) with the trainers'
+    Bias terms; per fairness kind SP / EOP / CAL, 3 rounds, bias scalars recorded."""
+    from flame.optimizer.bias import Bias
+    gen = torch.Generator().manual_seed(83)
+    ends = [f"t{i}" for i in range(5)]
+    rounds = [ends, ends[1:], ends[::2]]
+    fw = FixtureWriter()
+    weights = small_weights(gen, FEDDYN_SHAPES, 1.0)
+    fw.put_weights("weights0", weights)
+    biases = {}
+    counts_all, orders = [], []
+    for fair in ("SP", "EOP", "CAL"):
+        opt = optimizer_provider.get("fedgft", fair=fair, gamma=0.5)
+        w = deepcopy(weights)
+        for r, rends in enumerate(rounds):
+            clients = [small_weights(gen, FEDDYN_SHAPES, 1e-2) for _ in rends]
+            counts = [int(x) for x in torch.randint(1, 1001, (len(rends),), generator=gen)]
+            cache = Cache()
+            for e, cw, c in zip(rends, clients, counts):
+                cache[e] = TrainResult(cw, c)
+            order = list(cache.iterkeys())
+            w = opt.do(deepcopy(w), cache, total=sum(counts), num_trainers=len(rends))
+            local = {}
+            terms = []
+            for e in rends:
+                b = Bias(fair=fair, local=True)
+                b.a, b.b, b.c, b.d = [float(x) for x in torch.rand(4, generator=gen, dtype=torch.float64)]
+                b.val = b.a / 1.25 - b.c / 0.75
+                local[e] = b
+                terms.append([b.a, b.b, b.c, b.d, b.val])
+            sizes = dict(zip(rends, counts))
+            opt.update_bias(dataset_sizes=sizes, local_biases=local)
+            tag = f"{fair}/r{r}"
+            for i, cw in enumerate(clients):
+                fw.put_weights(f"{tag}/client{i}", cw)
+            fw.put_weights(f"{tag}/out", w)
+            biases[tag] = {"local": terms, "sizes": sizes, "order": order, "counts": counts,
+                           "global": [opt.bias.a, opt.bias.b, opt.bias.c, opt.bias.d, opt.bias.val,
+                                      opt.bias.sign], "get_bias": opt.get_bias()}
+    fw.meta.update({"kind": "fedgft_rounds", "gamma": 0.5, "rounds": rounds, "fairs": ["SP", "EOP", "CAL"],
+                    "bias": biases})
+    fw.save(os.path.join(HERE, "fedgft_rounds.npz"))
+    print("wrote fedgft_rounds.npz")
+
+
+CASES = {"feddyn_rounds": feddyn_rounds, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():

@@ -271,6 +271,46 @@ def run_scaffold(fx, make_opt, device):
     return res
 
 
+class _LocalBias:
+    """Duck-typed trainer-side Bias terms (bias.py:34-42) as the top aggregator receives them."""
+
+    def __init__(self, a, b, c, d, val):
+        self.a, self.b, self.c, self.d, self.val = a, b, c, d, val
+
+
+def _bias_terms(opt):
+    if hasattr(opt, "bias_terms"):
+        return opt.bias_terms()
+    b = opt.bias
+    return [b.a, b.b, b.c, b.d, b.val, b.sign]
+
+
+def run_fedgft(fx, make_opt, device):
+    """fedgft/top_aggregator.py:52-86 + syncfl aggregate (make_golden.fedgft_rounds):
+    do(deepcopy(weights), cache, total=...) then update_bias(dataset_sizes, local_biases)."""
+    m = fx.meta
+    res = []
+    for fair in m["fairs"]:
+        opt = make_opt("fedgft", fair=fair, gamma=m["gamma"])
+        w = to_dev(fx.weights("weights0"), device)
+        for r, ends in enumerate(m["rounds"]):
+            tag = f"{fair}/r{r}"
+            bm = m["bias"][tag]
+            cache = SortedCache()
+            for i, (e, c) in enumerate(zip(ends, bm["counts"])):
+                cache[e] = TR(to_dev(fx.weights(f"{tag}/client{i}"), device), c)
+            assert list(cache.iterkeys()) == bm["order"]
+            w = opt.do(deepcopy(w), cache, total=sum(bm["counts"]), num_trainers=len(ends))
+            assert len(cache) == 0
+            local = {e: _LocalBias(*t) for e, t in zip(ends, bm["local"])}
+            opt.update_bias(dataset_sizes={e: bm["sizes"][e] for e in ends}, local_biases=local)
+            res.append((f"{tag}/out", to_cpu(w), fx.weights(f"{tag}/out")))
+            got = {"bias": torch.tensor(_bias_terms(opt) + [opt.get_bias()], dtype=torch.float64)}
+            exp = {"bias": torch.tensor(bm["global"] + [bm["get_bias"]], dtype=torch.float64)}
+            res.append((f"{tag}/bias", got, exp))
+    return res
+
+
 BITWISE_FIXTURES = [
     ("fedavg_small.npz", run_fedavg),
     ("fedavg_dtypes.npz", run_fedavg),
@@ -284,6 +324,7 @@ BITWISE_FIXTURES = [
     ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
+    ("fedgft_rounds.npz", run_fedgft),
 ]
 FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz"]
 

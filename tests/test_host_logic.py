@@ -86,10 +86,11 @@ def test_fedbuff_stale_errors_raise_before_launch():
 def test_provider_semantics():
     from flame_amd.optimizers import optimizer_provider, ObjectFactory, install, DROP_INS
     with pytest.raises(ValueError):
-        optimizer_provider.get("fedgft")
+        optimizer_provider.get("fedsgd")
     f = ObjectFactory()
     install(f)
-    ctor = {"fedprox": {"mu": 0.01}, "feddyn": {"alpha": 0.01}, "scaffold": {"k": 3}}
+    ctor = {"fedprox": {"mu": 0.01}, "feddyn": {"alpha": 0.01}, "scaffold": {"k": 3},
+            "fedgft": {"fair": "SP", "gamma": 0.5}}
     for k in DROP_INS:
         kw = ctor.get(k, {})
         assert isinstance(f.create(k, **kw), DROP_INS[k])
@@ -167,10 +168,10 @@ def test_scaffold_weight_dict_and_none_paths():
 
 
 def test_drop_in_keys_cover_reference_provider():
-    """Every key flame's provider registers (optimizers.py:37-48) except fedgft is a drop-in."""
+    """Every key flame's provider registers (optimizers.py:40-48) is a drop-in."""
     from flame_amd.optimizers import DROP_INS
     assert set(DROP_INS) == {"fedavg", "fedadagrad", "fedadam", "fedyogi", "fedbuff", "fedprox",
-                             "feddyn", "scaffold"}
+                             "feddyn", "scaffold", "fedgft"}
 
 
 def test_plan_per_segment_rates_layout():
@@ -241,3 +242,20 @@ def test_metric_collector_hook_without_launches():
     from flame_amd.optimizers import DROP_INS
     for sort, cls in DROP_INS.items():
         assert getattr(cls.do, "__wrapped__", None) is not None, sort
+
+
+def test_fedgft_bias_matches_reference_fixture(golden):
+    """FedGFT.update_bias / get_bias (fedgft.py:50-58, bias.py:74-106) against the values
+    the reference produced for the same trainer terms (fedgft_rounds.npz); host arithmetic only."""
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.optimizer.fedavg import FedAvg
+    fx = golden("fedgft_rounds.npz")
+    m = fx.meta
+    for fair in m["fairs"]:
+        opt = optimizer_provider.get("fedgft", fair=fair, gamma=m["gamma"])
+        assert isinstance(opt, FedAvg) and opt.get_bias() == 0.0
+        for r, ends in enumerate(m["rounds"]):
+            bm = m["bias"][f"{fair}/r{r}"]
+            local = {e: S._LocalBias(*t) for e, t in zip(ends, bm["local"])}
+            opt.update_bias(dataset_sizes={e: bm["sizes"][e] for e in ends}, local_biases=local)
+            assert S._bias_terms(opt) == bm["global"] and opt.get_bias() == bm["get_bias"]

@@ -18,6 +18,8 @@ def make_oracle(sort, **kw):
         return O.OracleFedDyn(**kw)
     if sort == "scaffold":
         return O.OracleScaffold(**kw)
+    if sort == "fedgft":
+        return O.OracleFedGFT(**kw)
     return O.OracleFedOPT(sort, **kw)
 
 
