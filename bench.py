@@ -28,6 +28,7 @@ import statistics
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -65,6 +66,8 @@ def parse():
                          "replaced at the next fetch, asyncfl/middle_aggregator.py:119-120,244-246)")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "hier_fedbuff", "feddyn", "scaffold"])
+    ap.add_argument("--feddyn-order", default="sorted", choices=["sorted", "shuffled"],
+                    help="feddyn: active_ends order (sorted = the cache order: one merged pass)")
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
     ap.add_argument("--params", type=int, default=None,
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
@@ -313,6 +316,11 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
     keys = [f"{i:05d}" for i in range(n)]
     if args.workload == "feddyn":
         opt = optimizer_provider.get("feddyn", alpha=0.01)
+        # the role's active_ends are the channel's join order (feddyn/top_aggregator.py:137);
+        # "shuffled" makes it differ from the cache's sorted order (two-phase program)
+        ends = list(keys)
+        if args.feddyn_order == "shuffled":
+            ends = [keys[i] for i in np.random.default_rng(5).permutation(n)]
     else:
         opt = optimizer_provider.get("scaffold", k=3)
         opt.save_state("pre", dataset_sizes={k: int(c) for k, c in zip(keys, counts)},
@@ -324,7 +332,7 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
         for i, k in enumerate(keys):
             cache[k] = TR(client_w[i], int(counts[i]))
         if args.workload == "feddyn":
-            opt.save_state("pre", active_ends=keys)   # the role's per-round call (feddyn top_aggregator)
+            opt.save_state("pre", active_ends=ends)   # the role's per-round call (feddyn top_aggregator)
             state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=n)
         else:
             ctl = Cache()
@@ -335,7 +343,8 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
 
     step()  # FedDyn: the first round copies every trainer's history (untimed, as FedOPT's round 1)
     elapsed, events = timed(world, args.steps, args.warmup, step)
-    ks = kernel_stats(events, "flame_agg_reduce")
+    kname = "flame_feddyn_round" if args.workload == "feddyn" else "flame_agg_reduce"
+    ks = kernel_stats(events, kname)
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
@@ -343,9 +352,10 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
             "metric": f"aggregated params/sec (device-resident), {args.workload} server round",
             "value": n * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
             "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32",
-            "config": {"workload": f"{args.workload}: {n} clients x {P} fp32 params, {args.layout} layout"},
+            "config": {"workload": f"{args.workload}: {n} clients x {P} fp32 params, {args.layout} layout"
+                                   + (f", active_ends {args.feddyn_order}" if args.workload == "feddyn" else "")},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": "flame_agg_reduce",
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes,
                          "bytes_per_client_param": k_bytes / (n * P * 4)},

@@ -22,14 +22,16 @@ FLAME_SEG_UNALIGNED = 1
 FLAME_HIER_TOP_ACCUM = 1
 FLAME_HIER_TOP_APPLY = 2
 FLAME_HIER_MID_READONLY = 4
+FLAME_DYN_W, FLAME_DYN_AVG, FLAME_DYN_HIN, FLAME_DYN_HOUT, FLAME_DYN_MEAN = 1, 2, 4, 8, 16
 HIER_SEGMENT_INT64S = 8  # sizeof(flame_hier_segment) / 8
+DYN_SEGMENT_INT64S = 8  # sizeof(flame_dyn_segment) / 8
 SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
 
 # every symbol include/flame_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
     "flame_agg_reduce", "flame_fedopt_reduce_adapt", "flame_fedbuff_scale_add", "flame_hier_fedbuff",
-    "flame_synth_fill",
+    "flame_feddyn_round", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
 )
 
@@ -69,6 +71,9 @@ def lib() -> ctypes.CDLL:
     L.flame_fedbuff_scale_add.argtypes = [ctypes.c_int, vp, i32, i64, i64, vp]
     L.flame_hier_fedbuff.restype = ctypes.c_int
     L.flame_hier_fedbuff.argtypes = [ctypes.c_int, u32, vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, f32, vp]
+    L.flame_feddyn_round.restype = ctypes.c_int
+    L.flame_feddyn_round.argtypes = [ctypes.c_int, vp, i32, i64, vp, vp, i32, i32, ctypes.c_double,
+                                     ctypes.c_double, vp]
     L.flame_synth_fill.restype = ctypes.c_int
     L.flame_synth_fill.argtypes = [ctypes.c_int, vp, i64, u64, u64, i64, f32, vp]
     L.flame_host_register.restype = ctypes.c_int

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdarg>
+#include <type_traits>
 
 #include "../../include/flame_amd.h"
 
@@ -76,6 +77,12 @@ namespace {
 #endif
 #ifndef FLAME_HST
 #define FLAME_HST FLAME_ST_NT  // hierarchy kernel: store policy of the middle weights (encoding of FLAME_ST_NT)
+#endif
+#ifndef FLAME_DYN_CU
+#define FLAME_DYN_CU 4    // FedDyn kernel: program steps whose loads are issued together
+#endif
+#ifndef FLAME_DYN_ST
+#define FLAME_DYN_ST FLAME_ST_NT  // FedDyn kernel: store policy of the updated histories
 #endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
@@ -850,6 +857,149 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
         }
 }
 
+// ---------------------------------------------------------------- FedDyn server round
+// One pass over a FedDyn aggregation round (optimizer/feddyn.py:90-113,125-139), driven
+// by a host-built step program.  Per element, in step order (every op rounded in dtype):
+//   W:    load the arrival w (tiled or contiguous, like flame_agg_reduce's clients)
+//   HIN:  load a history h (contiguous)
+//   AVG:  avg = avg + tmp(w, r_avg)                           (FedAvg, rate 1/len(cache))
+//   HOUT: h' = HIN ? h + w : w, stored to h_out               (add_to_hist)
+//   MEAN: mean = mean + tmp(HOUT ? h' : h, r_mean), mean0 = +0 (0.0 + Σ rate*h)
+// then out = avg, cld = avg + mean.  Steps [0, n_phase1) run before [n_phase1, n_steps);
+// batched loads never cross that boundary, so a phase-2 step may re-read what a phase-1
+// step stored (history order != arrival order).
+template <int DT, int CU, bool VEC>
+__device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const uint64_t* __restrict__ row,
+                                             const uint32_t* __restrict__ sflags, int n_steps, int n_phase1,
+                                             float ra32, float rm32, double ra64, double rm64, int64_t e0,
+                                             int64_t coff, int64_t hoff) {
+    using X = Tr<DT>;
+    using T = typename X::T;
+    using A = typename X::A;
+    constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
+    const int64_t ooff = e0 * static_cast<int64_t>(sizeof(T));   // base / average / cld: contiguous
+    auto load = [&](uint64_t base, int64_t off, T (&x)[kVPT][EPT]) {
+        const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            if constexpr (VEC) {
+                unpack<T, EPT>(ld_nt(p + v * VS), x[v]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) x[v][j] = (e0 + v * VS + j < sg.numel) ? ld1(p + v * VS + j) : T(0);
+            }
+        }
+    };
+    auto store = [&](void* base, int64_t off, const T (&x)[kVPT][EPT], auto pol) {
+        constexpr int POL = decltype(pol)::value;
+        T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            if constexpr (VEC) {
+                st_pol<POL>(p + v * VS, pack<T, EPT>(x[v]));
+            } else {
+#pragma unroll
+                for (int j = 0; j < EPT; ++j)
+                    if (e0 + v * VS + j < sg.numel) st1(p + v * VS + j, x[v][j]);
+            }
+        }
+    };
+    using out_pol = std::integral_constant<int, FLAME_ST_NT>;
+    using hist_pol = std::integral_constant<int, FLAME_DYN_ST>;
+    A avg[kVPT][EPT], mean[kVPT][EPT];
+    {
+        T b[kVPT][EPT];
+        load(reinterpret_cast<uint64_t>(sg.in), ooff, b);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) { avg[v][j] = X::ld(b[v][j]); mean[v][j] = A(0); }
+    }
+#pragma unroll 1
+    for (int phase = 0; phase < 2; ++phase) {
+        const int end = phase ? n_steps : n_phase1;
+#pragma unroll 1
+        for (int k = phase ? n_phase1 : 0; k < end; k += CU) {
+            const int nb = (end - k < CU) ? end - k : CU;
+            T w[CU][kVPT][EPT], h[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                if (u >= nb) break;
+                const uint32_t f = sflags[k + u];
+                const uint64_t* p = row + static_cast<int64_t>(k + u) * 3;
+                if (f & FLAME_DYN_W) load(p[0], coff, w[u]);
+                if (f & FLAME_DYN_HIN) load(p[1], hoff, h[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                if (u >= nb) break;
+                const uint32_t f = sflags[k + u];
+                if (f & FLAME_DYN_AVG) {
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                        for (int j = 0; j < EPT; ++j) avg[v][j] = X::add(avg[v][j], X::tmp(w[u][v][j], ra32, ra64));
+                }
+                if (f & FLAME_DYN_HOUT) {
+                    if (f & FLAME_DYN_HIN) {
+#pragma unroll
+                        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                            for (int j = 0; j < EPT; ++j) h[u][v][j] = X::st(X::add(X::ld(h[u][v][j]), X::ld(w[u][v][j])));
+                    } else {
+#pragma unroll
+                        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                            for (int j = 0; j < EPT; ++j) h[u][v][j] = w[u][v][j];
+                    }
+                    store(reinterpret_cast<void*>(row[static_cast<int64_t>(k + u) * 3 + 2]), hoff, h[u], hist_pol{});
+                }
+                if (f & FLAME_DYN_MEAN) {
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                        for (int j = 0; j < EPT; ++j) mean[v][j] = X::add(mean[v][j], X::tmp(h[u][v][j], rm32, rm64));
+                }
+            }
+        }
+    }
+    T o[kVPT][EPT], c[kVPT][EPT];
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) { o[v][j] = X::st(avg[v][j]); c[v][j] = X::st(X::add(avg[v][j], mean[v][j])); }
+    store(sg.out, ooff, o, out_pol{});
+    store(sg.cld, ooff, c, out_pol{});
+}
+
+template <int DT, int CU>
+__global__ __launch_bounds__(kBlock) void feddyn_kernel(const flame_dyn_segment* __restrict__ segs, int n_segs,
+                                                        const uint64_t* __restrict__ steps,
+                                                        const uint32_t* __restrict__ sflags, int n_steps,
+                                                        int n_phase1, float ra32, float rm32, double ra64,
+                                                        double rm64) {
+    using X = Tr<DT>;
+    constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_dyn_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    const int64_t coff = client_offset<DT>(sg, chunk);
+    // histories: contiguous, or tiled like the arrivals (a FedDyn history store in the slab layout)
+    const int64_t hoff = sg.hist_tile_stride
+        ? (chunk - sg.chunk_begin) * sg.hist_tile_stride + static_cast<int64_t>(threadIdx.x) * EPT * static_cast<int64_t>(sizeof(typename X::T))
+        : e0 * static_cast<int64_t>(sizeof(typename X::T));
+    const uint64_t* row = steps + static_cast<int64_t>(s) * n_steps * 3;
+    const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    if (vec)
+        feddyn_chunk<DT, CU, true>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+    else
+        feddyn_chunk<DT, 1, false>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+}
+
 // ---------------------------------------------------------------- synthetic generator
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1044,6 +1194,43 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     return check_launch("flame_hier_fedbuff");
+}
+
+int flame_feddyn_round(int dtype, const flame_dyn_segment* segs, int32_t n_segs, int64_t n_chunks,
+                       const void* const* steps, const uint32_t* step_flags, int32_t n_steps, int32_t n_phase1,
+                       double rate_avg, double rate_mean, void* stream) {
+    if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
+    if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
+    if (n_steps < 1 || !steps) return set_err(FLAME_EINVAL, "flame_feddyn_round: empty step program");
+    if (n_steps > 0 && !step_flags) return set_err(FLAME_EINVAL, "flame_feddyn_round: step flag array is NULL");
+    if (n_phase1 < 0 || n_phase1 > n_steps)
+        return set_err(FLAME_EINVAL, "flame_feddyn_round: n_phase1 %d outside [0, %d]", n_phase1, n_steps);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    auto sp = reinterpret_cast<const uint64_t*>(steps);
+    // torch rounds the Python-float rates to the tensor's opmath type: fp32, fp64 for f64 tensors
+    const float ra32 = static_cast<float>(rate_avg), rm32 = static_cast<float>(rate_mean);
+    switch (dtype) {
+    case FLAME_F32:
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F32, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+                           n_phase1, ra32, rm32, rate_avg, rate_mean);
+        break;
+    case FLAME_BF16:
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_BF16, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+                           n_phase1, ra32, rm32, rate_avg, rate_mean);
+        break;
+    case FLAME_F16:
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F16, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+                           n_phase1, ra32, rm32, rate_avg, rate_mean);
+        break;
+    case FLAME_F64:
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F64, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+                           n_phase1, ra32, rm32, rate_avg, rate_mean);
+        break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_feddyn_round: dtype %d not supported (f32, bf16, f16, f64)", dtype);
+    }
+    return check_launch("flame_feddyn_round");
 }
 
 int flame_host_register(void* host, uint64_t nbytes) {

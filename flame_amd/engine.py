@@ -544,6 +544,90 @@ def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_
     keep.append(dm)
 
 
+# ------------------------------------------------------------------ FedDyn server round
+def feddyn_program(arrivals: Sequence, dict_order: Sequence, had_history) -> tuple:
+    """Step program of one flame_feddyn_round launch (host only, no GPU).
+
+    ``arrivals``: the ends in cache.iterkeys() order; ``dict_order``: local_param_dict's
+    order after this round's untracked ends were appended (feddyn.py:125-139);
+    ``had_history``: ends whose history existed (not None) before the round.  Returns
+    ``([(flags, end), ...], n_phase1)``.  The FedAvg sum must run in arrival order and the
+    history mean in dict order (feddyn.py:96-112).  When the arrivals appear in dict
+    order in the same relative order, both sums ride one merged step list (each update
+    and history read once); otherwise phase 1 walks the arrivals (average + history
+    update) and phase 2 re-reads the histories in dict order for the mean."""
+    arrived = set(arrivals)
+    pos = {e: i for i, e in enumerate(dict_order)}
+    ap = [pos[e] for e in arrivals]
+    merged = all(a < b for a, b in zip(ap, ap[1:]))
+    hist = [e for e in dict_order if e in arrived or e in had_history]
+
+    def arrival(e):
+        return N.FLAME_DYN_W | N.FLAME_DYN_AVG | N.FLAME_DYN_HOUT | (N.FLAME_DYN_HIN if e in had_history else 0)
+
+    if merged:
+        steps = [((arrival(e) | N.FLAME_DYN_MEAN) if e in arrived else (N.FLAME_DYN_HIN | N.FLAME_DYN_MEAN), e)
+                 for e in hist]
+        return steps, len(steps)
+    steps = [(arrival(e), e) for e in arrivals] + [(N.FLAME_DYN_HIN | N.FLAME_DYN_MEAN, e) for e in hist]
+    return steps, len(arrivals)
+
+
+@dataclass
+class DynSeg:
+    """One tensor of a FedDyn round: base / average / cld pointers and, per program step,
+    (w, h_in, h_out) pointers (0 where the step has none)."""
+    numel: int
+    out: int
+    inp: int
+    cld: int
+    steps: Sequence[Sequence[int]]
+    tile_stride: int = 0
+    hist_tile_stride: int = 0
+
+
+def plan_feddyn(code: int, segs: Sequence[DynSeg], flags: Sequence[int]):
+    """[segments (8 words)] [steps S x K x 3] [flags u32 K] -> (meta, n_chunks, byte offsets)."""
+    S, K = len(segs), len(flags)
+    if S == 0 or K == 0:
+        raise ValueError("feddyn plan needs >= 1 segment and >= 1 step")
+    chunk = chunk_elems(code)
+    head = np.zeros((S, N.DYN_SEGMENT_INT64S), dtype=np.uint64)
+    tab = np.zeros((S, K * 3), dtype=np.uint64)
+    begin = 0
+    for i, s in enumerate(segs):
+        if len(s.steps) != K:
+            raise ValueError("every segment needs one pointer triple per step")
+        tab[i] = np.asarray(s.steps, dtype=np.uint64).reshape(-1)
+        unaligned = bool(np.any(tab[i] % VEC_BYTES)) or any(p % VEC_BYTES for p in (s.out, s.inp, s.cld))
+        head[i] = (s.out, s.inp, s.cld, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride,
+                   s.hist_tile_stride)
+        begin += -(-s.numel // chunk) if s.numel > 0 else 0
+    fl = np.asarray(flags, dtype=np.uint32)
+    if fl.size % 2:
+        fl = np.concatenate([fl, np.zeros(1, np.uint32)])
+    parts = [head.view(np.int64).reshape(-1), tab.view(np.int64).reshape(-1), fl.view(np.int64)]
+    offs = {"segs": 0, "steps": parts[0].size * 8, "flags": (parts[0].size + parts[1].size) * 8}
+    return np.concatenate(parts), max(begin, 1), offs
+
+
+def feddyn_round_(code: int, segs: Sequence[DynSeg], flags: Sequence[int], n_phase1: int, rate_avg: float,
+                  rate_mean: float, device, keep: list) -> None:
+    """One flame_feddyn_round launch (the caller checked dtypes / devices / contiguity)."""
+    meta, n_chunks, offs = plan_feddyn(code, segs, flags)
+    dm = _staging.upload(meta, device)
+    b = dm.data_ptr()
+    P = sum(s.numel for s in segs)
+    reads = sum(bool(f & N.FLAME_DYN_W) + bool(f & N.FLAME_DYN_HIN) for f in flags)
+    writes = sum(bool(f & N.FLAME_DYN_HOUT) for f in flags)
+    nbytes = ITEMSIZE[code] * P * (reads + writes + 3)     # + base read, average and cld written
+    with _timed("flame_feddyn_round", device, nbytes):
+        N.check(N.lib().flame_feddyn_round(code, b + offs["segs"], len(segs), n_chunks, b + offs["steps"],
+                                           b + offs["flags"], len(flags), n_phase1, float(rate_avg),
+                                           float(rate_mean), _stream_ptr(device)))
+    keep.append(dm)
+
+
 def synth_fill_(out: torch.Tensor, seed: int, stream_id: int, start: int, sigma: float) -> None:
     """Fill a device tensor with flame_amd.synth values (bench / test inputs)."""
     from .synth import scale_for_sigma

@@ -19,6 +19,8 @@
  *                               arrivals) + :101-127 (scale_add) + the delta of
  *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246,
  *                               fed to the top's FedBuff (asyncfl/top_aggregator.py:85-109)
+ *   flame_feddyn_round          optimizer/feddyn.py:90-113,125-139 (FedDyn.do: add_to_hist,
+ *                               FedAvg with rate 1/len(cache), mean of the histories, cld_model)
  *   flame_synth_fill            (bench/test plumbing: counter-based synthetic updates)
  *
  * Conventions
@@ -202,6 +204,38 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment *segs
                        const float *mid_rates, const float *mid_goal, const float *top_rates,
                        float top_goal, void *stream);
 
+/* flame_feddyn_round step flags */
+#define FLAME_DYN_W 1u      /* the step has an arrival w (steps[..][0]) */
+#define FLAME_DYN_AVG 2u    /* avg = avg + tmp(w, rate_avg)            (needs W) */
+#define FLAME_DYN_HIN 4u    /* load the history h (steps[..][1]) */
+#define FLAME_DYN_HOUT 8u   /* h' = HIN ? h + w : w, stored to steps[..][2] (needs W) */
+#define FLAME_DYN_MEAN 16u  /* mean = mean + tmp(HOUT ? h' : h, rate_mean) (needs HIN or HOUT) */
+/* One contiguous run of elements of a FedDyn round (one state_dict tensor). */
+typedef struct flame_dyn_segment {
+    void *out;                   /* the average (may == in) */
+    const void *in;              /* base weights: the FedAvg start (deepcopy of cld_model) */
+    void *cld;                   /* cld_model = avg + mean history (out) */
+    int64_t numel;
+    int64_t chunk_begin;         /* prefix sum of ceil(numel / flame_chunk_elems(dtype)) */
+    int64_t flags;               /* FLAME_SEG_UNALIGNED */
+    int64_t client_tile_stride;  /* arrivals: as flame_segment.client_tile_stride */
+    int64_t hist_tile_stride;    /* histories: 0 = contiguous, else bytes between their chunks */
+} flame_dyn_segment;
+/*
+ * One FedDyn server round (optimizer/feddyn.py:90-113 do() + :125-139 add_to_hist) in one
+ * launch, per dtype.  steps: device [n_segs][n_steps][3] pointers (w, h_in,
+ * h_out) per segment; step_flags: device [n_steps].  Per element, steps run in order with
+ * mean starting at +0 (`0.0 + Σ rate*h`); every op rounds in dtype as torch-CPU does, so the
+ * result is bit-identical to the reference's op sequence when the program lists the
+ * arrivals in cache.iterkeys() order (AVG) and the histories in local_param_dict order
+ * (MEAN).  Steps [n_phase1, n_steps) start after every earlier step's store, so they may
+ * re-read a history written by a phase-1 step; within a phase no step may read another
+ * step's output.  rate_avg = 1/len(cache), rate_mean = 1/len(local_param_dict) (rounded to
+ * fp32 for f32/bf16/f16).  dtype FLAME_F32, FLAME_BF16, FLAME_F16 or FLAME_F64.
+ */
+int flame_feddyn_round(int dtype, const flame_dyn_segment *segs, int32_t n_segs, int64_t n_chunks,
+                       const void *const *steps, const uint32_t *step_flags, int32_t n_steps,
+                       int32_t n_phase1, double rate_avg, double rate_mean, void *stream);
 /*
  * Host buffers the kernels read zero-copy over PCIe (ingest; flame_amd/ingest.py).
  *   flame_host_register:   page-lock + map an existing host range (e.g. a received

@@ -56,12 +56,16 @@ def test_argument_validation_without_gpu():
         _native.check(L.flame_synth_fill(0, None, 5, 0, 0, 0, 1.0, None))
 
 
-def test_segment_struct_size():
+@pytest.mark.parametrize("struct,words", [("flame_segment", "SEGMENT_INT64S"),
+                                          ("flame_hier_segment", "HIER_SEGMENT_INT64S"),
+                                          ("flame_dyn_segment", "DYN_SEGMENT_INT64S")])
+def test_segment_struct_size(struct, words):
     src = open(HDR).read()
-    body = re.search(r"typedef struct flame_segment \{(.*?)\} flame_segment;", src, re.S).group(1)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (struct, struct), src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     fields = [ln for ln in body.split(";") if ln.strip()]
     from flame_amd import _native
-    assert len(fields) == _native.SEGMENT_INT64S  # every field is 8 bytes
+    assert len(fields) == getattr(_native, words)  # every field is 8 bytes
 
 
 def test_fedopt_and_host_entry_points_validate_without_gpu():
@@ -82,3 +86,14 @@ def test_agg_reduce_rejects_unknown_flags_without_gpu():
     fake = ctypes.c_void_p(4096)   # never dereferenced: flags are checked on the host first
     assert L.flame_agg_reduce(0, 4, fake, 1, 1, None, 0, None, None, None) == _native.FLAME_EINVAL
     assert b"unknown flags" in L.flame_last_error()
+
+
+def test_feddyn_round_validates_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    fake = ctypes.c_void_p(4096)   # never dereferenced: argument checks run on the host first
+    assert L.flame_feddyn_round(0, None, 0, 1, None, None, 0, 0, 0.5, 0.5, None) == _native.FLAME_EINVAL
+    assert L.flame_feddyn_round(0, fake, 1, 1, fake, None, 2, 0, 0.5, 0.5, None) == _native.FLAME_EINVAL
+    assert b"step flag" in L.flame_last_error()
+    assert L.flame_feddyn_round(0, fake, 1, 1, fake, fake, 2, 3, 0.5, 0.5, None) == _native.FLAME_EINVAL
+    assert b"n_phase1" in L.flame_last_error()

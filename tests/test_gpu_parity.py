@@ -578,18 +578,26 @@ def _dyn_update(g, tmpl, i, scale=1e-2):
             else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
 
 
-@pytest.mark.parametrize("placement", ["hbm", "slab"])
-def test_feddyn_vs_oracle_partial_participation(placement):
+@pytest.mark.parametrize("placement,order", [("hbm", "sorted"), ("slab", "sorted"), ("hbm", "shuffled"),
+                                             ("slab", "shuffled")])
+def test_feddyn_vs_oracle_partial_participation(placement, order):
     """FedDyn drop-in == oracle bitwise over 4 rounds with ends dropping out, returning and
     one untracked end; updates device-resident or tiled UpdateSlab views (history copies
-    are untiled).  ~1M params x 24 ends."""
+    are untiled).  ~1M params x 24 ends.  ``sorted`` active_ends = the cache order (one
+    merged flame_feddyn_round program); ``shuffled`` = the channel's join order differs, so
+    the mean re-reads the updated histories in a second phase."""
     from flame_amd.slab import UpdateSlab
     O = _oracle()
     g = torch.Generator().manual_seed(23)
     tmpl = _dyn_model(g, 1_000_003)
     all_ends = [f"e{i:02d}" for i in range(24)]
+    if order == "shuffled":
+        all_ends = [all_ends[i] for i in np.random.default_rng(7).permutation(24)]
     rounds = [all_ends[:16], all_ends[4:], all_ends[::3] + ["zz"], all_ends[1::2]]
     slab = UpdateSlab(tmpl, capacity=48, device=DEV) if placement == "slab" else None
+    from flame_amd import engine
+    launches = []
+    engine._recorders.append(launches)
     amd, ora = make_amd("feddyn", alpha=0.01), O.OracleFedDyn(alpha=0.01)
     ca_w, co_w = {k: v.to(DEV) for k, v in tmpl.items()}, {k: v.clone() for k, v in tmpl.items()}
     for r, ends in enumerate(rounds):
@@ -608,7 +616,10 @@ def test_feddyn_vs_oracle_partial_participation(placement):
         S.assert_bitwise(f"feddyn/{placement}/r{r}/cld", S.to_cpu(amd.cld_model), ora.cld_model)
         ca_w, co_w = amd.cld_model, ora.cld_model
         del ca, co
-    assert set(amd.local_param_dict) == set(ora.local_param_dict)
+    engine._recorders.remove(launches)
+    # float keys (f32, bf16, f16 groups) run as one flame_feddyn_round per dtype each round
+    assert sum(1 for ev in launches if ev[0] == "flame_feddyn_round") == 3 * len(rounds)
+    assert list(amd.local_param_dict) == list(ora.local_param_dict)
     for e, h in ora.local_param_dict.items():
         if h is not None:
             S.assert_bitwise(f"feddyn/{placement}/hist/{e}", S.to_cpu(amd.local_param_dict[e]), h)

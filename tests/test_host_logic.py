@@ -259,3 +259,22 @@ def test_fedgft_bias_matches_reference_fixture(golden):
             local = {e: S._LocalBias(*t) for e, t in zip(ends, bm["local"])}
             opt.update_bias(dataset_sizes={e: bm["sizes"][e] for e in ends}, local_biases=local)
             assert S._bias_terms(opt) == bm["global"] and opt.get_bias() == bm["get_bias"]
+
+
+def test_feddyn_program_merged_and_two_phase():
+    """engine.feddyn_program: FedAvg in arrival order, mean in dict order (feddyn.py:96-112)."""
+    W, AVG, HIN, HOUT, MEAN = N.FLAME_DYN_W, N.FLAME_DYN_AVG, N.FLAME_DYN_HIN, N.FLAME_DYN_HOUT, N.FLAME_DYN_MEAN
+    arr = W | AVG | HOUT
+    # arrivals in dict order: one merged list; a None end that does not arrive contributes nothing
+    steps, n1 = engine.feddyn_program(["a", "c", "z"], ["a", "b", "c", "d", "z"], {"a", "b"})
+    assert steps == [(arr | HIN | MEAN, "a"), (HIN | MEAN, "b"), (arr | MEAN, "c"), (arr | MEAN, "z")]
+    assert n1 == len(steps)
+    # arrival order differs from dict order: phase 1 = arrivals, phase 2 = the mean in dict order
+    steps, n1 = engine.feddyn_program(["a", "c"], ["c", "b", "a"], {"a", "b", "c"})
+    assert n1 == 2
+    assert steps == [(arr | HIN, "a"), (arr | HIN, "c"), (HIN | MEAN, "c"), (HIN | MEAN, "b"), (HIN | MEAN, "a")]
+    meta, n_chunks, offs = engine.plan_feddyn(
+        N.FLAME_F32, [engine.DynSeg(5000, out=4096, inp=4096, cld=8192, steps=[(16, 32, 32)] * 5)], [f for f, _ in steps])
+    T = engine.chunk_elems(N.FLAME_F32)
+    assert n_chunks == -(-5000 // T) and offs["steps"] == 64 and offs["flags"] == 64 + 5 * 3 * 8
+    assert list(meta[offs["flags"] // 8:].view(np.uint32)[:5]) == [f for f, _ in steps]

@@ -50,6 +50,12 @@ VARIANTS = {
     "wgc2d": {"FLAME_WGC": 2, "FLAME_DEFER_ST": 1},
     "wgc4d": {"FLAME_WGC": 4, "FLAME_DEFER_ST": 1},
     "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
+    # FedDyn round kernel (bench.py --workload feddyn with FLAME_AMD_LIB=build/variants/lib_<name>.so)
+    "dyncu2": {"FLAME_DYN_CU": 2},
+    "dyncu8": {"FLAME_DYN_CU": 8},
+    "dynst0": {"FLAME_DYN_ST": 0},
+    "dynst1": {"FLAME_DYN_ST": 1},
+    "dynst2": {"FLAME_DYN_ST": 2},
 }
 
 
