@@ -56,9 +56,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--hier-mode", default="fused", choices=["fused", "group", "serial"],
+    ap.add_argument("--hier-mode", default="fused", choices=["fused", "group", "serial", "sync", "sync_serial"],
                     help="hier_fedbuff: the node's middles AND the top in one pass (fused, "
-                         "flame_hier_fedbuff), co-located middles in one launch (group) or one by one")
+                         "flame_hier_fedbuff), co-located middles in one launch (group) or one by one; "
+                         "sync / sync_serial: the synchronous FedAvg hierarchy (syncfl middles -> top) in one "
+                         "FLAME_HIER_SYNC launch or as the roles' separate FedAvg.do + delta calls")
     ap.add_argument("--hier-middles", default="own", choices=["own", "fetched"],
                     help="hier_fedbuff fused: own = every middle keeps its own weights, updated in place; "
                          "fetched = the middles hold the top model they fetched this round (one shared "
@@ -582,13 +584,48 @@ def bench_hier(args, world, rank, dev):
                         update_middle_weights=not fetched)
         gather()
 
-    step = {"fused": step_fused, "group": step_group, "serial": step_serial}[args.hier_mode]
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    counts = [int(c) for c in synth.counts(args.seed + 4, M * C)]
+
+    def sync_caches():
+        specs = []
+        for m in range(M):
+            cache = Cache()
+            for t in range(C):
+                i = m * C + t
+                cache[f"{i:05d}"] = TR(client_w[i], counts[i])
+            specs.append(({"model": mids[m]}, cache, sum(counts[m * C:(m + 1) * C])))
+        return specs
+
+    def step_sync():
+        # synchronous hierarchy (syncfl middles -> syncfl top): every middle's FedAvg,
+        # its delta and the top's FedAvg over the deltas in ONE launch (FLAME_HIER_SYNC)
+        sync_hierarchy_round(sync_caches(), {"model": gw})
+        gather()
+
+    fedavg_opt = optimizer_provider.get("fedavg")
+
+    def step_sync_serial():
+        # the same round as the roles issue it: FedAvg.do per middle, delta, FedAvg.do at the top
+        top_cache = Cache()
+        totals = 0
+        for m, (w, cache, total) in enumerate(sync_caches()):
+            new = fedavg_opt.do({"model": w["model"].clone()}, cache, total=total)
+            top_cache[f"mid{m:03d}"] = TR({"model": new["model"] - w["model"]}, total)
+            mids[m].copy_(new["model"])
+            totals += total
+        fedavg_opt.do({"model": gw}, top_cache, total=totals)
+        gather()
+
+    step = {"fused": step_fused, "group": step_group, "serial": step_serial, "sync": step_sync,
+            "sync_serial": step_sync_serial}[args.hier_mode]
     elapsed, events = timed(world, args.steps, args.warmup, step)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_clients > 0:
+    if rank == 0 and world == 1 and args.cpu_clients > 0 and not args.hier_mode.startswith("sync"):
         cpu = cpu_baseline_hier([store.read(i, "model").cpu() for i in range(C)], P, stale[:C], rnd,
                                 args.cpu_rounds)
-    names = ("flame_hier_fedbuff",) if args.hier_mode == "fused" else ("flame_agg_reduce", "flame_fedbuff_scale_add")
+    names = {"fused": ("flame_hier_fedbuff",), "sync": ("flame_hier_fedbuff",),
+             "sync_serial": ("flame_agg_reduce",)}.get(args.hier_mode, ("flame_agg_reduce", "flame_fedbuff_scale_add"))
     kst = {nm: kernel_stats(events, nm) for nm in names}
     red = kst[names[0]]
     traffic = None
@@ -602,11 +639,14 @@ def bench_hier(args, world, rank, dev):
             pass
     if rank == 0:
         per_step_kernel = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
+        sync = args.hier_mode.startswith("sync")
         print(json.dumps({
-            "metric": "aggregated params/sec (device-resident), hierarchical FedBuff shard",
+            "metric": ("aggregated params/sec (device-resident), hierarchical "
+                       + ("FedAvg (synchronous) shard" if sync else "FedBuff shard")),
             "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
-            "dtype": "bf16", "config": {"workload": f"hier_fedbuff: {M} middles x {C} clients x {P} bf16 per GPU",
+            "dtype": "bf16", "config": {"workload": f"{'hier_fedavg' if sync else 'hier_fedbuff'}: {M} middles x {C} "
+                                                    f"clients x {P} bf16 per GPU",
                                         "middles": args.hier_mode, "middle_weights": args.hier_middles},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,

@@ -22,6 +22,7 @@ FLAME_SEG_UNALIGNED = 1
 FLAME_HIER_TOP_ACCUM = 1
 FLAME_HIER_TOP_APPLY = 2
 FLAME_HIER_MID_READONLY = 4
+FLAME_HIER_SYNC = 8
 FLAME_DYN_W, FLAME_DYN_AVG, FLAME_DYN_HIN, FLAME_DYN_HOUT, FLAME_DYN_MEAN = 1, 2, 4, 8, 16
 HIER_SEGMENT_INT64S = 8  # sizeof(flame_hier_segment) / 8
 DYN_SEGMENT_INT64S = 8  # sizeof(flame_dyn_segment) / 8

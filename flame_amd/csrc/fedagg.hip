@@ -714,7 +714,12 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
 #else
 #define FLAME_HIER_ATTR __launch_bounds__(kBlock)
 #endif
-template <int DT, int CU>
+// SYNC (FLAME_HIER_SYNC): the synchronous hierarchy instead (syncfl/middle_aggregator.py:163-229,
+// syncfl/top_aggregator.py:122-176): each middle's FedAvg starts from its weights,
+//   a = w_m + tmp(c_{m,0}, r_{m,0}) + ...;  w_m' = a;  d_m = w_m' - w_m
+// and the top's FedAvg adds tmp(d_m, top_rates[m]) to the top weights (top_agg_in).
+template <int DT> __device__ __forceinline__ float rnd(float x);
+template <int DT, int CU, bool SYNC>
 __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
                                                               int n_mids, int n_clients,
                                                               const uint64_t* __restrict__ mid_w,
@@ -762,7 +767,16 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
             for (int v = 0; v < kVPT; ++v) wv[v] = ld_v(wp + v * VS);
 #endif
             A acc[kVPT][EPT];
-            reduce_clients<DT, CU, true>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+            T wo[SYNC ? kVPT : 1][EPT];
+            if constexpr (SYNC) {     // FedAvg starts from the middle's weights (deepcopy(self.weights))
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v) {
+                    unpack<T, EPT>(ld_v(wp + v * VS), wo[v]);
+#pragma unroll
+                    for (int j = 0; j < EPT; ++j) acc[v][j] = X::ld(wo[v][j]);
+                }
+            }
+            reduce_clients<DT, CU, true>(acc, !SYNC, crow + static_cast<int64_t>(m) * n_clients, n_clients,
                                          mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
                                          coff);
             T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
@@ -770,6 +784,17 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
 #pragma unroll
             for (int v = 0; v < kVPT; ++v) {
                 T w[EPT], d[EPT];
+                if constexpr (SYNC) {
+#pragma unroll
+                    for (int j = 0; j < EPT; ++j) {
+                        w[j] = X::st(acc[v][j]);
+                        d[j] = X::st(rnd<DT>(__fsub_rn(X::ld(w[j]), X::ld(wo[v][j]))));
+                        top[v][j] = X::add(top[v][j], X::tmp(d[j], rt, 0.0));
+                    }
+                    if (!(flags & FLAME_HIER_MID_READONLY)) st_pol<FLAME_HST>(wp + v * VS, pack<T, EPT>(w));
+                    if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
+                    continue;
+                }
 #if FLAME_HPF
                 unpack<T, EPT>(wv[v], w);
 #elif FLAME_HDIAG == 2
@@ -820,9 +845,16 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
 #pragma unroll 1
     for (int m = 0; m < n_mids; ++m) {
         A acc[kVPT][EPT];
-        reduce_clients<DT, 1, false>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
-                                     mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel, coff);
         T* wp = reinterpret_cast<T*>(wrow[m]) + e0;
+        if constexpr (SYNC) {
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j)
+                    acc[v][j] = (e0 + v * VS + j < sg.numel) ? X::ld(ld1(wp + v * VS + j)) : A(0);
+        }
+        reduce_clients<DT, 1, false>(acc, !SYNC, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+                                     mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel, coff);
         T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
         const float g = mid_goal[m], rt = top_rates[m];
 #pragma unroll
@@ -832,7 +864,13 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                 const int64_t o = v * VS + j;
                 if (e0 + o >= sg.numel) continue;
                 T w = ld1(wp + o), d;
-                S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
+                if constexpr (SYNC) {
+                    const T wn = X::st(acc[v][j]);
+                    d = X::st(rnd<DT>(__fsub_rn(X::ld(wn), X::ld(w))));
+                    w = wn;
+                } else {
+                    S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
+                }
                 if (!(flags & FLAME_HIER_MID_READONLY)) st1(wp + o, w);
                 if (dp) st1(dp + o, d);
                 const A t = X::tmp(d, rt, 0.0);
@@ -1169,27 +1207,30 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     if (n_mids < 1 || n_clients < 1) return set_err(FLAME_EINVAL, "flame_hier_fedbuff: need >= 1 middle and >= 1 arrival per middle");
     if (!mid_w || !clients || !mid_rates || !mid_goal || !top_rates)
         return set_err(FLAME_EINVAL, "flame_hier_fedbuff: NULL table");
-    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY | FLAME_HIER_MID_READONLY))
+    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY | FLAME_HIER_MID_READONLY | FLAME_HIER_SYNC))
         return set_err(FLAME_EINVAL, "flame_hier_fedbuff: unknown flags 0x%x", flags);
+    if ((flags & FLAME_HIER_SYNC) && ((flags & FLAME_HIER_TOP_APPLY) || !(flags & FLAME_HIER_TOP_ACCUM)))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff: FLAME_HIER_SYNC needs FLAME_HIER_TOP_ACCUM (the top's "
+                                     "FedAvg starts from its weights) and no FLAME_HIER_TOP_APPLY");
     if ((flags & FLAME_HIER_TOP_APPLY) && top_goal == 0.f) return set_err(FLAME_EINVAL, "top agg_goal must be nonzero");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     auto w = reinterpret_cast<const uint64_t*>(mid_w);
     auto d = reinterpret_cast<const uint64_t*>(mid_delta);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-    switch (dtype) {
-    case FLAME_F32:
-        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, n_mids,
+#define FLAME_HIER_LAUNCH(DT, CUV)                                                                             \
+    if (sync)                                                                                                  \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true>), grid, block, 0, st, segs, n_segs, n_mids,     \
+                           n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);              \
+    else                                                                                                       \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false>), grid, block, 0, st, segs, n_segs, n_mids,    \
                            n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
-        break;
-    case FLAME_BF16:
-        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_BF16, kHierUnroll16>), grid, block, 0, st, segs, n_segs,
-                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
-        break;
-    case FLAME_F16:
-        hipLaunchKernelGGL((hier_fedbuff_kernel<FLAME_F16, kHierUnroll16>), grid, block, 0, st, segs, n_segs,
-                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
-        break;
+    const bool sync = (flags & FLAME_HIER_SYNC) != 0;
+    switch (dtype) {
+    case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll) break;
+    case FLAME_BF16: FLAME_HIER_LAUNCH(FLAME_BF16, kHierUnroll16) break;
+    case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16) break;
+#undef FLAME_HIER_LAUNCH
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
     }

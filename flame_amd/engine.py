@@ -519,14 +519,15 @@ def plan_hier(code: int, segs: Sequence[HierSeg], mid_rates, mid_goals, top_rate
 
 
 def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_rates, *, top_accum: bool,
-                  top_goal: Optional[int], device, keep: list, mid_readonly: bool = False) -> None:
-    """One flame_hier_fedbuff launch (the caller checked dtypes / devices / contiguity)."""
+                  top_goal: Optional[int], device, keep: list, mid_readonly: bool = False, sync: bool = False) -> None:
+    """One flame_hier_fedbuff launch (the caller checked dtypes / devices / contiguity).
+    ``sync``: the synchronous FedAvg hierarchy (FLAME_HIER_SYNC; needs ``top_accum``)."""
     L = N.lib()
     p = plan_hier(code, segs, mid_rates, mid_goals, top_rates)
     dm = _staging.upload(p.meta, device)
     b = dm.data_ptr()
     flags = ((N.FLAME_HIER_TOP_ACCUM if top_accum else 0) | (N.FLAME_HIER_TOP_APPLY if top_goal is not None else 0)
-             | (N.FLAME_HIER_MID_READONLY if mid_readonly else 0))
+             | (N.FLAME_HIER_MID_READONLY if mid_readonly else 0) | (N.FLAME_HIER_SYNC if sync else 0))
     with_delta = any(s.mid_delta is not None for s in segs)
     P = sum(s.numel for s in segs)
     isz = ITEMSIZE[code]

@@ -14,7 +14,9 @@
  *   flame_fedbuff_scale_add     optimizer/fedbuff.py:101-127 (scale_add_agg_weights), fused with
  *                               common/util.py:152-159 (delta_weights_pytorch) as used by
  *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246
- *   flame_hier_fedbuff          a node's co-located two-level FedBuff hierarchy in one pass:
+ *   flame_hier_fedbuff          a node's co-located two-level FedBuff hierarchy in one pass
+ *                               (FLAME_HIER_SYNC: the synchronous FedAvg hierarchy,
+ *                               syncfl/middle_aggregator.py:163-229 -> syncfl/top_aggregator.py:122-176):
  *                               per middle optimizer/fedbuff.py:89-97,136-157 (None-start
  *                               arrivals) + :101-127 (scale_add) + the delta of
  *                               mode/horizontal/asyncfl/middle_aggregator.py:221-226,246,
@@ -165,6 +167,12 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment *segs, int32_t n_segs
                                       base of their deltas (the async middle role replaces them with
                                       the top's model at its next fetch,
                                       asyncfl/middle_aggregator.py:119-120); mid_w may then alias */
+#define FLAME_HIER_SYNC 8u   /* the synchronous hierarchy (syncfl/middle_aggregator.py:163-229 feeding
+                                syncfl/top_aggregator.py:122-176): per middle FedAvg from its weights,
+                                a = w_m + tmp(c_{m,0}, r_{m,0}) + ..., w_m' = a, d_m = w_m' - w_m; the top
+                                is a FedAvg from its weights: top = top_agg_in + tmp(d_m, top_rates[m]) in
+                                order.  Needs FLAME_HIER_TOP_ACCUM, excludes FLAME_HIER_TOP_APPLY; mid_goal
+                                is not read (any values) */
 
 /* One contiguous run of elements of the hierarchy (one state_dict tensor). */
 typedef struct flame_hier_segment {

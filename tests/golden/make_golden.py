@@ -457,7 +457,56 @@ def fedgft_rounds():
     print("wrote fedgft_rounds.npz")
 
 
-CASES = {"feddyn_rounds": feddyn_rounds, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def hier_fedavg_small():
+    """Synchronous hierarchy: 3 middles x 4 trainers, each middle runs FedAvg from its own
+    weights (syncfl/middle_aggregator.py:163-204), uploads delta_weights_pytorch(new, prev)
+    with its sample total (:206-229, common/util.py:152-159); the top runs FedAvg over the
+    deltas (syncfl/top_aggregator.py:122-176).  f32 / bf16 / f16 / int64 keys, 2 rounds."""
+    from flame.common.util import delta_weights_pytorch
+    gen = torch.Generator().manual_seed(62)
+    shapes = {"w": ((33, 17), torch.float32), "bf": ((300,), torch.bfloat16), "h": ((129,), torch.float16),
+              "nbt": ((), torch.int64)}
+    fw = FixtureWriter()
+    top_w = small_weights(gen, shapes, 1.0)
+    fw.put_weights("top_w0", top_w)
+    mids = [deepcopy(top_w) for _ in range(3)]
+    meta = {"rounds": []}
+    for r in range(2):
+        rmeta = {"mids": []}
+        top_cache = Cache()
+        totals = []
+        for m in range(3):
+            clients = [small_weights(gen, shapes, 1e-2) for _ in range(4)]
+            for i, c in enumerate(clients):
+                c["nbt"] = torch.tensor(3 * r + i + m, dtype=torch.int64)
+            counts = [int(x) for x in torch.randint(1, 1001, (4,), generator=gen)]
+            ids = [f"r{r}m{m}t{i}" for i in range(4)]
+            cache = Cache()
+            for e, w, c in zip(ids, clients, counts):
+                cache[e] = TrainResult(w, c)
+            order = list(cache.iterkeys())
+            opt = optimizer_provider.get("fedavg")
+            prev = mids[m]
+            new = opt.do(deepcopy(prev), cache, total=sum(counts))
+            delta = delta_weights_pytorch(new, prev)
+            mids[m] = new
+            for i, c in enumerate(clients):
+                fw.put_weights(f"r{r}/m{m}/client{i}", c)
+            fw.put_weights(f"r{r}/m{m}/new", new)
+            fw.put_weights(f"r{r}/m{m}/delta", delta)
+            top_cache[f"mid{m}"] = TrainResult(delta, sum(counts))
+            totals.append(sum(counts))
+            rmeta["mids"].append({"ids": ids, "counts": counts, "order": order})
+        rmeta["top_order"] = list(top_cache.iterkeys())
+        top_w = optimizer_provider.get("fedavg").do(deepcopy(top_w), top_cache, total=sum(totals))
+        fw.put_weights(f"r{r}/top", top_w)
+        meta["rounds"].append(rmeta)
+    fw.meta.update({"kind": "hier_fedavg", **meta})
+    fw.save(os.path.join(HERE, "hier_fedavg_small.npz"))
+    print("wrote hier_fedavg_small.npz")
+
+
+CASES = {"feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():

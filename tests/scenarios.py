@@ -225,6 +225,63 @@ def run_hier(fx, make_opt, device, delta_fn):
     return res
 
 
+def run_hier_fedavg(fx, make_opt, device):
+    """Synchronous hierarchy as separate calls (make_golden.hier_fedavg_small): per middle
+    FedAvg.do(deepcopy(w), cache, total) + delta; top FedAvg.do over the deltas."""
+    m = fx.meta
+    top = to_dev(fx.weights("top_w0"), device)
+    mids = [to_dev(fx.weights("top_w0"), device) for _ in range(3)]
+    res = []
+    for r, rm in enumerate(m["rounds"]):
+        top_cache = SortedCache()
+        totals = []
+        for j, mm in enumerate(rm["mids"]):
+            cache = SortedCache()
+            for i, (e, c) in enumerate(zip(mm["ids"], mm["counts"])):
+                cache[e] = TR(to_dev(fx.weights(f"r{r}/m{j}/client{i}"), device), c)
+            assert list(cache.iterkeys()) == mm["order"]
+            new = make_opt("fedavg").do(deepcopy(mids[j]), cache, total=sum(mm["counts"]))
+            delta = {k: new[k] - mids[j][k] for k in new}
+            mids[j] = new
+            res.append((f"r{r}/m{j}/new", to_cpu(new), fx.weights(f"r{r}/m{j}/new")))
+            res.append((f"r{r}/m{j}/delta", to_cpu(delta), fx.weights(f"r{r}/m{j}/delta")))
+            top_cache[f"mid{j}"] = TR(delta, sum(mm["counts"]))
+            totals.append(sum(mm["counts"]))
+        assert list(top_cache.iterkeys()) == rm["top_order"]
+        top = make_opt("fedavg").do(deepcopy(top), top_cache, total=sum(totals))
+        res.append((f"r{r}/top", to_cpu(top), fx.weights(f"r{r}/top")))
+    return res
+
+
+def run_hier_fedavg_fused(fx, device, with_delta=True, slab=False):
+    """The same rounds through flame_amd.optimizer.sync_hierarchy.sync_hierarchy_round (GPU)."""
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    m = fx.meta
+    top = to_dev(fx.weights("top_w0"), device)
+    mids = [to_dev(fx.weights("top_w0"), device) for _ in range(3)]
+    store = None
+    if slab:
+        from flame_amd.slab import UpdateSlab
+        store = UpdateSlab(fx.weights("top_w0"), capacity=16, device=device)
+    res = []
+    for r, rm in enumerate(m["rounds"]):
+        specs = []
+        for j, mm in enumerate(rm["mids"]):
+            cache = SortedCache()
+            for i, (e, c) in enumerate(zip(mm["ids"], mm["counts"])):
+                w = to_dev(fx.weights(f"r{r}/m{j}/client{i}"), device)
+                cache[e] = TR(store.put(w) if store is not None else w, c)
+            specs.append((mids[j], cache, sum(mm["counts"])))
+        top, deltas = sync_hierarchy_round(specs, top, with_delta=with_delta)
+        for j in range(len(rm["mids"])):
+            res.append((f"r{r}/m{j}/new", to_cpu(mids[j]), fx.weights(f"r{r}/m{j}/new")))
+            if with_delta:
+                res.append((f"r{r}/m{j}/delta", to_cpu(deltas[j]), fx.weights(f"r{r}/m{j}/delta")))
+        res.append((f"r{r}/top", to_cpu(top), fx.weights(f"r{r}/top")))
+        del specs
+    return res
+
+
 class _PRE:
     """Stands in for flame.common.constants.TrainState.PRE (value "pre")."""
     value = "pre"
@@ -325,6 +382,7 @@ BITWISE_FIXTURES = [
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
+    ("hier_fedavg_small.npz", run_hier_fedavg),
 ]
 FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz"]
 

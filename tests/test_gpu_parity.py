@@ -1024,3 +1024,59 @@ def test_nonfinite_updates_match_oracle(dtype):
     ow = {"w": base.clone()}
     ofb.scale_add_agg_weights(ow, oagg, len(cl))
     S.assert_same_nonfinite(f"fedbuff {dtype}", w["w"], ow["w"])
+
+
+@pytest.mark.parametrize("with_delta,slab", [(True, False), (False, False), (True, True)])
+def test_sync_hierarchy_golden(golden, with_delta, slab):
+    """sync_hierarchy_round (one FLAME_HIER_SYNC launch per float dtype; the int64 key
+    composes the separate calls) == the reference's syncfl middles + top, bitwise
+    (hier_fedavg_small.npz: 3 middles x 4 trainers, f32/bf16/f16/int64, 2 rounds)."""
+    from flame_amd import engine
+    launches = []
+    engine._recorders.append(launches)
+    try:
+        res = S.run_hier_fedavg_fused(golden("hier_fedavg_small.npz"), DEV, with_delta=with_delta, slab=slab)
+    finally:
+        engine._recorders.remove(launches)
+    for label, got, exp in res:
+        S.assert_bitwise(f"hier_fedavg:{label}", got, exp)
+    assert sum(1 for ev in launches if ev[0] == "flame_hier_fedbuff") == 3 * 2   # f32, bf16, f16 x 2 rounds
+
+
+def test_sync_hierarchy_vs_oracle_readonly_middles():
+    """8 middles x 16 trainers over ~1M params (tails, every float dtype + int64): top and
+    deltas == the oracle's FedAvg / delta / FedAvg composition; with
+    update_middle_weights=False one shared middle tensor is read, never written."""
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    O = _oracle()
+    g = torch.Generator().manual_seed(41)
+    tmpl = _dyn_model(g, 1_000_003)
+    M, C = 8, 16
+    mid_cpu = {k: v.clone() for k, v in tmpl.items()}
+    top_cpu = {k: (v * 0.5 if v.is_floating_point() else v) for k, v in tmpl.items()}
+    ups = [[_dyn_update(g, tmpl, 5 * j + i) for i in range(C)] for j in range(M)]
+    counts = [[int(x) for x in torch.randint(1, 1000, (C,), generator=g)] for _ in range(M)]
+    shared = {k: v.to(DEV) for k, v in mid_cpu.items()}
+    specs = []
+    for j in range(M):
+        cache = S.SortedCache()
+        for i in range(C):
+            cache[f"m{j}t{i:02d}"] = S.TR({k: v.to(DEV) for k, v in ups[j][i].items()}, counts[j][i])
+        specs.append((shared, cache, sum(counts[j])))
+    top = {k: v.to(DEV) for k, v in top_cpu.items()}
+    top, deltas = sync_hierarchy_round(specs, top, with_delta=True, update_middle_weights=False)
+    S.assert_bitwise("sync/readonly/middle", S.to_cpu(shared), mid_cpu)
+    # oracle: the separate calls
+    exp_deltas, top_cache = [], S.SortedCache()
+    for j in range(M):
+        cache = S.SortedCache()
+        for i in range(C):
+            cache[f"m{j}t{i:02d}"] = S.TR({k: v.clone() for k, v in ups[j][i].items()}, counts[j][i])
+        new = O.OracleFedAvg().do({k: v.clone() for k, v in mid_cpu.items()}, cache, total=sum(counts[j]))
+        exp_deltas.append({k: new[k] - mid_cpu[k] for k in new})
+        top_cache[f"mid{j}"] = S.TR(exp_deltas[-1], sum(counts[j]))
+    exp_top = O.OracleFedAvg().do({k: v.clone() for k, v in top_cpu.items()}, top_cache,
+                                  total=sum(sum(c) for c in counts))
+    for j in range(M):
+        S.assert_bitwise(f"sync/readonly/delta{j}", S.to_cpu(deltas[j]), exp_deltas[j])
+    S.assert_bitwise("sync/readonly/top", S.to_cpu(top), exp_top)
