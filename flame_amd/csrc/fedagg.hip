@@ -84,6 +84,10 @@ namespace {
 #ifndef FLAME_DYN_ST
 #define FLAME_DYN_ST FLAME_ST_NT  // FedDyn kernel: store policy of the updated histories
 #endif
+#ifndef FLAME_OCC_LDS
+#define FLAME_OCC_LDS 0   // sweep variants: dynamic LDS bytes per reduction / hierarchy workgroup (caps
+                          // resident workgroups per CU at 160 KiB / FLAME_OCC_LDS; the kernels use no LDS)
+#endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
@@ -1117,22 +1121,22 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     auto cl = reinterpret_cast<const uint64_t*>(clients);
     switch (dtype) {
     case FLAME_F32:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_BF16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_F16:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_F64:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_I64:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     case FLAME_I32:
-        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
         break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_agg_reduce: unsupported dtype %d", dtype);
@@ -1220,10 +1224,10 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     auto cl = reinterpret_cast<const uint64_t*>(clients);
 #define FLAME_HIER_LAUNCH(DT, CUV)                                                                             \
     if (sync)                                                                                                  \
-        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true>), grid, block, 0, st, segs, n_segs, n_mids,     \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, n_mids,     \
                            n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);              \
     else                                                                                                       \
-        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false>), grid, block, 0, st, segs, n_segs, n_mids,    \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, n_mids,    \
                            n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
     switch (dtype) {

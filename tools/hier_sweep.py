@@ -71,7 +71,7 @@ def main():
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
-        build_variants([n for n in names if n != "probe"])
+        build_variants(sorted({n.split(":")[0] for n in names if n != "probe"}))
         return
 
     import torch
@@ -99,11 +99,25 @@ def main():
     dm = torch.from_numpy(p.meta).to(dev)
     b = dm.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    libs = {nm: load(nm) for nm in names if nm != "probe"}
+    libs = {nm: load(nm.split(":")[0]) for nm in names if nm != "probe"}
+    # "<variant>:sync" = the same build in FLAME_HIER_SYNC mode (FedAvg middles + top FedAvg, same bytes)
+    sseg = engine.HierSeg(P, mid_w=seg.mid_w, clients=seg.clients, top_in=gw.data_ptr(), top_out=top.data_ptr(),
+                          tile_stride=seg.tile_stride)
+    ps = engine.plan_hier(code, [sseg], mid_rates, [C] * M, [1 / (1 + m % 2) ** 0.5 for m in range(M)])
+    dms = torch.from_numpy(ps.meta).to(dev)
+    bs = dms.data_ptr()
 
     def launch(nm):
         if nm == "probe":
             assert PL.probe_read(slab.data_ptr(), pbytes, pout.data_ptr(), 16384, 2, stream) == 0
+            return
+        if nm.endswith(":sync"):
+            rc = libs[nm].flame_hier_fedbuff(code, N.FLAME_HIER_TOP_ACCUM | N.FLAME_HIER_SYNC, bs + ps.offs["segs"],
+                                             ps.n_segs, ps.n_chunks, M, C, bs + ps.offs["mid_w"], None,
+                                             bs + ps.offs["clients"], bs + ps.offs["mid_rates"],
+                                             bs + ps.offs["mid_goal"], bs + ps.offs["top_rates"], 0.0, stream)
+            if rc:
+                raise RuntimeError(libs[nm].flame_last_error())
             return
         rc = libs[nm].flame_hier_fedbuff(code, N.FLAME_HIER_TOP_APPLY, b + p.offs["segs"], p.n_segs, p.n_chunks,
                                          M, C, b + p.offs["mid_w"], None, b + p.offs["clients"],
@@ -127,7 +141,7 @@ def main():
         launch(nm)
         torch.cuda.synchronize()
         got = (mids.clone(), gw.clone(), top.clone())
-        if nm.startswith("hdiag"):
+        if nm.startswith("hdiag") or nm.endswith(":sync"):
             continue
         if ref is None:
             ref = got
@@ -152,7 +166,7 @@ def main():
         med, mn = statistics.median(times[nm]), min(times[nm])
         nb = pbytes if nm == "probe" else nbytes
         print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nb / med / 1e6:8.1f} GB/s  "
-              f"{VARIANTS.get(nm, {})}", flush=True)
+              f"{VARIANTS.get(nm.split(':')[0], {})}", flush=True)
 
 
 if __name__ == "__main__":

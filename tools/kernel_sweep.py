@@ -56,6 +56,11 @@ VARIANTS = {
     "dynst0": {"FLAME_DYN_ST": 0},
     "dynst1": {"FLAME_DYN_ST": 1},
     "dynst2": {"FLAME_DYN_ST": 2},
+    # resident workgroups per CU capped by dynamic LDS (reduction + hierarchy kernels)
+    "occ3": {"FLAME_OCC_LDS": 53248},
+    "occ4": {"FLAME_OCC_LDS": 40960},
+    "occ5": {"FLAME_OCC_LDS": 32768},
+    "occ6": {"FLAME_OCC_LDS": 27136},
 }
 
 
