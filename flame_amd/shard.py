@@ -191,3 +191,177 @@ class ShardedSliceFedAvg:
         for w in works:
             w.wait()
         return base_weights
+
+
+class _SlicedResult:
+    """TrainResult-shaped record carrying this rank's slice of a client's weights."""
+
+    __slots__ = ("weights", "count", "version")
+
+    def __init__(self, weights, count, version):
+        self.weights, self.count, self.version = weights, count, version
+
+
+class _SliceCache:
+    """A view of the caller's cache that hands out this rank's slice of every entry, in
+    the caller's ``iterkeys()`` order; popping it pops the caller's entry."""
+
+    def __init__(self, cache, slicer):
+        self._cache, self._slicer = cache, slicer
+
+    def __len__(self):
+        return len(self._cache)
+
+    def iterkeys(self):
+        return self._cache.iterkeys()
+
+    def pop(self, key, default=None):
+        tres = self._cache.pop(key, default)
+        if tres is None or tres is default:
+            return tres
+        return _SlicedResult(self._slicer(tres.weights), getattr(tres, "count", 0), getattr(tres, "version", 0))
+
+
+class ShardedOptimizer:
+    """Any flame optimizer's ``do()`` executed parameter-sharded over a process group.
+
+    Each rank runs the wrapped optimizer (a drop-in from ``flame_amd.optimizer``) on
+    ITS slice of every state_dict tensor -- a dict with the model's own keys, each
+    value the rank's contiguous range ``[lo, hi)`` of the flattened tensor
+    (``shard_bounds`` with a dtype-independent 2048-element alignment, so a key whose
+    dtype changes between rounds keeps its ranges) -- so the optimizer's state
+    (FedOPT ``m_t`` / ``v_t`` / ``current_weights``, a FedBuff aggregate) exists only
+    for that slice and is never exchanged; one all-gather per
+    result dtype (the rank's slices packed) reassembles the model.  Per element the
+    arithmetic is the wrapped optimizer's, so results are bit-identical to one process.
+
+    * ``do(base_weights, cache, ...)``: the wrapped ``do`` on the slices, then the
+      all-gather into ``base_weights`` (returned).  A key whose result dtype differs
+      (FedOPT promotes integer buffers to fp32, fedopt.py:106-129) gets a new tensor of
+      that dtype, as the reference's ``current_weights`` does.
+    * FedBuff (``accumulate_only=True``): the aggregate stays sharded -- ``do`` returns
+      the wrapped optimizer's slice aggregate, ``scale_add_agg_weights(base_weights,
+      agg, goal)`` applies it on the slices and gathers.  Call ``set_layout(model)``
+      once so arrivals can be sliced before any base is seen.
+    """
+
+    ALIGN_ELEMS = 2048
+
+    def __init__(self, inner, group=None, device: Optional[torch.device] = None, accumulate_only: bool = False):
+        import torch.distributed as dist
+        self.dist = dist
+        self.inner = inner
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device
+        self.accumulate_only = accumulate_only
+        self.layout = None        # key -> (numel, shape, [(lo, hi)] per rank)
+        self._layout_device = None
+
+    # ---------------------------------------------------------------- slicing
+    def set_layout(self, model_weights) -> None:
+        """The model whose per-key ranges the slices cover (FedBuff: the role's self.weights)."""
+        self.layout = collections.OrderedDict()
+        for k, t in model_weights.items():
+            n = t.numel()
+            self.layout[k] = (n, tuple(t.shape), shard_bounds(n, self.world, 1, self.ALIGN_ELEMS))
+        self._layout_device = _first_device(model_weights)
+
+    def _slice(self, weights, device, copy=False):
+        from . import engine
+        out = collections.OrderedDict()
+        for k in weights.keys():
+            n, _, bounds = self.layout[k]
+            lo, hi = bounds[self.rank]
+            t = weights[k]
+            if hi <= lo:
+                t = torch.empty(0, dtype=t.dtype, device=t.device)
+            elif t.is_cuda:
+                t = engine.slice_elems(t, lo, hi, n)      # keeps UpdateSlab views tiled
+            else:
+                t = t.reshape(-1)[lo:hi]
+            if t.device != device:
+                t = t.to(device)                        # H2D of this rank's range only
+            out[k] = t.clone() if copy else t
+        return out
+
+    def _gather_into(self, base_weights, result):
+        out = base_weights
+        packs = collections.OrderedDict()
+        for k, r in result.items():
+            packs.setdefault(r.dtype, []).append(k)
+        for dt, keys in packs.items():
+            pers = [self.layout[k][2][0][1] - self.layout[k][2][0][0] for k in keys]
+            L = sum(pers)
+            dev = result[keys[0]].device
+            local = torch.zeros(L, dtype=dt, device=dev)
+            off = 0
+            for k, per in zip(keys, pers):
+                lo, hi = self.layout[k][2][self.rank]
+                if hi > lo:
+                    local[off:off + hi - lo] = result[k].reshape(-1)[:hi - lo]
+                off += per
+            full = torch.empty(L * self.world, dtype=dt, device=dev)
+            if self.dist.get_backend(self.group) == "gloo" and dev.type == "cuda":
+                host = torch.empty(full.numel(), dtype=dt)
+                self.dist.all_gather_into_tensor(host, local.cpu(), group=self.group)
+                full.copy_(host)
+            else:
+                self.dist.all_gather_into_tensor(full, local, group=self.group)
+            off = 0
+            for k, per in zip(keys, pers):
+                n, shape, bounds = self.layout[k]
+                parts = [full[r * L + off: r * L + off + (hi - lo)] for r, (lo, hi) in enumerate(bounds)]
+                flat = torch.cat(parts) if len(parts) > 1 else parts[0]
+                dst = base_weights[k]
+                if dst.dtype == dt:
+                    dst.copy_(flat.view(shape))
+                else:                     # promoted by the optimizer: a new tensor, as the reference
+                    out[k] = flat.view(shape).to(dst.device).clone()
+                off += per
+        return out
+
+    # ---------------------------------------------------------------- optimizer contract
+    def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
+        if self.accumulate_only:             # FedBuff: base_weights is the (sharded) aggregate
+            if len(cache) == 0 or total == 0:
+                return self.inner.do(base_weights, cache, total=total, version=version, **kwargs)
+            if self.layout is None:
+                raise RuntimeError("ShardedOptimizer(accumulate_only): call set_layout(model_weights) first")
+            device = self.device or self._layout_device
+            sliced = _SliceCache(cache, lambda w: self._slice(w, device))
+            return self.inner.do(base_weights, sliced, total=total, version=version, **kwargs)
+        assert base_weights is not None
+        if len(cache) == 0 or total == 0:
+            return self.inner.do(base_weights, cache, total=total, version=version, **kwargs)
+        if self.layout is None or list(self.layout) != list(base_weights.keys()):
+            self.set_layout(base_weights)
+        device = self.device or _first_device(base_weights)
+        sliced_base = self._slice(base_weights, device, copy=True)
+        sliced = _SliceCache(cache, lambda w: self._slice(w, device))
+        res = self.inner.do(sliced_base, sliced, total=total, version=version, **kwargs)
+        if res is None:
+            return None
+        return self._gather_into(base_weights, res)
+
+    def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal: int):
+        """fedbuff.py:101-127 on this rank's slices, then the all-gather into base_weights."""
+        if self.layout is None:
+            self.set_layout(base_weights)
+        device = self.device or _first_device(base_weights)
+        sliced_base = self._slice(base_weights, device, copy=True)
+        res = self.inner.scale_add_agg_weights(sliced_base, agg_goal_weights, agg_goal)
+        return self._gather_into(base_weights, res)
+
+    def __getattr__(self, name):              # regularizer, m_t, v_t, ... of the wrapped optimizer
+        inner = self.__dict__.get("inner")
+        if inner is None:
+            raise AttributeError(name)
+        return getattr(inner, name)
+
+
+def _first_device(weights):
+    for t in weights.values():
+        return t.device
+    return torch.device("cpu")

@@ -1080,3 +1080,65 @@ def test_sync_hierarchy_vs_oracle_readonly_middles():
     for j in range(M):
         S.assert_bitwise(f"sync/readonly/delta{j}", S.to_cpu(deltas[j]), exp_deltas[j])
     S.assert_bitwise("sync/readonly/top", S.to_cpu(top), exp_top)
+
+
+def _sharded_opt_gpu_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # two ranks share the one GPU
+    ok = True
+    try:
+        from flame_amd import shard
+        from flame_amd.optimizers import optimizer_provider
+        from flame_amd.slab import UpdateSlab
+        g = torch.Generator().manual_seed(51)
+        tmpl = _dyn_model(g, 300_007)
+        hyper = dict(beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+        sharded = shard.ShardedOptimizer(optimizer_provider.get("fedadam", **hyper))
+        single = optimizer_provider.get("fedadam", **hyper)
+        slab = UpdateSlab({k: v for k, v in tmpl.items()}, capacity=16, device=DEV)
+        ws = {k: v.to(DEV) for k, v in tmpl.items()}
+        wr = {k: v.clone() for k, v in ws.items()}
+        for r in range(3):
+            ups = [_dyn_update(g, tmpl, 3 * r + i) for i in range(6)]
+            counts = [11 + 7 * i for i in range(6)]
+            ca, cb = S.SortedCache(), S.SortedCache()
+            for i, u in enumerate(ups):
+                ca[f"t{i}"] = S.TR(slab.put({k: v.to(DEV) for k, v in u.items()}), counts[i])
+                cb[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, counts[i])
+            ws = sharded.do({k: v.clone() for k, v in ws.items()}, ca, total=sum(counts))
+            wr = single.do({k: v.clone() for k, v in wr.items()}, cb, total=sum(counts))
+            torch.cuda.synchronize()
+            for k in wr:
+                a, b = ws[k].cpu(), wr[k].cpu()
+                ok = ok and a.dtype == b.dtype and torch.equal(a.view(torch.int16) if a.dtype in (torch.bfloat16, torch.half) else a,
+                                                               b.view(torch.int16) if b.dtype in (torch.bfloat16, torch.half) else b)
+            del ca, cb
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fedadam_two_ranks_one_gpu():
+    """ShardedOptimizer(FedAdam drop-in) with two gloo ranks sharing the GPU: each rank runs
+    the HIP FedAdam on its per-key slices of slab-resident updates (tiled views sliced
+    tiled); the gathered model == one process's FedAdam, bitwise, over 3 rounds (f32, bf16,
+    f16 keys and an int64 buffer that FedOPT promotes)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sharded_opt_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert res == {0: True, 1: True}, res
