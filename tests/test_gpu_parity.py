@@ -1142,3 +1142,120 @@ def test_sharded_fedadam_two_ranks_one_gpu():
     for p in ps:
         p.join(timeout=30)
     assert res == {0: True, 1: True}, res
+
+
+def test_c4_full_size_fedadam_sampled_columns():
+    """Config 4 at full size (FedAdam, 1024 x 25M fp32 in a tiled slab, round 1 passthrough then
+    an adaptive round): cur / m / v at 65,538 sampled elements vs the oracle FedOPT run on
+    those columns (round 1 bitwise; the adaptive round within the §8(c) contract)."""
+    from flame_amd import synth, engine
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    n, P = 1024, 25_000_000
+    free, _ = torch.cuda.mem_get_info()
+    if free < (n + 10) * P * 4:
+        pytest.skip(f"needs {(n + 10) * P * 4 / 1e9:.1f} GB of HBM, {free / 1e9:.1f} GB free")
+    slab = UpdateSlab({"model": torch.empty(P)}, capacity=n, device=DEV)
+    tmp = torch.empty(P, device=DEV)
+    ws = []
+    for i in range(n):
+        engine.synth_fill_(tmp, 3, 1 + i, 0, 1e-2)
+        ws.append(slab.put({"model": tmp}))
+    del tmp
+    base = _synth_dev(3, 0, P, 1.0)
+    idx = np.sort(np.random.default_rng(1).choice(P, 65_536, replace=False))
+    idx = np.concatenate([[0], idx, [P - 1]])
+    T = slab.storage[torch.float32].shape[2]
+    it = torch.from_numpy(idx).to(DEV)
+    cols = slab.storage[torch.float32][it // T, :, it % T].t().cpu()        # [n, 65538]
+    base_cols = base[it].cpu()
+    amd = make_amd("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    ora = O.OracleFedOPT("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    wa, wo = {"model": base}, {"model": base_cols.clone()}
+    for r in range(2):
+        counts = synth.counts(3 + r, n)
+        total = int(counts.sum())
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i in range(n):
+            ca[f"{i:05d}"] = S.TR(ws[i], int(counts[i]))
+            co[f"{i:05d}"] = S.TR({"model": cols[i].contiguous()}, int(counts[i]))
+        wa = amd.do({"model": wa["model"].clone()}, ca, total=total)
+        wo = ora.do({"model": wo["model"].clone()}, co, total=total)
+        torch.cuda.synchronize()
+        got = {"model": wa["model"][it].cpu()}
+        if r == 0:
+            S.assert_bitwise("c4/r0/cur", got, wo)
+        else:
+            S.assert_close_fedopt("c4/r1/cur", got, wo)
+            S.assert_close_fedopt("c4/r1/m", {"model": amd.m_t["model"][it].cpu()}, {"model": ora.m_t["model"]})
+            S.assert_close_fedopt("c4/r1/v", {"model": amd.v_t["model"][it].cpu()}, {"model": ora.v_t["model"]})
+            S.assert_bitwise("c4/r1/avg", {"model": amd.agg_weights["model"][it].cpu()},
+                             {"model": ora.agg_weights["model"]})
+    del ws, slab, wa, amd
+    torch.cuda.empty_cache()
+
+
+def test_c5_full_size_hierarchy_sampled_columns():
+    """Config 5's per-GPU shard at full size (64 middles x 64 arrivals x 15.625M bf16 = 128 GB
+    in a tiled slab, staleness 0..3): ONE hierarchy_round launch; middle weights, top weights
+    and the top aggregate at 65,538 sampled elements == the oracle's FedBuff op sequence
+    (per-arrival do, scale_add + delta per middle, top do per delta, top scale_add), bitwise."""
+    from flame_amd import synth, engine
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    M, C, P, rnd = 64, 64, 15_625_000, 10
+    free, _ = torch.cuda.mem_get_info()
+    if free < (M * C + 2 * M + 8) * P * 2:
+        pytest.skip(f"needs {(M * C + 2 * M + 8) * P * 2 / 1e9:.1f} GB of HBM, {free / 1e9:.1f} GB free")
+    dt = torch.bfloat16
+    slab = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M * C, device=DEV)
+    tmp = torch.empty(P, dtype=dt, device=DEV)
+    ws = []
+    for i in range(M * C):
+        engine.synth_fill_(tmp, 6, 1 + i, 0, 1e-2)
+        ws.append(slab.put({"model": tmp}))
+    mids = []
+    for m in range(M):
+        engine.synth_fill_(tmp, 6, 10_000 + m, 0, 1.0)
+        mids.append(tmp.clone())
+    engine.synth_fill_(tmp, 6, 0, 0, 1.0)
+    top_w = tmp.clone()
+    del tmp
+    stale = [int(x) % 4 for x in synth.counts(6, M * C)]
+    idx = np.sort(np.random.default_rng(2).choice(P, 65_536, replace=False))
+    idx = np.concatenate([[0], idx, [P - 1]])
+    it = torch.from_numpy(idx).to(DEV)
+    T = slab.storage[dt].shape[2]
+    cols = slab.storage[dt][it // T, :, it % T].t().cpu()                  # [M*C, 65538]
+    mid_cols = [x[it].cpu() for x in mids]
+    top_cols = top_w[it].cpu()
+    opts, aggs = [make_amd("fedbuff") for _ in range(M)], [None] * M
+    for m in range(M):
+        for t in range(C):
+            cache = S.SortedCache()
+            cache[f"{m * C + t:05d}"] = S.TR(ws[m * C + t], 1, rnd - stale[m * C + t])
+            aggs[m] = opts[m].do(aggs[m], cache, total=1, version=rnd)
+    top_agg, _ = hierarchy_round([({"model": mids[m]}, aggs[m], C, rnd - (m % 2)) for m in range(M)], None,
+                                 version=rnd, top_weights={"model": top_w}, top_goal=M)
+    torch.cuda.synchronize()
+    # oracle on the sampled columns
+    top_o, top_agg_o = O.OracleFedBuff(), None
+    for m in range(M):
+        mo, agg_o = O.OracleFedBuff(), None
+        for t in range(C):
+            cache = S.SortedCache()
+            cache["a"] = S.TR({"model": cols[m * C + t].contiguous()}, 1, rnd - stale[m * C + t])
+            agg_o = mo.do(agg_o, cache, total=1, version=rnd)
+        w = {"model": mid_cols[m].clone()}
+        d = {"model": O.scale_add_tensor(w["model"], agg_o["model"], C, want_delta=True)}
+        S.assert_bitwise(f"c5/mid{m}", {"model": mids[m][it].cpu()}, w)
+        cache = S.SortedCache()
+        cache["d"] = S.TR(d, 1, rnd - (m % 2))
+        top_agg_o = top_o.do(top_agg_o, cache, total=1, version=rnd)
+    S.assert_bitwise("c5/top agg", {"model": top_agg["model"][it].cpu()}, top_agg_o)
+    tw = {"model": top_cols.clone()}
+    top_o.scale_add_agg_weights(tw, top_agg_o, M)
+    S.assert_bitwise("c5/top w", {"model": top_w[it].cpu()}, tw)
+    del ws, aggs, opts, slab, top_agg
+    torch.cuda.empty_cache()
