@@ -88,6 +88,10 @@ namespace {
 #define FLAME_OCC_LDS 0   // sweep variants: dynamic LDS bytes per reduction / hierarchy workgroup (caps
                           // resident workgroups per CU at 160 KiB / FLAME_OCC_LDS; the kernels use no LDS)
 #endif
+#ifndef FLAME_XCD_SWIZZLE
+#define FLAME_XCD_SWIZZLE 0  // sweep variant: each XCD (workgroups are dispatched to XCDs round-robin)
+                             // streams one contiguous eighth of the chunks
+#endif
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
@@ -485,9 +489,16 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
     for (int k = 0; k < kWGC; ++k)
         if (full[k]) store_chunk(op[k], ov[k]);
 #else
+#if FLAME_XCD_SWIZZLE
+    // bijection: XCD x (= blockIdx % 8) owns q + (x < r) consecutive workgroup slots
+    const int64_t q = gridDim.x / 8, r = gridDim.x % 8, x = blockIdx.x % 8;
+    const int64_t wg = x * q + (x < r ? x : r) + blockIdx.x / 8;
+#else
+    const int64_t wg = blockIdx.x;
+#endif
 #pragma unroll 1
     for (int k = 0; k < kWGC; ++k) {
-        const int64_t chunk = static_cast<int64_t>(blockIdx.x) * kWGC + k;
+        const int64_t chunk = wg * kWGC + k;
         if (chunk >= n_chunks) break;
         V16 ov[kVPT];
         T* op;

@@ -61,6 +61,7 @@ VARIANTS = {
     "occ4": {"FLAME_OCC_LDS": 40960},
     "occ5": {"FLAME_OCC_LDS": 32768},
     "occ6": {"FLAME_OCC_LDS": 27136},
+    "xcd": {"FLAME_XCD_SWIZZLE": 1},
 }
 
 
