@@ -1259,3 +1259,17 @@ def test_c5_full_size_hierarchy_sampled_columns():
     S.assert_bitwise("c5/top w", {"model": top_w[it].cpu()}, tw)
     del ws, aggs, opts, slab, top_agg
     torch.cuda.empty_cache()
+
+
+def test_mnist_example_config1():
+    """Config 1 (examples/mnist: 2 trainers x MNIST Net, counts 2000/2000) end to end through
+    channel payloads -> ingest.decode -> DeviceUpdateCache -> FedAvg drop-in, bitwise vs the
+    reference's op sequence each round (examples/mnist_aggregation.py)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "mnist_aggregation", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                          "examples", "mnist_aggregation.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.run(rounds=3, verbose=False)
