@@ -64,6 +64,8 @@ def run(rounds: int = 3, seed: int = 0, verbose: bool = True) -> bool:
     host_weights = {k: v.clone() for k, v in weights.items()}
     weights = {k: v.to(dev) for k, v in weights.items()}
     optimizer = optimizer_provider.get("fedavg")
+    # the role's self.cache lives across rounds (syncfl/top_aggregator.py internal init)
+    cache = ingest.DeviceUpdateCache(device=dev, placement="hbm", capacity=4)
     ok = True
     for rnd in range(rounds):
         # trainers: train (here: a synthetic delta) and send {WEIGHTS, DATASET_SIZE} on the channel
@@ -74,7 +76,6 @@ def run(rounds: int = 3, seed: int = 0, verbose: bool = True) -> bool:
             sent.append((local, 2000))
         # aggregator: recv_fifo -> cache[end] = TrainResult(weights, count); total = Σ count
         t0 = time.perf_counter()
-        cache = ingest.DeviceUpdateCache(device=dev, placement="hbm", capacity=4)
         total = 0
         for end, payload in payloads:
             msg = ingest.decode(payload)
