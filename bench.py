@@ -138,11 +138,26 @@ def cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
         ts.append(time.perf_counter() - t0)
     t = statistics.median(ts)
     model = _cpu_model()
+    # also one thread (a smaller sample keeps it to a few seconds)
+    threads = torch.get_num_threads()
+    n1 = min(16, n_cpu)
+    torch.set_num_threads(1)
+    try:
+        t1s = []
+        for _ in range(rounds):
+            t0 = time.perf_counter()
+            torch_cpu.fedavg_round(agg, ups[:n1], cts[:n1], tot)
+            t1s.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(threads)
+    t1 = statistics.median(t1s)
     return {
-        "value": n_cpu * P / t, "unit": "client-params/s", "cores": torch.get_num_threads(), "kind": "port",
+        "value": n_cpu * P / t, "unit": "client-params/s", "cores": threads, "kind": "port",
         "sample": f"reference FedAvg op sequence (fedavg.py:84-104, torch CPU, oracle/torch_cpu.py) over "
                   f"{n_cpu} of the same synthetic clients x {P} fp32 params, median of {rounds} rounds "
-                  f"({t:.3f} s/round), {torch.get_num_threads()} threads on {model}; diskcache I/O excluded",
+                  f"({t:.3f} s/round), {threads} threads on {model}; diskcache I/O excluded",
+        "single_thread": {"value": n1 * P / t1, "cores": 1,
+                          "sample": f"{n1} clients x {P}, median of {rounds} rounds ({t1:.3f} s/round)"},
     }
 
 
