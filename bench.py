@@ -460,7 +460,11 @@ def main():
         k_bytes = ks["bytes_per_launch"] * launches_per_step
         achieved = k_bytes / k_time / 1e9
         line = {
-            "metric": METRIC,
+            # BASELINE.json's metric for the headline FedAvg; the FedOPT workloads (config 4) name theirs
+            "metric": METRIC if args.workload == "fedavg" else
+            f"aggregated params/sec (device-resident), {n}-client "
+            f"{ {'fedadam': 'FedAdam', 'fedyogi': 'FedYogi', 'fedadagrad': 'FedAdaGrad'}.get(args.workload, args.workload)}"
+            f" (adaptive round)",
             "value": n * P * world / (elapsed / args.steps),
             "unit": "client-params/s",
             "n_gpus": world,
