@@ -535,7 +535,8 @@ def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_
     # arrivals + middle weights (read, write) [+ deltas] + top (in) + top out [+ top weights r/w]
     # distinct middle-weight tensors (read-only middles may share one base: it is read once)
     wsum = sum(s.numel * len(set(int(p) for p in s.mid_w)) for s in segs)
-    nbytes = isz * (P * (M * C + (M if with_delta else 0) + (1 if top_accum else 0) + 1
+    top_out = any(s.top_out for s in segs)
+    nbytes = isz * (P * (M * C + (M if with_delta else 0) + (1 if top_accum else 0) + (1 if top_out else 0)
                          + (2 if top_goal is not None else 0)) + wsum * (1 if mid_readonly else 2))
     with _timed("flame_hier_fedbuff", device, nbytes):
         N.check(L.flame_hier_fedbuff(code, flags, b + p.offs["segs"], p.n_segs, p.n_chunks, M, C,

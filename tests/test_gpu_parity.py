@@ -364,6 +364,55 @@ def test_fedbuff_deferred_equals_per_arrival(dtype):
     S.assert_bitwise("scale_add", S.to_cpu(wa), S.to_cpu(wb))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("placement", ["slab", "tensors"])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_fedbuff_fused_scale_add(dtype, placement, with_delta):
+    """scale_add straight from the queued arrivals (one flame_hier_fedbuff launch, the
+    aggregate never materialised) == flush + scale_add, bitwise -- weights, delta, and the
+    aggregate itself when it is read afterwards; an already materialised aggregate takes
+    the separate path."""
+    from flame_amd import engine
+    from flame_amd.slab import UpdateSlab
+    g = torch.Generator().manual_seed(71)
+    shapes = {"w": (3001,), "m": (17, 129), "b": (5,)}
+    K, rnd = 11, 9
+    ups = [{k: (torch.randn(s, generator=g) * 1e-2).to(dtype) for k, s in shapes.items()} for _ in range(K)]
+    w0 = {k: torch.randn(s, generator=g).to(dtype) for k, s in shapes.items()}
+    slab = UpdateSlab({k: torch.empty(s, dtype=dtype) for k, s in shapes.items()}, capacity=2 * K, device=DEV) \
+        if placement == "slab" else None
+    res = {}
+    for fuse in (True, False):
+        opt, agg = make_amd("fedbuff", fuse_scale_add=fuse), None
+        for i, u in enumerate(ups):
+            w = {k: v.to(DEV) for k, v in u.items()}
+            cache = S.SortedCache()
+            cache["a"] = S.TR(slab.put(w) if slab is not None else w, 1, rnd - i % 4)
+            agg = opt.do(agg, cache, total=1, version=rnd)
+        base = {k: v.to(DEV) for k, v in w0.items()}
+        launches = []
+        engine._recorders.append(launches)
+        try:
+            if with_delta:
+                _, delta = opt.scale_add_agg_weights_with_delta(base, agg, K)
+            else:
+                opt.scale_add_agg_weights(base, agg, K)
+                delta = None
+        finally:
+            engine._recorders.remove(launches)
+        names = [e[0] for e in launches]
+        if fuse:
+            assert names == ["flame_hier_fedbuff"], names    # one launch per dtype (3 keys, one dtype)
+        else:
+            assert "flame_hier_fedbuff" not in names, names
+        res[fuse] = (S.to_cpu(base), S.to_cpu(delta) if delta is not None else None, S.to_cpu(dict(agg)))
+        del agg
+    S.assert_bitwise("fused base", res[True][0], res[False][0])
+    if with_delta:
+        S.assert_bitwise("fused delta", res[True][1], res[False][1])
+    S.assert_bitwise("aggregate read afterwards", res[True][2], res[False][2])
+
+
 def test_zero_copy_pinned_host_clients():
     """Pinned host updates are streamed by the kernel directly (no staging copy): bitwise."""
     O = _oracle()
