@@ -205,6 +205,10 @@ typedef struct flame_hier_segment {
  *   mid_rates : device [n_mids][n_clients] fp32 staleness rates float(1/sqrt(1+version-v))
  *   mid_goal  : device [n_mids] float(agg_goal) of each middle; top_rates: device [n_mids]
  * dtype FLAME_F32, FLAME_BF16 or FLAME_F16.
+ * With n_mids = 1, top_agg_out = NULL and no flags this is a single FedBuff aggregator's
+ * scale_add (optimizer/fedbuff.py:101-127) applied straight from its queued arrivals
+ * (fedbuff.py:89-97,136-157) -- the aggregate is never stored (the async top's round,
+ * asyncfl/top_aggregator.py:85-110).
  */
 int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment *segs, int32_t n_segs,
                        int64_t n_chunks, int32_t n_mids, int32_t n_clients, const void *const *mid_w,

@@ -13,6 +13,7 @@ References (``/root/reference/lib/python/flame/``):
   * FedBuff.do           optimizer/fedbuff.py:59-99, scale_add :101-127, _aggregate :136-157
   * FedDyn               optimizer/feddyn.py:51-62 (save_state), :64-115 (do), :125-139 (add_to_hist)
   * Scaffold             optimizer/scaffold.py:58-90 (save_state), :92-139 (do), :141-150
+  * FedGFT               optimizer/fedgft.py:27-58 (FedAvg.do + update_bias), bias.py:74-106
 Parity of this oracle is pinned by ``tests/test_oracle_golden.py`` against
 vectors produced by the real reference (``tests/golden/make_golden.py``).
 """
