@@ -619,7 +619,7 @@ def test_fedopt_fused_reduced_precision_vs_reference_ops(sort, dtype):
 def _dyn_model(g, P):
     return {"w": torch.randn(P, generator=g), "m": torch.randn(31, 129, generator=g),
             "bf": torch.randn(4099, generator=g).bfloat16(), "h": torch.randn(777, generator=g).half(),
-            "nbt": torch.tensor(3, dtype=torch.int64)}
+            "d": torch.randn(2051, generator=g).double(), "nbt": torch.tensor(3, dtype=torch.int64)}
 
 
 def _dyn_update(g, tmpl, i, scale=1e-2):
@@ -666,8 +666,8 @@ def test_feddyn_vs_oracle_partial_participation(placement, order):
         ca_w, co_w = amd.cld_model, ora.cld_model
         del ca, co
     engine._recorders.remove(launches)
-    # float keys (f32, bf16, f16 groups) run as one flame_feddyn_round per dtype each round
-    assert sum(1 for ev in launches if ev[0] == "flame_feddyn_round") == 3 * len(rounds)
+    # float keys (f32, bf16, f16, f64 groups) run as one flame_feddyn_round per dtype each round
+    assert sum(1 for ev in launches if ev[0] == "flame_feddyn_round") == 4 * len(rounds)
     assert list(amd.local_param_dict) == list(ora.local_param_dict)
     for e, h in ora.local_param_dict.items():
         if h is not None:
