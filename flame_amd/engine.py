@@ -670,7 +670,9 @@ def accumulate(agg: dict, entries, *, device=None) -> None:
     """
     if not entries:
         return
-    device = device or pick_device(agg, *[w for w, _ in entries])
+    if device is None:   # the aggregate's own device first (no per-entry list for the common case)
+        device = next((t.device for t in agg.values() if isinstance(t, torch.Tensor) and t.is_cuda), None) \
+            or pick_device(*[w for w, _ in entries])
     if _accumulate_slab(agg, entries, device):
         return
     keys = list(agg.keys())
@@ -707,9 +709,13 @@ def _accumulate_slab(agg: dict, entries, device) -> bool:
     if slab is None or slab.device != device or len(slab.keys) != len(agg):
         return False
     nk = len(slab.keys)
-    for w, _ in entries:
-        if getattr(w, "slab", None) is not slab or len(w) != nk:
-            return False
+    # one pass: every entry a full SlotWeights of this slab (SlotWeights carry .slab/.slot)
+    try:
+        slot_list = [w.slot for w, _ in entries if w.slab is slab and len(w) == nk]
+    except AttributeError:
+        return False
+    if len(slot_list) != len(entries):
+        return False
     layouts = {}
     for k in agg.keys():
         if k not in slab.meta:
@@ -718,7 +724,7 @@ def _accumulate_slab(agg: dict, entries, device) -> bool:
         if lay[0] != agg[k].dtype or agg[k].numel() != lay[1]:
             return False
         layouts[k] = lay
-    slots = np.fromiter((w.slot for w, _ in entries), dtype=np.uint64, count=len(entries))
+    slots = np.array(slot_list, dtype=np.uint64)
     rates = [r for _, r in entries]
     targets = {k: _Target(agg[k], device) for k in agg.keys()}
     groups = collections.OrderedDict()

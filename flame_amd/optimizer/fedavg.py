@@ -28,12 +28,8 @@ class FedAvg(AbstractOptimizer):
         self.regularizer = Regularizer()
 
     def _pop_entries(self, cache, total):
-        entries = []
-        for k in list(cache.iterkeys()):
-            # after popping, the item is removed from the cache (fedavg.py:80-82)
-            tres = cache.pop(k)
-            entries.append((tres.weights, tres.count / total))
-        return entries
+        # after popping, the item is removed from the cache (fedavg.py:80-82); rate = count / total
+        return [(tres.weights, tres.count / total) for tres in map(cache.pop, list(cache.iterkeys()))]
 
     def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         """Aggregate the cached trainer updates into ``base_weights`` (in place)."""
