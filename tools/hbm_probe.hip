@@ -94,3 +94,39 @@ extern "C" int probe_read_region(const void* p, int64_t bytes, void* out, int64_
     else hipLaunchKernelGGL((read_region_kernel<8>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, region, pitch, bytes, (uint32_t*)out);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Mixed read/write region probe: workgroup w reads R contiguous 4 KiB steps of region w
+// (UN in flight) and then writes ONE 4 KiB block (256 lanes x 16 B) to dst + w * 4 KiB --
+// the traffic shape of the reduction kernel with R - 1 clients plus the base (R reads per
+// output block).  POL: 0 plain store, 4 write-through `sc0 sc1 nt` (the product's policy).
+template <int POL>
+__global__ __launch_bounds__(256) void mix_region_kernel(const uint8_t* __restrict__ p, uint8_t* __restrict__ dst,
+                                                         int R) {
+    const int64_t region = (int64_t)R * 4096;
+    const uint8_t* src = p + (int64_t)blockIdx.x * region + threadIdx.x * 16;
+    u4 acc = {0u, 0u, 0u, 0u};
+    int i = 0;
+    for (; i + 8 <= R; i += 8) {
+        u4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(src + (int64_t)(i + u) * 4096));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u];
+    }
+    for (; i < R; ++i)
+        acc ^= __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(src + (int64_t)i * 4096));
+    uint8_t* o = dst + (int64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    if constexpr (POL == 4) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(o), "v"(acc) : "memory");
+    } else {
+        *(__attribute__((address_space(1))) u4*)o = acc;
+    }
+}
+
+extern "C" int probe_mix_region(const void* p, void* dst, int64_t blocks, int R, int pol, void* stream) {
+    if (R < 1 || blocks < 1 || blocks > 0x7FFFFFFF) return 2;
+    if (pol == 4) hipLaunchKernelGGL((mix_region_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, (uint8_t*)dst, R);
+    else hipLaunchKernelGGL((mix_region_kernel<0>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, (uint8_t*)dst, R);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
