@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""FedDyn round kernel: history layout A/B (contiguous rows vs tiled like the UpdateSlab).
+"""FedDyn round kernel: history layout A/B (contiguous rows vs tiled like the UpdateSlab),
+updated in place or written to a second buffer (ping-pong).
 
 One process, interleaved rounds, 512 ends x 25M fp32, every end tracked and arriving
 (the merged one-pass program: read w, read h, write h', avg, mean).  Arrivals are
@@ -36,6 +37,9 @@ def main():
     engine.synth_fill_(h_rows.view(-1), 3, 2, 0, 1e-2)
     h_tiled = torch.empty((tiles, n, T), dtype=torch.float32, device=dev)
     engine.synth_fill_(h_tiled.view(-1), 3, 2, 0, 1e-2)
+    # second history buffers: the updated history written to a different address (ping-pong)
+    h_rows2 = torch.empty_like(h_rows)
+    h_tiled2 = torch.empty_like(h_tiled)
     base = torch.empty(P, dtype=torch.float32, device=dev)
     engine.synth_fill_(base, 3, 0, 0, 1.0)
     out = torch.empty_like(base)
@@ -50,6 +54,13 @@ def main():
         "tiled": engine.DynSeg(P, out=out.data_ptr(), inp=base.data_ptr(), cld=cld.data_ptr(),
                                steps=[(wp[i], h_tiled[0, i].data_ptr(), h_tiled[0, i].data_ptr()) for i in range(n)],
                                tile_stride=n * T * 4, hist_tile_stride=n * T * 4),
+        "rows_pingpong": engine.DynSeg(P, out=out.data_ptr(), inp=base.data_ptr(), cld=cld.data_ptr(),
+                                       steps=[(wp[i], h_rows[i].data_ptr(), h_rows2[i].data_ptr()) for i in range(n)],
+                                       tile_stride=n * T * 4),
+        "tiled_pingpong": engine.DynSeg(P, out=out.data_ptr(), inp=base.data_ptr(), cld=cld.data_ptr(),
+                                        steps=[(wp[i], h_tiled[0, i].data_ptr(), h_tiled2[0, i].data_ptr())
+                                               for i in range(n)],
+                                        tile_stride=n * T * 4, hist_tile_stride=n * T * 4),
     }
     nbytes = (3 * n + 3) * P * 4
     times = {k: [] for k in variants}
