@@ -722,6 +722,7 @@ def bench_hier(args, world, rank, dev):
                        + ("FedAvg (synchronous) shard" if sync else "FedBuff shard")),
             "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
+            "host_issue_ms_per_step": ISSUE_S / args.steps * 1e3,
             "dtype": "bf16", "config": {"workload": f"{'hier_fedavg' if sync else 'hier_fedbuff'}: {M} middles x {C} "
                                                     f"clients x {P} bf16 per GPU",
                                         "middles": args.hier_mode, "middle_weights": args.hier_middles},
