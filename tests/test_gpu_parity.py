@@ -1322,3 +1322,29 @@ def test_mnist_example_config1():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.run(rounds=3, verbose=False)
+
+
+def test_integration_ctypes_stub_runs():
+    """The reference-side ctypes stub printed in INTEGRATION.md §2 works as written
+    (library path substituted) and equals the oracle's FedAvg, bitwise."""
+    import os
+    import re
+    from flame_amd import _native
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    code = re.search(r"```python\n(# flame/optimizer/_mi355x\.py.*?)```", doc, re.S).group(1)
+    code = code.replace('ctypes.CDLL("libflame_amd.so")', f'ctypes.CDLL("{_native.LIB_PATH}")')
+    ns = {}
+    exec(compile(code, "INTEGRATION.md:stub", "exec"), ns)
+    O = _oracle()
+    g = torch.Generator().manual_seed(77)
+    P, n = 100_003, 9
+    agg = torch.randn(P, generator=g)
+    ups = [torch.randn(P, generator=g) * 1e-2 for _ in range(n)]
+    rates = [(i + 1) / 45 for i in range(n)]
+    dev_agg = agg.to(DEV)
+    ns["aggregate_fp32"](dev_agg, [u.to(DEV) for u in ups], rates)
+    torch.cuda.synchronize()
+    exp = agg.clone()
+    O.reduce_tensor(exp, ups, rates)
+    S.assert_bitwise("ctypes stub", {"x": dev_agg}, {"x": exp})
