@@ -69,6 +69,9 @@ def assert_close_fedopt(label, got, exp, rtol=1e-6, elementwise=True):
     where |ref| >= rtol*max|ref|, and rel-L2 <= rtol; across rounds (state already differs by
     torch-CPU's sqrt ulps) rel-L2 <= rtol only (elementwise=False)."""
     for k in exp:
+        assert got[k].shape == exp[k].shape, f"{label}/{k}: shape {got[k].shape} vs {exp[k].shape}"
+        if exp[k].numel() == 0:
+            continue
         g = got[k].detach().cpu().double()
         e = exp[k].double()
         den = e.abs()

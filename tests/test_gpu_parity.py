@@ -1348,3 +1348,73 @@ def test_integration_ctypes_stub_runs():
     exp = agg.clone()
     O.reduce_tensor(exp, ups, rates)
     S.assert_bitwise("ctypes stub", {"x": dev_agg}, {"x": exp})
+
+
+def test_empty_and_tiny_keys_every_path():
+    """Models with 0-element and 1-element tensors between ordinary ones: FedAvg, FedAdam,
+    FedBuff (fused scale_add), FedDyn and the sync hierarchy all match the oracle, bitwise
+    (FedOPT within the §8(c) contract)."""
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    O = _oracle()
+    g = torch.Generator().manual_seed(91)
+    shapes = {"a": (0,), "w": (5000,), "e": (0, 7), "one": (1,), "m": (33, 3)}
+
+    def model(scale):
+        return {k: torch.randn(s, generator=g) * scale for k, s in shapes.items()}
+    base, ups = model(1.0), [model(1e-2) for _ in range(5)]
+    counts = [3, 9, 1, 4, 7]
+
+    def caches():
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i, (u, c) in enumerate(zip(ups, counts)):
+            ca[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, c, 5 - i % 2)
+            co[f"t{i}"] = S.TR({k: v.clone() for k, v in u.items()}, c, 5 - i % 2)
+        return ca, co
+    # FedAvg
+    ca, co = caches()
+    out = make_amd("fedavg").do({k: v.to(DEV) for k, v in base.items()}, ca, total=sum(counts))
+    exp = O.OracleFedAvg().do({k: v.clone() for k, v in base.items()}, co, total=sum(counts))
+    S.assert_bitwise("fedavg", S.to_cpu(out), exp)
+    # FedAdam: passthrough round then an adaptive round
+    amd, ora = make_amd("fedadam"), O.OracleFedOPT("fedadam")
+    wa, wo = {k: v.to(DEV) for k, v in base.items()}, {k: v.clone() for k, v in base.items()}
+    for _ in range(2):
+        ca, co = caches()
+        wa = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=sum(counts))
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, co, total=sum(counts))
+    S.assert_close_fedopt("fedadam", S.to_cpu(wa), wo)
+    # FedBuff: arrivals one per do(), fused scale_add
+    fb, ob, fa, oa = make_amd("fedbuff"), O.OracleFedBuff(), None, None
+    for i, (u, c) in enumerate(zip(ups, counts)):
+        c1, c2 = S.SortedCache(), S.SortedCache()
+        c1["a"] = S.TR({k: v.to(DEV) for k, v in u.items()}, c, 5 - i % 2)
+        c2["a"] = S.TR({k: v.clone() for k, v in u.items()}, c, 5 - i % 2)
+        fa = fb.do(fa, c1, total=c, version=5)
+        oa = ob.do(oa, c2, total=c, version=5)
+    wb, wbo = {k: v.to(DEV) for k, v in base.items()}, {k: v.clone() for k, v in base.items()}
+    fb.scale_add_agg_weights(wb, fa, 5)
+    ob.scale_add_agg_weights(wbo, oa, 5)
+    S.assert_bitwise("fedbuff", S.to_cpu(wb), wbo)
+    # FedDyn, two rounds
+    da, do_ = make_amd("feddyn", alpha=0.1), O.OracleFedDyn(alpha=0.1)
+    xa, xo = {k: v.to(DEV) for k, v in base.items()}, {k: v.clone() for k, v in base.items()}
+    for _ in range(2):
+        da.save_state(S._PRE, active_ends=[f"t{i}" for i in range(5)])
+        do_.save_state(S._PRE, active_ends=[f"t{i}" for i in range(5)])
+        ca, co = caches()
+        xa = da.do({k: v.clone() for k, v in xa.items()}, ca, total=sum(counts))
+        xo = do_.do({k: v.clone() for k, v in xo.items()}, co, total=sum(counts))
+        S.assert_bitwise("feddyn cld", S.to_cpu(da.cld_model), do_.cld_model)
+        xa, xo = da.cld_model, do_.cld_model
+    # sync hierarchy: two middles of the same five trainers
+    mids = [{k: v.to(DEV) for k, v in base.items()} for _ in range(2)]
+    top = {k: v.to(DEV) for k, v in base.items()}
+    specs = [(mids[j], caches()[0], sum(counts)) for j in range(2)]
+    top, _ = sync_hierarchy_round(specs, top)
+    exp_mid = O.OracleFedAvg().do({k: v.clone() for k, v in base.items()}, caches()[1], total=sum(counts))
+    d = {k: exp_mid[k] - base[k] for k in base}
+    tc = S.SortedCache()
+    tc["m0"], tc["m1"] = S.TR(d, sum(counts)), S.TR({k: v.clone() for k, v in d.items()}, sum(counts))
+    exp_top = O.OracleFedAvg().do({k: v.clone() for k, v in base.items()}, tc, total=2 * sum(counts))
+    S.assert_bitwise("sync mid", S.to_cpu(mids[0]), exp_mid)
+    S.assert_bitwise("sync top", S.to_cpu(top), exp_top)
