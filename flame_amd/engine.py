@@ -93,11 +93,12 @@ class Plan:
 
 
 def plan(code: int, segs: Sequence[Seg], rates: Sequence, chunk: Optional[int] = None,
-         seg_rates: bool = False) -> Plan:
+         seg_rates: bool = False, compact: bool = False) -> Plan:
     """Build the device metadata block for one launch (no GPU needed).
 
     ``rates`` holds one rate per client, or with ``seg_rates`` one row of rates per
-    segment (FLAME_AGG_SEG_RATES)."""
+    segment (FLAME_AGG_SEG_RATES).  ``compact`` keeps only the rate array the dtype
+    reads (its other offset is -1) -- the kernel-argument launch path."""
     n_segs = len(segs)
     if n_segs == 0:
         raise ValueError("empty segment list")
@@ -129,10 +130,18 @@ def plan(code: int, segs: Sequence[Seg], rates: Sequence, chunk: Optional[int] =
     r32 = r64.astype(np.float32)            # RNE, as torch rounds a Python float scalar
     if r32.size % 2:
         r32 = np.concatenate([r32, np.zeros(1, np.float32)])
-    off_r64 = off_r32 + r32.size * 4
-    meta = np.concatenate([head.view(np.int64).reshape(-1), table.view(np.int64).reshape(-1),
-                           r32.view(np.int64), r64.view(np.int64)])
-    return Plan(code, meta, n_segs, begin, n, off_clients, off_r32, off_r64)
+    parts = [head.view(np.int64).reshape(-1), table.view(np.int64).reshape(-1)]
+    if compact:    # only the rate array the dtype reads (f64 tensors use the fp64 rates)
+        if code == N.FLAME_F64:
+            off_r64, off_r32 = off_r32, -1
+            parts.append(r64.view(np.int64))
+        else:
+            off_r64 = -1
+            parts.append(r32.view(np.int64))
+    else:
+        off_r64 = off_r32 + r32.size * 4
+        parts += [r32.view(np.int64), r64.view(np.int64)]
+    return Plan(code, np.concatenate(parts), n_segs, begin, n, off_clients, off_r32, off_r64)
 
 
 # ------------------------------------------------------------------ device staging
@@ -141,8 +150,12 @@ class _Staging:
 
     def __init__(self):
         self._inflight = collections.deque()
+        self._streams = {}
 
     def upload(self, meta: np.ndarray, device: torch.device) -> torch.Tensor:
+        """The copy runs on a side stream, so it overlaps whatever kernel the launch stream is
+        still running (the next launch only waits for its own few-KB table, not for a copy
+        queued behind the previous kernel); the launch stream waits on the copy's event."""
         while self._inflight and self._inflight[0][0].query():
             self._inflight.popleft()
         host = torch.from_numpy(meta)
@@ -150,9 +163,16 @@ class _Staging:
             host = host.pin_memory()
         except RuntimeError:
             pass
-        dev = host.to(device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
+        cur = torch.cuda.current_stream(device)
+        side = self._streams.get(device)
+        if side is None:
+            side = self._streams[device] = torch.cuda.Stream(device)
+        with torch.cuda.stream(side):
+            dev = host.to(device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        cur.wait_event(ev)
+        dev.record_stream(cur)      # allocated on the side stream, read by kernels on the launch stream
         self._inflight.append((ev, host))
         return dev
 
@@ -343,14 +363,39 @@ def _launch_reduce(code, segs, rates, device, keep, *, init_first=False, seg_rat
     flags = N.FLAME_AGG_INIT_FIRST if init_first else 0
     if seg_rates:
         flags |= N.FLAME_AGG_SEG_RATES
+    nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (_n_clients(rates, seg_rates) + (1 if init_first else 2))
+    if ARGMETA:
+        # small launch: the metadata block goes with the dispatch as a kernel argument (no H2D blit)
+        p = plan(code, segs, rates, seg_rates=seg_rates, compact=True)
+        if p.meta.nbytes <= argmeta_max_bytes():
+            with _timed("flame_agg_reduce", device, nbytes):
+                N.check(L.flame_agg_reduce_argmeta(code, flags, p.meta.ctypes.data, p.meta.nbytes, p.n_segs,
+                                                   p.n_chunks, p.n_clients, p.off_clients, p.off_r32, p.off_r64,
+                                                   _stream_ptr(device)))
+            return
     p = plan(code, segs, rates, seg_rates=seg_rates)
     dm = _staging.upload(p.meta, device)
     segp, clp, r32p, r64p = _device_ptrs(dm, p)
-    nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (p.n_clients + (1 if init_first else 2))
     with _timed("flame_agg_reduce", device, nbytes):
         N.check(L.flame_agg_reduce(code, flags, segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, r64p,
                                    _stream_ptr(device)))
     keep.append(dm)
+
+
+# Kernel-argument metadata for small launches (FLAME_AMD_ARGMETA=0 disables).
+ARGMETA = os.environ.get("FLAME_AMD_ARGMETA", "1") != "0"
+_ARGMETA_MAX = None
+
+
+def argmeta_max_bytes() -> int:
+    global _ARGMETA_MAX
+    if _ARGMETA_MAX is None:
+        _ARGMETA_MAX = int(N.lib().flame_agg_argmeta_max_bytes())
+    return _ARGMETA_MAX
+
+
+def _n_clients(rates, seg_rates) -> int:
+    return len(rates[0]) if seg_rates else len(rates)
 
 
 FEDOPT_VARIANT = {"fedadam": N.FLAME_FEDADAM, "fedyogi": N.FLAME_FEDYOGI, "fedadagrad": N.FLAME_FEDADAGRAD}

@@ -136,6 +136,20 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment *segs, int32
                      const float *rates32, const double *rates64, void *stream);
 
 /*
+ * flame_agg_reduce for small launches: the same metadata block (segments, then the client
+ * pointer table and the rates, at byte offsets off_clients / off_r32 / off_r64 -- pass -1 for
+ * the rate array the dtype does not use) is passed from HOST memory and travels to the GPU as
+ * a kernel argument, so no H2D copy (a blit kernel on gfx950, ≈15 µs of GPU timeline per
+ * launch) precedes the reduction.  meta_bytes <= flame_agg_argmeta_max_bytes() (3,584).
+ * Semantics, flags and dtypes as flame_agg_reduce; the client and segment pointers inside
+ * the block are device pointers as there.
+ */
+int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void *host_meta, int64_t meta_bytes,
+                             int32_t n_segs, int64_t n_chunks, int32_t n_clients, int64_t off_clients,
+                             int64_t off_r32, int64_t off_r64, void *stream);
+int64_t flame_agg_argmeta_max_bytes(void);
+
+/*
  * Fused FedAvg + FedOPT adaptive step (dtype FLAME_F32, FLAME_BF16 or FLAME_F16; base,
  * cur, m, v, outputs and clients all of that dtype).  After the reduction above (avg kept
  * in registers, optionally written to seg.out), per element, every op rounded in dtype:

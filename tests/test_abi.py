@@ -97,3 +97,18 @@ def test_feddyn_round_validates_without_gpu():
     assert b"step flag" in L.flame_last_error()
     assert L.flame_feddyn_round(0, fake, 1, 1, fake, fake, 2, 3, 0.5, 0.5, None) == _native.FLAME_EINVAL
     assert b"n_phase1" in L.flame_last_error()
+
+
+def test_agg_reduce_argmeta_validates_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    cap = L.flame_agg_argmeta_max_bytes()
+    assert cap == 3584
+    blk = (ctypes.c_uint64 * 64)()
+    assert L.flame_agg_reduce_argmeta(0, 0, None, 80, 1, 1, 0, 80, -1, -1, None) == _native.FLAME_EINVAL
+    assert L.flame_agg_reduce_argmeta(0, 0, blk, cap + 8, 1, 1, 0, 80, -1, -1, None) == _native.FLAME_EINVAL
+    assert L.flame_agg_reduce_argmeta(0, 0, blk, 512, 1, 1, 100, 80, 96, -1, None) == _native.FLAME_EINVAL
+    assert b"outside" in L.flame_last_error()
+    assert L.flame_agg_reduce_argmeta(0, 0, blk, 512, 1, 1, 4, 80, -1, -1, None) == _native.FLAME_EINVAL
+    assert b"rate" in L.flame_last_error()
+    assert L.flame_agg_reduce_argmeta(0, 8, blk, 512, 1, 1, 4, 80, 112, -1, None) == _native.FLAME_EINVAL

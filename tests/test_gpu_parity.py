@@ -1418,3 +1418,44 @@ def test_empty_and_tiny_keys_every_path():
     exp_top = O.OracleFedAvg().do({k: v.clone() for k, v in base.items()}, tc, total=2 * sum(counts))
     S.assert_bitwise("sync mid", S.to_cpu(mids[0]), exp_mid)
     S.assert_bitwise("sync top", S.to_cpu(top), exp_top)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64])
+def test_argmeta_launch_equals_device_table_launch(dtype):
+    """Small launches pass the metadata as a kernel argument (flame_agg_reduce_argmeta); the
+    result equals the device-table launch and the oracle, bitwise -- plain, INIT_FIRST and
+    per-segment rate rows (FLAME_AGG_SEG_RATES) -- and big tables still take the upload path."""
+    from flame_amd import engine
+    O = _oracle()
+    g = torch.Generator().manual_seed(93)
+    shapes = [(5000,), (3, 77), (1,), (0,), (2049,)]
+
+    def rnd(s, scale):
+        x = torch.randn(s, generator=g, dtype=torch.float64) * scale
+        return (x * 1000).to(dtype) if dtype == torch.int64 else x.to(dtype)
+    n = 7
+    base = [rnd(s, 1.0) for s in shapes]
+    cl = [[rnd(s, 1e-2) for _ in range(n)] for s in shapes]
+    rates = [(i + 2) / 37 for i in range(n)]
+    rows = [[(i + 1 + j) / 41 for i in range(n)] for j in range(len(shapes))]
+    results = {}
+    for argmeta in (True, False):
+        engine.ARGMETA = argmeta
+        try:
+            outs = [b.to(DEV) for b in base]
+            engine.reduce_(outs, outs, [[c.to(DEV) for c in row] for row in cl], rates)
+            first = [torch.empty(b.shape, dtype=dtype, device=DEV) for b in base]
+            engine.reduce_(first, None, [[c.to(DEV) for c in row] for row in cl], rates, init_first=True)
+            segr = [b.to(DEV) for b in base]
+            engine.reduce_(segr, segr, [[c.to(DEV) for c in row] for row in cl], None, seg_rates=rows)
+            torch.cuda.synchronize()
+            results[argmeta] = [[t.cpu() for t in ts] for ts in (outs, first, segr)]
+        finally:
+            engine.ARGMETA = True
+    for a, b in zip(results[True], results[False]):
+        for j, (x, y) in enumerate(zip(a, b)):
+            S.assert_bitwise(f"argmeta/{dtype}/{j}", {"x": x}, {"x": y})
+    for j, b in enumerate(base):
+        exp = b.clone()
+        O.reduce_tensor(exp, cl[j], rates)
+        S.assert_bitwise(f"oracle/{dtype}/{j}", {"x": results[True][0][j]}, {"x": exp})
