@@ -764,15 +764,14 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
 // and the top's FedAvg adds tmp(d_m, top_rates[m]) to the top weights (top_agg_in).
 template <int DT> __device__ __forceinline__ float rnd(float x);
 template <int DT, int CU, bool SYNC>
-__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
-                                                              int n_mids, int n_clients,
-                                                              const uint64_t* __restrict__ mid_w,
-                                                              const uint64_t* __restrict__ mid_delta,
-                                                              const uint64_t* __restrict__ clients,
-                                                              const float* __restrict__ mid_rates,
-                                                              const float* __restrict__ mid_goal,
-                                                              const float* __restrict__ top_rates, float top_goal,
-                                                              unsigned flags) {
+__device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __restrict__ segs, int n_segs,
+                                                  int n_mids, int n_clients, const uint64_t* __restrict__ mid_w,
+                                                  const uint64_t* __restrict__ mid_delta,
+                                                  const uint64_t* __restrict__ clients,
+                                                  const float* __restrict__ mid_rates,
+                                                  const float* __restrict__ mid_goal,
+                                                  const float* __restrict__ top_rates, float top_goal,
+                                                  unsigned flags) {
     using X = Tr<DT>;
     using S = SA<DT>;
     using T = typename X::T;
@@ -937,6 +936,35 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                 st1(gp, gw);
             }
         }
+}
+
+template <int DT, int CU, bool SYNC>
+__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
+                                                    int n_mids, int n_clients, const uint64_t* __restrict__ mid_w,
+                                                    const uint64_t* __restrict__ mid_delta,
+                                                    const uint64_t* __restrict__ clients,
+                                                    const float* __restrict__ mid_rates,
+                                                    const float* __restrict__ mid_goal,
+                                                    const float* __restrict__ top_rates, float top_goal,
+                                                    unsigned flags) {
+    hier_fedbuff_body<DT, CU, SYNC>(segs, n_segs, n_mids, n_clients, mid_w, mid_delta, clients, mid_rates, mid_goal,
+                                    top_rates, top_goal, flags);
+}
+
+// The same with the metadata block in the kernel arguments (small launches, e.g. a single
+// FedBuff aggregator's fused scale_add); word offsets into the block, -1 = no delta table.
+template <int DT, int CU, bool SYNC>
+__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel_argmeta(const ArgMeta meta, int n_segs, int n_mids, int n_clients,
+                                                            int o_mid_w, int o_mid_delta, int o_clients,
+                                                            int o_mid_rates, int o_mid_goal, int o_top_rates,
+                                                            float top_goal, unsigned flags) {
+    (void)sizeof(meta);     // read in place in the kernarg segment (see agg_reduce_kernel_argmeta)
+    const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    hier_fedbuff_body<DT, CU, SYNC>(reinterpret_cast<const flame_hier_segment*>(w), n_segs, n_mids, n_clients,
+                                    w + o_mid_w, o_mid_delta >= 0 ? w + o_mid_delta : nullptr, w + o_clients,
+                                    reinterpret_cast<const float*>(w + o_mid_rates),
+                                    reinterpret_cast<const float*>(w + o_mid_goal),
+                                    reinterpret_cast<const float*>(w + o_top_rates), top_goal, flags);
 }
 
 // ---------------------------------------------------------------- FedDyn server round
@@ -1325,6 +1353,53 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     return check_launch("flame_hier_fedbuff");
+}
+
+int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta, int64_t meta_bytes, int32_t n_segs,
+                               int64_t n_chunks, int32_t n_mids, int32_t n_clients, int64_t off_mid_w,
+                               int64_t off_mid_delta, int64_t off_clients, int64_t off_mid_rates,
+                               int64_t off_mid_goal, int64_t off_top_rates, float top_goal, void* stream) {
+    if (!host_meta || meta_bytes <= 0 || meta_bytes % 8 || meta_bytes > static_cast<int64_t>(sizeof(ArgMeta)))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff_argmeta: metadata block must be 8..%d bytes, a multiple of 8",
+                       static_cast<int>(sizeof(ArgMeta)));
+    if (n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is empty");
+    if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
+    if (n_mids < 1 || n_clients < 1) return set_err(FLAME_EINVAL, "flame_hier_fedbuff_argmeta: need >= 1 middle and >= 1 arrival per middle");
+    if (flags & ~(FLAME_HIER_TOP_ACCUM | FLAME_HIER_TOP_APPLY | FLAME_HIER_MID_READONLY | FLAME_HIER_SYNC))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff_argmeta: unknown flags 0x%x", flags);
+    if ((flags & FLAME_HIER_SYNC) && ((flags & FLAME_HIER_TOP_APPLY) || !(flags & FLAME_HIER_TOP_ACCUM)))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff_argmeta: FLAME_HIER_SYNC needs FLAME_HIER_TOP_ACCUM and no FLAME_HIER_TOP_APPLY");
+    if ((flags & FLAME_HIER_TOP_APPLY) && top_goal == 0.f) return set_err(FLAME_EINVAL, "top agg_goal must be nonzero");
+    auto inside = [&](int64_t off, int64_t bytes) { return off >= 0 && off % 8 == 0 && off + bytes <= meta_bytes; };
+    const int64_t S = n_segs, M = n_mids, C = n_clients;
+    if (S * static_cast<int64_t>(sizeof(flame_hier_segment)) > meta_bytes || !inside(off_mid_w, S * M * 8) ||
+        (off_mid_delta >= 0 && !inside(off_mid_delta, S * M * 8)) || !inside(off_clients, S * M * C * 8) ||
+        !inside(off_mid_rates, M * C * 4) || !inside(off_mid_goal, M * 4) || !inside(off_top_rates, M * 4))
+        return set_err(FLAME_EINVAL, "flame_hier_fedbuff_argmeta: a table lies outside the metadata block");
+    ArgMeta m;
+    std::memcpy(m.w, host_meta, static_cast<size_t>(meta_bytes));
+    const int ow = static_cast<int>(off_mid_w / 8), od = off_mid_delta >= 0 ? static_cast<int>(off_mid_delta / 8) : -1;
+    const int oc = static_cast<int>(off_clients / 8), orr = static_cast<int>(off_mid_rates / 8);
+    const int og = static_cast<int>(off_mid_goal / 8), ot = static_cast<int>(off_top_rates / 8);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const bool sync = (flags & FLAME_HIER_SYNC) != 0;
+#define FLAME_HIER_ARG_LAUNCH(DT, CUV)                                                                          \
+    if (sync)                                                                                                  \
+        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, true>), grid, block, FLAME_OCC_LDS, st, m, n_segs, \
+                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);                      \
+    else                                                                                                       \
+        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, false>), grid, block, FLAME_OCC_LDS, st, m, n_segs, \
+                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);
+    switch (dtype) {
+    case FLAME_F32: FLAME_HIER_ARG_LAUNCH(FLAME_F32, kClientUnroll) break;
+    case FLAME_BF16: FLAME_HIER_ARG_LAUNCH(FLAME_BF16, kHierUnroll16) break;
+    case FLAME_F16: FLAME_HIER_ARG_LAUNCH(FLAME_F16, kHierUnroll16) break;
+#undef FLAME_HIER_ARG_LAUNCH
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff_argmeta: dtype %d not supported (f32, bf16, f16)", dtype);
+    }
+    return check_launch("flame_hier_fedbuff_argmeta");
 }
 
 int flame_feddyn_round(int dtype, const flame_dyn_segment* segs, int32_t n_segs, int64_t n_chunks,

@@ -569,8 +569,6 @@ def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_
     ``sync``: the synchronous FedAvg hierarchy (FLAME_HIER_SYNC; needs ``top_accum``)."""
     L = N.lib()
     p = plan_hier(code, segs, mid_rates, mid_goals, top_rates)
-    dm = _staging.upload(p.meta, device)
-    b = dm.data_ptr()
     flags = ((N.FLAME_HIER_TOP_ACCUM if top_accum else 0) | (N.FLAME_HIER_TOP_APPLY if top_goal is not None else 0)
              | (N.FLAME_HIER_MID_READONLY if mid_readonly else 0) | (N.FLAME_HIER_SYNC if sync else 0))
     with_delta = any(s.mid_delta is not None for s in segs)
@@ -583,6 +581,17 @@ def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_
     top_out = any(s.top_out for s in segs)
     nbytes = isz * (P * (M * C + (M if with_delta else 0) + (1 if top_accum else 0) + (1 if top_out else 0)
                          + (2 if top_goal is not None else 0)) + wsum * (1 if mid_readonly else 2))
+    if ARGMETA and p.meta.nbytes <= argmeta_max_bytes():
+        # small launch (e.g. one FedBuff aggregator's fused scale_add): metadata as a kernel argument
+        o = p.offs
+        with _timed("flame_hier_fedbuff", device, nbytes):
+            N.check(L.flame_hier_fedbuff_argmeta(code, flags, p.meta.ctypes.data, p.meta.nbytes, p.n_segs, p.n_chunks,
+                                                 M, C, o["mid_w"], o["mid_delta"] if with_delta else -1, o["clients"],
+                                                 o["mid_rates"], o["mid_goal"], o["top_rates"], float(top_goal or 0),
+                                                 _stream_ptr(device)))
+        return
+    dm = _staging.upload(p.meta, device)
+    b = dm.data_ptr()
     with _timed("flame_hier_fedbuff", device, nbytes):
         N.check(L.flame_hier_fedbuff(code, flags, b + p.offs["segs"], p.n_segs, p.n_chunks, M, C,
                                      b + p.offs["mid_w"], b + p.offs["mid_delta"] if with_delta else None,

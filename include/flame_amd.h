@@ -263,6 +263,18 @@ int flame_feddyn_round(int dtype, const flame_dyn_segment *segs, int32_t n_segs,
                        const void *const *steps, const uint32_t *step_flags, int32_t n_steps,
                        int32_t n_phase1, double rate_avg, double rate_mean, void *stream);
 /*
+ * flame_hier_fedbuff for small launches: the metadata block (segments, then the mid_w,
+ * mid_delta, client, mid_rates, mid_goal and top_rates tables at the given byte offsets;
+ * off_mid_delta = -1 for none) is passed from HOST memory as a kernel argument instead of
+ * being copied to the device first.  meta_bytes <= flame_agg_argmeta_max_bytes().
+ */
+int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void *host_meta, int64_t meta_bytes,
+                               int32_t n_segs, int64_t n_chunks, int32_t n_mids, int32_t n_clients,
+                               int64_t off_mid_w, int64_t off_mid_delta, int64_t off_clients,
+                               int64_t off_mid_rates, int64_t off_mid_goal, int64_t off_top_rates,
+                               float top_goal, void *stream);
+
+/*
  * Host buffers the kernels read zero-copy over PCIe (ingest; flame_amd/ingest.py).
  *   flame_host_register:   page-lock + map an existing host range (e.g. a received
  *                          channel payload or the LIFL shared-memory segment,

@@ -112,3 +112,20 @@ def test_agg_reduce_argmeta_validates_without_gpu():
     assert L.flame_agg_reduce_argmeta(0, 0, blk, 512, 1, 1, 4, 80, -1, -1, None) == _native.FLAME_EINVAL
     assert b"rate" in L.flame_last_error()
     assert L.flame_agg_reduce_argmeta(0, 8, blk, 512, 1, 1, 4, 80, 112, -1, None) == _native.FLAME_EINVAL
+
+
+def test_hier_fedbuff_argmeta_validates_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    blk = (ctypes.c_uint64 * 64)()
+    # every call below is invalid, so nothing is ever launched (the pointers in blk are zeros)
+    args = [0, 0, blk, 512, 1, 1, 1, 2, 64, -1, 504, 88, 96, 104, 0.0, None]   # client table runs past 512 B
+    assert L.flame_hier_fedbuff_argmeta(*args) == _native.FLAME_EINVAL
+    assert b"outside" in L.flame_last_error()
+    bad = list(args)
+    bad[3] = 4096
+    assert L.flame_hier_fedbuff_argmeta(*bad) == _native.FLAME_EINVAL
+    bad = list(args)
+    bad[1] = 16
+    assert L.flame_hier_fedbuff_argmeta(*bad) == _native.FLAME_EINVAL
+    assert b"unknown flags" in L.flame_last_error()
