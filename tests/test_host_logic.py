@@ -278,3 +278,41 @@ def test_feddyn_program_merged_and_two_phase():
     T = engine.chunk_elems(N.FLAME_F32)
     assert n_chunks == -(-5000 // T) and offs["steps"] == 64 and offs["flags"] == 64 + 5 * 3 * 8
     assert list(meta[offs["flags"] // 8:].view(np.uint32)[:5]) == [f for f, _ in steps]
+
+
+def test_plan_chunk_map_property():
+    """Randomised: every non-empty segment owns ceil(numel/chunk) consecutive chunks, the
+    chunks tile [0, n_chunks) with no gap or overlap, and the tables sit where the offsets
+    say (full and compact blocks) -- the invariants the kernel's chunk -> segment lookup
+    and the C ABI's bounds checks rely on."""
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+
+    @hyp.settings(max_examples=200, deadline=None)
+    @hyp.given(numels=st.lists(st.integers(0, 5000), min_size=1, max_size=12),
+               n=st.integers(1, 9), code=st.sampled_from([N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16, N.FLAME_F64]),
+               compact=st.booleans())
+    def check(numels, n, code, compact):
+        segs = [engine.Seg(k, out=64 * (i + 1), inp=64 * (i + 1), clients=[4096 * (i * n + j + 1) for j in range(n)])
+                for i, k in enumerate(numels)]
+        rates = [1.0 / (j + 2) for j in range(n)]
+        p = engine.plan(code, segs, rates, compact=compact)
+        w = p.meta
+        chunk = engine.chunk_elems(code)
+        nxt = 0
+        for i, k in enumerate(numels):
+            assert w[i * N.SEGMENT_INT64S + 6] == k
+            assert w[i * N.SEGMENT_INT64S + 7] == nxt
+            nxt += -(-k // chunk)
+        assert p.n_chunks == max(nxt, 1)
+        tab = w[p.off_clients // 8:p.off_clients // 8 + len(segs) * n]
+        assert list(tab) == [c for s in segs for c in s.clients]
+        if compact:
+            assert (p.off_r32 == -1) == (code == N.FLAME_F64) and (p.off_r64 == -1) == (code != N.FLAME_F64)
+        off = p.off_r64 if p.off_r32 < 0 else p.off_r32
+        dt = np.float64 if p.off_r32 < 0 else np.float32
+        got = w.view(np.uint8)[off:off + n * np.dtype(dt).itemsize].view(dt)
+        assert list(got) == [dt(r) for r in rates]
+        assert off + n * np.dtype(dt).itemsize <= w.nbytes
+
+    check()
