@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import collections
 import enum
+import functools
 import pickle
 import struct
 import warnings
@@ -100,40 +101,55 @@ class PayloadDecoder:
         while True:
             op = mv[p]
             p += 1
-            if op == 0x80:      # PROTO
+            # opcodes in order of frequency in update payloads (MEMOIZE, BININT1, REDUCE, ... first)
+            if op == 0x94:    # MEMOIZE
+                memo[len(memo)] = stack[-1]
+            elif op == 0x4B:    # BININT1
+                stack.append(mv[p])
+                p += 1
+            elif op == 0x52:    # REDUCE
+                args = stack.pop()
+                fn = stack.pop()
+                stack.append(self._call(fn, args))
+            elif op == 0x68:    # BINGET
+                stack.append(memo[mv[p]])
+                p += 1
+            elif op == 0x8C:    # SHORT_BINUNICODE
+                n = mv[p]
+                stack.append(bytes(mv[p + 1:p + 1 + n]).decode("utf-8"))
+                p += 1 + n
+            elif op == 0x85:    # TUPLE1
+                stack[-1] = (stack[-1],)
+            elif op == 0x28:    # MARK
+                marks.append(len(stack))
+            elif op == 0x74:    # TUPLE
+                k = marks.pop()
+                stack[k:] = [tuple(stack[k:])]
+            elif op == 0x29:    # EMPTY_TUPLE
+                stack.append(())
+            elif op == 0x89:    # NEWFALSE
+                stack.append(False)
+            elif op == 0x80:      # PROTO
                 p += 1
             elif op == 0x95:    # FRAME
                 p += 8
             elif op == 0x2E:    # STOP
                 return stack.pop(), p
-            elif op == 0x28:    # MARK
-                marks.append(len(stack))
             elif op == 0x7D:    # EMPTY_DICT
                 stack.append({})
             elif op == 0x5D:    # EMPTY_LIST
                 stack.append([])
-            elif op == 0x29:    # EMPTY_TUPLE
-                stack.append(())
             elif op == 0x8F:    # EMPTY_SET
                 stack.append(set())
-            elif op == 0x94:    # MEMOIZE
-                memo[len(memo)] = stack[-1]
             elif op == 0x71:    # BINPUT
                 memo[mv[p]] = stack[-1]
                 p += 1
             elif op == 0x72:    # LONG_BINPUT
                 i, p = self._unpack("<I", p)
                 memo[i] = stack[-1]
-            elif op == 0x68:    # BINGET
-                stack.append(memo[mv[p]])
-                p += 1
             elif op == 0x6A:    # LONG_BINGET
                 i, p = self._unpack("<I", p)
                 stack.append(memo[i])
-            elif op == 0x8C:    # SHORT_BINUNICODE
-                n = mv[p]
-                stack.append(bytes(mv[p + 1:p + 1 + n]).decode("utf-8"))
-                p += 1 + n
             elif op == 0x58:    # BINUNICODE
                 n, p = self._unpack("<I", p)
                 stack.append(bytes(mv[p:p + n]).decode("utf-8"))
@@ -152,9 +168,6 @@ class PayloadDecoder:
                     n, p = self._unpack("<Q", p)
                 stack.append(_Span(p, n))
                 p += n
-            elif op == 0x4B:    # BININT1
-                stack.append(mv[p])
-                p += 1
             elif op == 0x4D:    # BININT2
                 v, p = self._unpack("<H", p)
                 stack.append(v)
@@ -172,17 +185,10 @@ class PayloadDecoder:
                 stack.append(None)
             elif op == 0x88:    # NEWTRUE
                 stack.append(True)
-            elif op == 0x89:    # NEWFALSE
-                stack.append(False)
-            elif op == 0x85:    # TUPLE1
-                stack[-1] = (stack[-1],)
             elif op == 0x86:    # TUPLE2
                 stack[-2:] = [tuple(stack[-2:])]
             elif op == 0x87:    # TUPLE3
                 stack[-3:] = [tuple(stack[-3:])]
-            elif op == 0x74:    # TUPLE
-                k = marks.pop()
-                stack[k:] = [tuple(stack[k:])]
             elif op == 0x6C:    # LIST
                 k = marks.pop()
                 stack[k:] = [list(stack[k:])]
@@ -221,10 +227,6 @@ class PayloadDecoder:
                 name = bytes(mv[p + e1 + 1:p + e1 + 1 + e2]).decode()
                 p += e1 + e2 + 2
                 stack.append(self._find(module, name))
-            elif op == 0x52:    # REDUCE
-                args = stack.pop()
-                fn = stack.pop()
-                stack.append(self._call(fn, args))
             elif op == 0x81:    # NEWOBJ
                 args = stack.pop()
                 cls = stack.pop()
@@ -263,11 +265,20 @@ class PayloadDecoder:
         if not isinstance(span, _Span):
             raise pickle.UnpicklingError("storage bytes expected")
         q = span.start
-        magic, q = self.load(q)
-        if magic != LEGACY_MAGIC:
-            raise pickle.UnpicklingError("not a legacy torch storage stream")
-        _proto, q = self.load(q)
-        _sysinfo, q = self.load(q)
+        # magic, protocol and sys-info pickles: the same bytes before every storage of a
+        # payload, so a header already parsed and checked is skipped by a byte compare
+        for h in _STORAGE_HEADERS:
+            if self.mv[q:q + len(h)] == h:
+                q += len(h)
+                break
+        else:
+            magic, q = self.load(q)
+            if magic != LEGACY_MAGIC:
+                raise pickle.UnpicklingError("not a legacy torch storage stream")
+            _proto, q = self.load(q)
+            _sysinfo, q = self.load(q)
+            if len(_STORAGE_HEADERS) < 8:
+                _STORAGE_HEADERS.append(bytes(self.mv[span.start:q]))
         found = []
 
         def pload(pid):
@@ -289,6 +300,9 @@ class PayloadDecoder:
         if q + nbytes > span.start + span.n:
             raise pickle.UnpicklingError("storage runs past its bytes")
         return _StorageRef(self.buf, q, numel, obj.dtype)
+
+
+_STORAGE_HEADERS = []   # validated legacy-stream headers (bytes)
 
 
 class _Span:
@@ -315,6 +329,7 @@ def _allow(fn):
 _CALLABLE_ALLOW = set()
 
 
+@functools.lru_cache(maxsize=None)   # built once: the flame import probe is not free
 def _default_globals():
     g = {
         ("torch._utils", "_rebuild_tensor_v2"): _allow(_rebuild_tensor_v2),
