@@ -6,7 +6,7 @@ the cache object lives across rounds, as the role's ``self.cache`` does), FedAvg
 ``do()`` issue and the wait for the GPU; medians over 25 warm rounds.  Also times
 the reference's ``cloudpickle.loads`` of the same two payloads.
 
-    python tools/c1_latency.py
+    python tools/c1_latency.py [--profile]
 """
 import os
 import statistics
@@ -63,6 +63,24 @@ def main():
     for _ in range(10):
         [cloudpickle.loads(p) for p in pls]
     print(f"reference cloudpickle.loads of the 2 payloads: {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
+    if "--profile" in sys.argv:     # where do()'s host time goes (HBM placement)
+        import cProfile
+        import pstats
+        cache = ingest.DeviceUpdateCache(device=dev, placement="hbm", capacity=4)
+        msgs = [ingest.decode(p) for p in pls]
+
+        def rounds(n):
+            for _ in range(n):
+                for i, m in enumerate(msgs):
+                    cache[f"t{i}"] = TrainResult(m["weights"], 2000)
+                opt.do(deepcopy(w), cache, total=4000)
+            torch.cuda.synchronize()
+        rounds(5)
+        pr = cProfile.Profile()
+        pr.enable()
+        rounds(200)
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(18)
 
 
 if __name__ == "__main__":
