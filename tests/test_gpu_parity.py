@@ -1459,3 +1459,52 @@ def test_argmeta_launch_equals_device_table_launch(dtype):
         exp = b.clone()
         O.reduce_tensor(exp, cl[j], rates)
         S.assert_bitwise(f"oracle/{dtype}/{j}", {"x": results[True][0][j]}, {"x": exp})
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_many_clients_one_launch(dtype):
+    """The largest flat reduction the BASELINE configs imply: all 4096 clients of config 5
+    (+1, an odd count) in ONE FedAvg launch over three keys (ragged sizes, one empty),
+    read from a tiled slab -- bitwise vs the oracle; and 4096 FedBuff arrivals queued then
+    read once (one launch) equal the oracle's per-arrival sequence."""
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    n = 4097
+    shapes = {"a": (3000,), "b": (7,), "c": (0,)}
+    g = torch.Generator().manual_seed(4097)
+    base = {k: torch.randn(s, generator=g, dtype=torch.float64).to(dtype) for k, s in shapes.items()}
+    cl = [{k: (torch.randn(s, generator=g, dtype=torch.float64) * 1e-2).to(dtype) for k, s in shapes.items()}
+          for _ in range(n)]
+    counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+    total = sum(counts)
+    exp = {k: v.clone() for k, v in base.items()}
+    for k in shapes:
+        O.reduce_tensor(exp[k], [c[k] for c in cl], [c / total for c in counts])
+    slab = UpdateSlab(base, capacity=n, device=DEV)
+    cache = S.SortedCache()
+    for i, (c, k) in enumerate(zip(cl, counts)):
+        cache[f"{i:05d}"] = S.TR(slab.put({kk: v.to(DEV) for kk, v in c.items()}), k)
+    from flame_amd import engine
+    engine.kernel_events = []
+    try:
+        out = make_amd("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache, total=total)
+        assert len(engine.kernel_events) == 1, [e[0] for e in engine.kernel_events]
+    finally:
+        engine.kernel_events = None
+    S.assert_bitwise(f"fedavg {n} clients {dtype}", out, exp)
+    del slab, cache
+    # FedBuff: 4096 queued arrivals, staleness 0..3, into an existing aggregate
+    m = 4096
+    vers = torch.randint(0, 4, (m,), generator=g).tolist()
+    agg0 = {k: (torch.randn(s, generator=g, dtype=torch.float64) * 1e-2).to(dtype) for k, s in shapes.items()}
+    exp = {k: v.clone() for k, v in agg0.items()}
+    rates = [1 / math.sqrt(1 + 3 - v) for v in vers]
+    for k in shapes:
+        O.reduce_tensor(exp[k], [c[k] for c in cl[:m]], rates)
+    opt = make_amd("fedbuff")
+    agg = {k: v.to(DEV) for k, v in agg0.items()}
+    for i in range(m):
+        cache = S.SortedCache()
+        cache[f"{i:05d}"] = S.TR({k: v.to(DEV) for k, v in cl[i].items()}, 1, vers[i])
+        agg = opt.do(agg, cache, total=1, version=3)
+    S.assert_bitwise(f"fedbuff {m} arrivals {dtype}", {k: agg[k] for k in shapes}, exp)
