@@ -316,3 +316,46 @@ def test_plan_chunk_map_property():
         assert off + n * np.dtype(dt).itemsize <= w.nbytes
 
     check()
+
+
+def test_plan_hier_property():
+    """Randomised flame_hier_fedbuff metadata: the seven tables follow one another with no
+    gap, each at its recorded offset and of its [S][M] / [S][M*C] / [M*C] / [M] size, and
+    the chunks tile [0, n_chunks) segment by segment."""
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+
+    @hyp.settings(max_examples=150, deadline=None)
+    @hyp.given(numels=st.lists(st.integers(0, 9000), min_size=1, max_size=6), M=st.integers(1, 5),
+               C=st.integers(1, 6), delta=st.booleans(), code=st.sampled_from([N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16]))
+    def check(numels, M, C, delta, code):
+        segs = [engine.HierSeg(k, mid_w=[256 * (i * M + m + 1) for m in range(M)],
+                               clients=[1 << 20 | 256 * (i * M * C + j) for j in range(M * C)],
+                               mid_delta=[1 << 24 | 256 * (i * M + m) for m in range(M)] if delta else None,
+                               top_out=1 << 28 | 256 * i)
+                for i, k in enumerate(numels)]
+        rates = [[1.0 / (m + c + 2) for c in range(C)] for m in range(M)]
+        goals = list(range(2, M + 2))
+        tops = [1.0 / (m + 1) for m in range(M)]
+        p = engine.plan_hier(code, segs, rates, goals, tops)
+        S, o, w = len(segs), p.offs, p.meta
+        sizes = {"segs": S * engine.HSEG_WORDS * 8, "mid_w": S * M * 8, "mid_delta": S * M * 8,
+                 "clients": S * M * C * 8, "mid_rates": -(-M * C // 2) * 8, "mid_goal": -(-M // 2) * 8,
+                 "top_rates": -(-M // 2) * 8}
+        at = 0
+        for nm in ["segs", "mid_w", "mid_delta", "clients", "mid_rates", "mid_goal", "top_rates"]:
+            assert o[nm] == at, nm
+            at += sizes[nm]
+        assert at == w.nbytes
+        assert list(w[o["clients"] // 8:o["clients"] // 8 + S * M * C]) == [c for s in segs for c in s.clients]
+        dt = list(w[o["mid_delta"] // 8:o["mid_delta"] // 8 + S * M])
+        assert dt == ([d for s in segs for d in s.mid_delta] if delta else [0] * (S * M))
+        f = w.view(np.float32)
+        assert list(f[o["mid_goal"] // 4:o["mid_goal"] // 4 + M]) == [float(g) for g in goals]
+        chunk, nxt = engine.chunk_elems(code), 0
+        for i, k in enumerate(numels):
+            assert w[i * engine.HSEG_WORDS + 3] == k and w[i * engine.HSEG_WORDS + 4] == nxt
+            nxt += -(-k // chunk)
+        assert p.n_chunks == max(nxt, 1) and (p.n_mids, p.n_clients, p.n_segs) == (M, C, S)
+
+    check()
