@@ -363,16 +363,18 @@ def _launch_reduce(code, segs, rates, device, keep, *, init_first=False, seg_rat
     flags = N.FLAME_AGG_INIT_FIRST if init_first else 0
     if seg_rates:
         flags |= N.FLAME_AGG_SEG_RATES
-    nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (_n_clients(rates, seg_rates) + (1 if init_first else 2))
-    if ARGMETA:
+    n_cl = _n_clients(rates, seg_rates)
+    nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (n_cl + (1 if init_first else 2))
+    est = compact_meta_bytes(code, len(segs), n_cl, seg_rates)
+    if ARGMETA and est <= argmeta_max_bytes():
         # small launch: the metadata block goes with the dispatch as a kernel argument (no H2D blit)
         p = plan(code, segs, rates, seg_rates=seg_rates, compact=True)
-        if p.meta.nbytes <= argmeta_max_bytes():
-            with _timed("flame_agg_reduce", device, nbytes):
-                N.check(L.flame_agg_reduce_argmeta(code, flags, p.meta.ctypes.data, p.meta.nbytes, p.n_segs,
-                                                   p.n_chunks, p.n_clients, p.off_clients, p.off_r32, p.off_r64,
-                                                   _stream_ptr(device)))
-            return
+        assert p.meta.nbytes == est
+        with _timed("flame_agg_reduce", device, nbytes):
+            N.check(L.flame_agg_reduce_argmeta(code, flags, p.meta.ctypes.data, p.meta.nbytes, p.n_segs,
+                                               p.n_chunks, p.n_clients, p.off_clients, p.off_r32, p.off_r64,
+                                               _stream_ptr(device)))
+        return
     p = plan(code, segs, rates, seg_rates=seg_rates)
     dm = _staging.upload(p.meta, device)
     segp, clp, r32p, r64p = _device_ptrs(dm, p)
@@ -392,6 +394,13 @@ def argmeta_max_bytes() -> int:
     if _ARGMETA_MAX is None:
         _ARGMETA_MAX = int(N.lib().flame_agg_argmeta_max_bytes())
     return _ARGMETA_MAX
+
+
+def compact_meta_bytes(code: int, n_segs: int, n_clients: int, seg_rates: bool = False) -> int:
+    """Size of ``plan(..., compact=True)``'s block without building it: segments, client
+    table and the one rate array the dtype reads (fp32 rates padded to 8 bytes)."""
+    n_rates = (n_segs if seg_rates else 1) * n_clients
+    return n_segs * (SEG_WORDS + n_clients) * 8 + (n_rates * 8 if code == N.FLAME_F64 else -(-n_rates // 2) * 8)
 
 
 def _n_clients(rates, seg_rates) -> int:

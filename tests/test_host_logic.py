@@ -359,3 +359,15 @@ def test_plan_hier_property():
         assert p.n_chunks == max(nxt, 1) and (p.n_mids, p.n_clients, p.n_segs) == (M, C, S)
 
     check()
+
+
+def test_compact_block_size_prediction():
+    """engine._launch_reduce decides kernel-argument vs uploaded metadata from the compact
+    block's size before building it; the prediction must equal the built size."""
+    import itertools
+    for code, S_, n, seg_rates in itertools.product([N.FLAME_F32, N.FLAME_BF16, N.FLAME_F64, N.FLAME_I64],
+                                                    [1, 2, 5], [0, 1, 2, 3, 255, 256], [False, True]):
+        segs = [engine.Seg(100, out=64, inp=64, clients=[4096] * n) for _ in range(S_)]
+        rates = [[0.5] * n for _ in range(S_)] if seg_rates else [0.5] * n
+        p = engine.plan(code, segs, rates, seg_rates=seg_rates, compact=True)
+        assert p.meta.nbytes == engine.compact_meta_bytes(code, S_, n, seg_rates), (code, S_, n, seg_rates)
