@@ -576,10 +576,10 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
 }
 
 template <int DT, int VARIANT, int CU>
-__global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __restrict__ segs, int n_segs,
-                                                        const uint64_t* __restrict__ clients, int n_clients,
-                                                        const float* __restrict__ r32, unsigned flags, float b1,
-                                                        float omb1, float b2, float omb2, float eta, float tau) {
+__device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ segs, int n_segs,
+                                            const uint64_t* __restrict__ clients, int n_clients,
+                                            const float* __restrict__ r32, unsigned flags, float b1,
+                                            float omb1, float b2, float omb2, float eta, float tau) {
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
@@ -668,6 +668,28 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
                 st1(cop + o, X::st(cj));
             }
     }
+}
+
+template <int DT, int VARIANT, int CU>
+__global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                        const uint64_t* __restrict__ clients, int n_clients,
+                                                        const float* __restrict__ r32, unsigned flags, float b1,
+                                                        float omb1, float b2, float omb2, float eta, float tau) {
+    fedopt_body<DT, VARIANT, CU>(segs, n_segs, clients, n_clients, r32, flags, b1, omb1, b2, omb2, eta, tau);
+}
+
+// The same with the metadata block as a kernel argument, read in place (flame_fedopt_reduce_adapt_argmeta;
+// see agg_reduce_kernel_argmeta).  Word offsets: client table at off_clients, fp32 rates at off_r32.
+template <int DT, int VARIANT, int CU>
+__global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta meta, int n_segs, int n_clients,
+                                                                int off_clients, int off_r32, unsigned flags,
+                                                                float b1, float omb1, float b2, float omb2,
+                                                                float eta, float tau) {
+    (void)sizeof(meta);
+    const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    fedopt_body<DT, VARIANT, CU>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
+                                 off_r32 >= 0 ? reinterpret_cast<const float*>(w + off_r32) : nullptr, flags,
+                                 b1, omb1, b2, omb2, eta, tau);
 }
 
 // ---------------------------------------------------------------- FedBuff scale-add (+delta)
@@ -1294,6 +1316,57 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
     }
 #undef FLAME_OPT_LAUNCH
     return check_launch("flame_fedopt_reduce_adapt");
+}
+
+int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, const void* host_meta,
+                                      int64_t meta_bytes, int32_t n_segs, int64_t n_chunks, int32_t n_clients,
+                                      int64_t off_clients, int64_t off_r32, float b1, float omb1, float b2,
+                                      float omb2, float eta, float tau, void* stream) {
+    if (!host_meta || meta_bytes <= 0 || meta_bytes % 8 || meta_bytes > static_cast<int64_t>(sizeof(ArgMeta)))
+        return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: metadata block must be 8..%d bytes, a multiple of 8",
+                       static_cast<int>(sizeof(ArgMeta)));
+    if (n_segs <= 0 || n_clients < 0)
+        return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: n_segs <= 0 or n_clients < 0");
+    if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
+    if (flags & ~FLAME_OPT_STATE_ZERO)
+        return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: unknown flags 0x%x", flags);
+    if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt_argmeta: unknown variant %d", variant);
+    auto inside = [&](int64_t off, int64_t bytes) { return off >= 0 && off % 8 == 0 && off + bytes <= meta_bytes; };
+    if (static_cast<int64_t>(n_segs) * static_cast<int64_t>(sizeof(flame_segment)) > meta_bytes ||
+        !inside(off_clients, static_cast<int64_t>(n_segs) * n_clients * 8) ||
+        (n_clients > 0 && !inside(off_r32, static_cast<int64_t>(n_clients) * 4)))
+        return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: a table lies outside the metadata block");
+    ArgMeta m;
+    std::memcpy(m.w, host_meta, static_cast<size_t>(meta_bytes));
+    const int oc = static_cast<int>(off_clients / 8);
+    const int o32 = n_clients > 0 ? static_cast<int>(off_r32 / 8) : -1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+#define FLAME_OPT_ARGMETA_LAUNCH(DT, CUV)                                                                        \
+    switch (variant) {                                                                                           \
+    case FLAME_FEDADAM:                                                                                          \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAM, CUV>), grid, block, 0, st, m, n_segs,        \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
+        break;                                                                                                   \
+    case FLAME_FEDYOGI:                                                                                          \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDYOGI, CUV>), grid, block, 0, st, m, n_segs,        \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
+        break;                                                                                                   \
+    default:                                                                                                     \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAGRAD, CUV>), grid, block, 0, st, m, n_segs,     \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
+        break;                                                                                                   \
+    }
+    switch (dtype) {
+    case FLAME_F32: FLAME_OPT_ARGMETA_LAUNCH(FLAME_F32, kClientUnroll) break;
+    case FLAME_BF16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_BF16, kClientUnroll16) break;
+    case FLAME_F16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_F16, kClientUnroll16) break;
+    default:
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt_argmeta: dtype %d not supported (f32, bf16, f16)", dtype);
+    }
+#undef FLAME_OPT_ARGMETA_LAUNCH
+    return check_launch("flame_fedopt_reduce_adapt_argmeta");
 }
 
 int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int64_t goal,

@@ -432,16 +432,27 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
             segs.append(Seg(base[s_].numel(), out=avg_out[s_].data_ptr() if avg_out[s_] is not None else 0,
                             inp=base[s_].data_ptr(), cur=cur[s_].data_ptr(), cur_out=cur_out[s_].data_ptr(),
                             m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row, tile_stride=tstride))
-        p = plan(code, segs, rates)
-        dm = _staging.upload(p.meta, device)
-        segp, clp, r32p, _ = _device_ptrs(dm, p)
         P = sum(sg.numel for sg in segs)
         isz = ITEMSIZE[code]
         # clients + base + cur (+ m, v unless zero state) read; avg, m, v, cur_out written
-        nbytes = isz * P * (p.n_clients + 2 + (0 if state_zero else 2) + 4)
+        nbytes = isz * P * (len(rates) + 2 + (0 if state_zero else 2) + 4)
         h = list(hyper)
         if code in (N.FLAME_BF16, N.FLAME_F16):  # torch-CPU rounds the scalar of `sqrt(v) + tau`
             h[5] = float(torch.tensor(float(h[5]), dtype=base[idx[0]].dtype))
+        opt_flags = N.FLAME_OPT_STATE_ZERO if state_zero else 0
+        if ARGMETA and compact_meta_bytes(code, len(segs), len(rates)) <= argmeta_max_bytes():
+            # small round: the metadata block rides in the kernel arguments (no H2D blit)
+            p = plan(code, segs, rates, compact=True)
+            with _timed("flame_fedopt_reduce_adapt", device, nbytes):
+                N.check(L.flame_fedopt_reduce_adapt_argmeta(code, FEDOPT_VARIANT[variant], opt_flags,
+                                                            p.meta.ctypes.data, p.meta.nbytes, p.n_segs,
+                                                            p.n_chunks, p.n_clients, p.off_clients, p.off_r32,
+                                                            *[float(x) for x in h], _stream_ptr(device)))
+            _keepalive(keep, device)
+            continue
+        p = plan(code, segs, rates)
+        dm = _staging.upload(p.meta, device)
+        segp, clp, r32p, _ = _device_ptrs(dm, p)
         with _timed("flame_fedopt_reduce_adapt", device, nbytes):
             N.check(L.flame_fedopt_reduce_adapt(code, FEDOPT_VARIANT[variant],
                                                 N.FLAME_OPT_STATE_ZERO if state_zero else 0,

@@ -167,6 +167,20 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
                               float b2, float omb2, float eta, float tau, void *stream);
 
 /*
+ * flame_fedopt_reduce_adapt with its metadata block (segments, then the [n_segs][n_clients]
+ * client table at byte offset off_clients, then the fp32 rates at off_r32; at most
+ * flame_agg_argmeta_max_bytes() bytes, host memory) passed as a kernel argument: no
+ * device table and no H2D copy before the launch.  Small rounds only (e.g. flame's MNIST
+ * model x a few trainers).  Replaces the same reference code as flame_fedopt_reduce_adapt
+ * (optimizer/fedopt.py:80-90,102-129).  FLAME_EINVAL if a table lies outside the block.
+ */
+int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, const void *host_meta,
+                                      int64_t meta_bytes, int32_t n_segs, int64_t n_chunks,
+                                      int32_t n_clients, int64_t off_clients, int64_t off_r32,
+                                      float b1, float omb1, float b2, float omb2, float eta,
+                                      float tau, void *stream);
+
+/*
  * FedBuff scale-add: out[e] = round(out[e] + round(in[e] / goal)); if seg.cur_out
  * is non-NULL also cur_out[e] = round(new - old) (the middle aggregator's delta).
  * Float dtypes only (the reference raises for integer tensors).

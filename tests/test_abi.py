@@ -129,3 +129,17 @@ def test_hier_fedbuff_argmeta_validates_without_gpu():
     bad[1] = 16
     assert L.flame_hier_fedbuff_argmeta(*bad) == _native.FLAME_EINVAL
     assert b"unknown flags" in L.flame_last_error()
+
+
+def test_fedopt_argmeta_validates_without_gpu():
+    from flame_amd import _native
+    L = _native.lib()
+    blk = (ctypes.c_uint64 * 64)()
+    hyper = [0.9, 0.1, 0.99, 0.01, 0.01, 0.001]
+    # every call below is invalid, so nothing is ever launched (the pointers in blk are zeros)
+    assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 0, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
+    assert b"outside" in L.flame_last_error()
+    assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 0, blk, 4096, 1, 1, 2, 80, 96, *hyper, None) == _native.FLAME_EINVAL
+    assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 2, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
+    assert b"unknown flags" in L.flame_last_error()
+    assert L.flame_fedopt_reduce_adapt_argmeta(0, 7, 0, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_ENOTSUP

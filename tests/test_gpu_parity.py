@@ -1508,3 +1508,36 @@ def test_many_clients_one_launch(dtype):
         cache[f"{i:05d}"] = S.TR({k: v.to(DEV) for k, v in cl[i].items()}, 1, vers[i])
         agg = opt.do(agg, cache, total=1, version=3)
     S.assert_bitwise(f"fedbuff {m} arrivals {dtype}", {k: agg[k] for k in shapes}, exp)
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fedopt_argmeta_equals_device_table(sort, dtype):
+    """Small FedOPT rounds pass their metadata as a kernel argument
+    (flame_fedopt_reduce_adapt_argmeta): three rounds (passthrough, zero state, running
+    state) equal the device-table launches bitwise."""
+    from flame_amd import engine
+    g = torch.Generator().manual_seed(17)
+    shapes = {"w": (300, 7), "b": (7,), "e": (0,), "t": (4099,)}
+    w0 = {k: torch.randn(s, generator=g, dtype=torch.float64).to(dtype) for k, s in shapes.items()}
+    rounds = [[({k: (w0[k].double() + torch.randn(s, generator=g, dtype=torch.float64) * 1e-2).to(dtype)
+                 for k, s in shapes.items()}, int(c)) for c in torch.randint(1, 500, (5,), generator=g)]
+              for _ in range(3)]
+    results = {}
+    for argmeta in (True, False):
+        engine.ARGMETA = argmeta
+        try:
+            opt = make_amd(sort)
+            w = {k: v.to(DEV) for k, v in w0.items()}
+            outs = []
+            for arrivals in rounds:
+                cache = S.SortedCache()
+                for i, (u, c) in enumerate(arrivals):
+                    cache[f"{i:03d}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, c)
+                w = opt.do({k: v.clone() for k, v in w.items()}, cache, total=sum(c for _, c in arrivals))
+                outs.append({k: v.cpu() for k, v in w.items()})
+            results[argmeta] = outs
+        finally:
+            engine.ARGMETA = True
+    for r, (a, b) in enumerate(zip(results[True], results[False])):
+        S.assert_bitwise(f"{sort}/{dtype}/round{r}", a, b)
