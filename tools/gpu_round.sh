@@ -28,5 +28,6 @@ if [ -n "${PROF:-}" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
       python bench.py --cpu-clients 0 --steps 10 --warmup 2 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 $OUT/prof.log
+  rm -f $OUT/prof/run_kernel_trace.csv   # tens of MB; the stats file is what gets committed
 fi
 exit 0
