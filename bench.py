@@ -7,21 +7,23 @@ per step / step time, summed over ranks.  Default workload = config 3: FedAvg of
 one ``FedAvg.do(base, cache, total=...)`` through flame's optimizer API (cache
 refill + iterkeys/pop drain + segment-table upload + one flame_agg_reduce launch).
 
-Multi-GPU (torchrun, one process per GPU, RCCL): the parameter vector is sharded;
-each rank owns a 25M-param slice of a (25M x world)-param model and reduces all
-1024 clients over it (weak scaling: per-GPU work fixed); the RCCL all-gather that
-reassembles the global model on every rank runs inside the timed step, pipelined
-behind the reduction (flame_amd.shard.ShardedSliceFedAvg).
+Multi-GPU (torchrun, one process per GPU, RCCL): the product's
+flame_amd.shard.ShardedOptimizer(FedAvg) over a (25M x world)-param model -- each
+rank owns 25M of its elements and holds only its slices of the 1024 client updates
+(a rank-local tiled slab, as DeviceUpdateCache(shard=plan) writes it), reduces them
+in three waves and all-gathers every wave in place over RCCL while the next wave is
+reduced (weak scaling: per-GPU work fixed; the gathers are inside the timed step).
 
 Other workloads (DESIGN.md numbers; the driver's bench line is the default):
   --workload fedadam|fedyogi|fedadagrad   config 4 (fused FedOPT kernel, round >= 2)
-  --workload hier_fedbuff                 config 5, one GPU's parameter shard
-                                          (4096 clients = 64 middles x 64, bf16;
-                                          --hier-mode group batches the co-located
-                                          middles: 4 launches per step instead of 130)
+  --workload hier_fedbuff                 config 5: 4096 clients = 64 middles x 64, bf16,
+                                          one GPU's 15.6M-param shard at N=1; at N>1 the
+                                          product's ShardedHierarchy over a (15.6M x N)-param
+                                          model with the top model all-gathered over RCCL
   --e2e                                   host-resident updates: H2D + kernel + D2H
 """
 import argparse
+import collections
 import json
 import os
 import statistics
@@ -125,8 +127,38 @@ def barrier(world):
         dist.barrier()
 
 
+def host_cores():
+    """The host cores this process may use, with the figures they come from (SURVEY.md
+    §8(d): state the core count).  A GPU box pins a job to a CPU share: the affinity mask
+    and the cgroup quota bound it; os.cpu_count() is the whole machine."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except Exception:  # noqa: BLE001
+        pass
+    use = min(aff, quota) if quota else aff
+    return use, {"os_cpu_count": os.cpu_count(), "sched_getaffinity": aff, "cgroup_cpu_quota": quota,
+                 "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "threads_used": use, "cpu_model": _cpu_model()}
+
+
 def cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
-    """The reference's op sequence (oracle/torch_cpu.py) on host cores, bounded sample."""
+    """The reference's op sequence (oracle/torch_cpu.py) on host cores, bounded sample,
+    with torch's intra-op pool set to the cores this process may use (host_cores)."""
+    cores, env = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        res = _cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds)
+    finally:
+        torch.set_num_threads(prev)
+    res["host"] = env
+    return res
+
+
+def _cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
     from oracle import torch_cpu
     n_cpu = min(n_cpu, n)
     ups = [{"model": host_row(i)} for i in range(n_cpu)]
@@ -158,7 +190,10 @@ def cpu_baseline(host_row, n, P, base0, counts, n_cpu, rounds):
         "value": n_cpu * P / t, "unit": "client-params/s", "cores": threads, "kind": "port",
         "sample": f"reference FedAvg op sequence (fedavg.py:84-104, torch CPU, oracle/torch_cpu.py) over "
                   f"{n_cpu} of the same synthetic clients x {P} fp32 params, median of {rounds} rounds "
-                  f"({t:.3f} s/round), {threads} threads on {model}; diskcache I/O excluded",
+                  f"({t:.3f} s/round), {threads} threads on {model}; diskcache I/O excluded.  value = sampled "
+                  f"client-params / round time: the op sequence costs the same per client, so this is the "
+                  f"{n}-client rate extrapolated per-client-linearly ({n} clients would take "
+                  f"{t * n / n_cpu:.1f} s)",
         "single_thread": {"value": n1 * P / t1, "cores": 1,
                           "sample": f"{n1} clients x {P}, median of {rounds} rounds ({t1:.3f} s/round)"},
     }
@@ -400,6 +435,8 @@ def main():
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
         return bench_e2e(args, n, P, dev)
+    if (world > 1 or args.force_shard) and args.workload in ("fedavg", "fedadam", "fedyogi", "fedadagrad"):
+        return bench_sharded(args, world, rank, dev, n, P)
     client_w, slab_buf, host_row = make_clients(args, n, P, rank, dev)
     base = torch.empty(P, dtype=torch.float32, device=dev)
     engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
@@ -411,11 +448,10 @@ def main():
     keys = [f"{i:05d}" for i in range(n)]
     torch.cuda.synchronize()
 
-    if (world > 1 or args.force_shard) and args.workload == "fedavg":
-        from flame_amd.shard import ShardedSliceFedAvg
-        opt = ShardedSliceFedAvg(fracs=(1.0,) if args.no_overlap else (0.75, 0.20, 0.05))
-    else:
-        opt = optimizer_provider.get(args.workload)
+    if world > 1:
+        raise SystemExit(f"--workload {args.workload} has no multi-GPU bench (its drop-in shards via "
+                         f"flame_amd.shard.ShardedOptimizer; see tests/test_shard_gloo.py)")
+    opt = optimizer_provider.get(args.workload)
     state = {"weights": {"model": base}}
 
     def received():
@@ -435,14 +471,6 @@ def main():
         else:  # FedOPT caller convention: weights = do(deepcopy(weights), ...)
             state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=total,
                                       num_trainers=n)
-        if world > 1 and args.workload != "fedavg":
-            import torch.distributed as dist
-            if dist.get_backend() == "gloo":
-                out = torch.empty(P * world, dtype=torch.float32)
-                dist.all_gather_into_tensor(out, state["weights"]["model"].cpu())
-            else:
-                out = torch.empty(P * world, dtype=torch.float32, device=dev)
-                dist.all_gather_into_tensor(out, state["weights"]["model"])
 
     if args.workload != "fedavg":
         step()  # FedOPT round 1 is a passthrough (fedopt.py:87-88); time adaptive rounds only
@@ -515,6 +543,185 @@ def main():
         dist.destroy_process_group()
 
 
+def _local_slab(plan, n, dev, seed, sigma):
+    """n synthetic client updates holding only this rank's slices of the (global) model: a
+    tiled slab over the plan's local names, as DeviceUpdateCache(shard=plan) writes it.  The
+    counter generator is indexed by GLOBAL element, so every rank holds slices of one model."""
+    from flame_amd import engine
+    from flame_amd.slab import UpdateSlab
+    store = UpdateSlab(plan.local_template(), capacity=n, device=dev)
+    tmp = {nm: torch.empty(plan.local_numel[nm], dtype=plan.dtypes[plan.by_name[nm].key], device=dev)
+           for nm in plan.names}
+    ws = []
+    for i in range(n):
+        for sub in plan.subs:
+            engine.synth_fill_(tmp[sub.name], seed, 1 + i, sub.lo, sigma)
+        ws.append(store.put(tmp))
+    return store, ws
+
+
+def _collective_note(plan, world, itemsize):
+    recv = sum((s.g1 - s.g0) - (s.hi - s.lo) for s in plan.subs if not s.tail) * itemsize
+    return {"kind": "in-place all_gather_into_tensor per wave (RCCL over xGMI)" if world > 1 else "none (world 1)",
+            "waves": plan.n_waves, "bytes_received_per_rank": recv,
+            "replicated_tail_elements": sum(s.hi - s.lo for s in plan.subs if s.tail)}
+
+
+def bench_sharded(args, world, rank, dev, n, P):
+    """Configs 3/4 at N GPUs through the product's ShardedOptimizer: weak scaling -- the
+    model has P x world params; each rank owns P of them (plus the replicated key tails)
+    and holds only its slices of the n client updates; every step = one FedAvg.do (or
+    FedOPT adaptive round) on the full model dict, three waves of reductions with their
+    in-place RCCL all-gathers overlapped behind the next wave."""
+    from flame_amd import engine, shard, synth
+    from flame_amd.optimizers import optimizer_provider
+    G = P * world
+    opt = shard.ShardedOptimizer(optimizer_provider.get(args.workload), device=dev,
+                                 fracs=(1.0,) if args.no_overlap else shard.DEFAULT_FRACS)
+    opt.set_layout({"model": torch.empty(G, dtype=torch.float32, device="meta")})
+    plan = opt.plan
+    store, client_w = _local_slab(plan, n, dev, args.seed, 1e-2)
+    base = torch.empty(G, dtype=torch.float32, device=dev)
+    engine.synth_fill_(base, args.seed, 0, 0, 1.0)
+    counts = synth.counts(args.seed, n)
+    total = int(counts.sum())
+    keys = [f"{i:05d}" for i in range(n)]
+    fedavg = args.workload == "fedavg"
+    torch.cuda.synchronize()
+    state = {"weights": {"model": base}}
+
+    def received():
+        cache = Cache()
+        for i, k in enumerate(keys):
+            cache[k] = TR(client_w[i], int(counts[i]))
+        return cache
+    arrived = [received() for _ in range(args.warmup + args.steps + (0 if fedavg else 1))]
+
+    def step():
+        cache = arrived.pop()
+        if fedavg:        # syncfl top: FedAvg mutates the base in place (fedavg.py:74,87)
+            opt.do(state["weights"], cache, total=total, num_trainers=n)
+        else:             # FedOPT caller convention: weights = do(deepcopy(weights), ...)
+            state["weights"] = opt.do({"model": state["weights"]["model"].clone()}, cache, total=total,
+                                      num_trainers=n)
+
+    if not fedavg:
+        step()            # FedOPT round 1 is a passthrough (fedopt.py:87-88); time adaptive rounds only
+    elapsed, events = timed(world, args.steps, args.warmup, step)
+    name = "flame_agg_reduce" if fedavg else "flame_fedopt_reduce_adapt"
+    ks = kernel_stats(events, name)
+    if rank == 0:
+        lps = ks["launches"] / args.steps
+        k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
+        achieved = k_bytes / k_time / 1e9
+        print(json.dumps({
+            "metric": METRIC if fedavg else f"aggregated params/sec (device-resident), {n}-client {args.workload} "
+                                            f"(adaptive round)",
+            "value": n * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "host_issue_ms_per_step": ISSUE_S / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (counter-based generator, flame_amd/synth.py), rank-local slices resident in HBM",
+            "config": {"workload": f"{args.workload}: {n} clients x {G} fp32 params, parameter-sharded over "
+                                   f"{world} rank(s) (flame_amd.shard.ShardedOptimizer, {plan.owned_elements()} "
+                                   f"params per rank, tiled rank-local slab)",
+                       "clients": n, "params_per_gpu": P, "global_params": G,
+                       "parallelism": f"param-shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": name,
+                         "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes, "launches_per_step": lps},
+            "collective": _collective_note(plan, world, 4),
+            "cpu_baseline": None,
+        }), flush=True)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def bench_hier_sharded(args, world, rank, dev, M, C, P):
+    """Config 5 as named (hierarchical FedBuff parameter-sharded over the node's GPUs with an
+    RCCL all-gather) through the product's ShardedHierarchy: the model has P x world bf16
+    params; each rank holds its slices of the M x C arrivals, of the 64 middles' weights and
+    FedBuff aggregates and of the top aggregate; per step the middles' do() per arrival,
+    then ShardedHierarchy.round (one flame_hier_fedbuff launch per wave) with the top model
+    all-gathered in place wave by wave (sync mode: ShardedHierarchy.sync_round)."""
+    from flame_amd import engine, shard, synth
+    G, dt = P * world, torch.bfloat16
+    if args.hier_mode not in ("fused", "sync"):
+        raise SystemExit("multi-GPU hier bench: --hier-mode fused or sync (the product's ShardedHierarchy)")
+    hier = shard.ShardedHierarchy({"model": torch.empty(G, dtype=dt, device="meta")}, device=dev,
+                                  fracs=(1.0,) if args.no_overlap else shard.DEFAULT_FRACS)
+    plan = hier.plan
+    store, client_w = _local_slab(plan, M * C, dev, args.seed + 4, 1e-2)
+    gw = torch.empty(G, dtype=dt, device=dev)
+    engine.synth_fill_(gw, args.seed + 4, 0, 0, 1.0)
+    fetched = args.hier_middles == "fetched"
+    if fetched:   # every middle holds the model it fetched from the top (read-only)
+        shared = {"model": gw.clone()}
+        mids = [shared] * M
+    else:         # each middle's own weights: sharded state, this rank's slices only
+        own = collections.OrderedDict((nm, torch.empty(plan.local_numel[nm], dtype=dt, device=dev)) for nm in plan.names)
+        for sub in plan.subs:
+            engine.synth_fill_(own[sub.name], args.seed + 4, 0, sub.lo, 1.0)
+        mids = [collections.OrderedDict((k, v.clone()) for k, v in own.items()) for _ in range(M)]
+    stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
+    counts = [int(c) for c in synth.counts(args.seed + 4, M * C)]
+    rnd = 10
+    mid_opts = [hier.middle_optimizer() for _ in range(M)]
+    torch.cuda.synchronize()
+
+    def step_fused():
+        aggs = [None] * M
+        for m in range(M):
+            opt = mid_opts[m]
+            for t in range(C):        # one arrival per do(), as the middle role hands them over
+                i = m * C + t
+                cache = Cache()
+                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
+                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        hier.round([(mids[m], aggs[m], C, rnd - (m % 2)) for m in range(M)], None, version=rnd,
+                   top_weights={"model": gw}, top_goal=M, update_middle_weights=not fetched)
+
+    def step_sync():
+        specs = []
+        for m in range(M):
+            cache = Cache()
+            for t in range(C):
+                i = m * C + t
+                cache[f"{i:05d}"] = TR(client_w[i], counts[i])
+            specs.append((mids[m], cache, sum(counts[m * C:(m + 1) * C])))
+        hier.sync_round(specs, {"model": gw}, update_middle_weights=not fetched)
+
+    elapsed, events = timed(world, args.steps, args.warmup, step_sync if args.hier_mode == "sync" else step_fused)
+    ks = kernel_stats(events, "flame_hier_fedbuff")
+    if rank == 0:
+        lps = ks["launches"] / args.steps
+        k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
+        sync = args.hier_mode == "sync"
+        print(json.dumps({
+            "metric": "aggregated params/sec (device-resident), hierarchical "
+                      + ("FedAvg (synchronous)" if sync else "FedBuff") + ", parameter-sharded",
+            "value": M * C * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "host_issue_ms_per_step": ISSUE_S / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (counter-based generator), rank-local slices resident in HBM",
+            "config": {"workload": f"{'hier_fedavg' if sync else 'hier_fedbuff'}: {M} middles x {C} clients x {G} "
+                                   f"bf16 params, parameter-sharded over {world} rank(s) "
+                                   f"(flame_amd.shard.ShardedHierarchy, {plan.owned_elements()} params per rank)",
+                       "middles": args.hier_mode, "middle_weights": args.hier_middles,
+                       "params_per_gpu": P, "global_params": G, "parallelism": f"param-shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "flame_hier_fedbuff", "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
+                         "launches_per_step": lps},
+            "collective": _collective_note(plan, world, 2),
+        }), flush=True)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def bench_fedbuff(args, world, rank, dev):
     """The asynchronous top aggregator (asyncfl/top_aggregator.py:54-115): aggGoal arrivals,
     each handed to FedBuff.do on its own (staleness U{0..3}), then scale_add_agg_weights
@@ -578,6 +785,8 @@ def bench_hier(args, world, rank, dev):
     C = (args.clients or 4096) // M
     P = args.params or 125_000_000 // 8
     dt = torch.bfloat16
+    if world > 1 or args.force_shard:
+        return bench_hier_sharded(args, world, rank, dev, M, C, P)
     from flame_amd.slab import UpdateSlab
     store = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M * C, device=dev)
     tmp = torch.empty(P, dtype=dt, device=dev)
@@ -592,8 +801,6 @@ def bench_hier(args, world, rank, dev):
     gw_fetched = gw.clone()   # --hier-middles fetched: the model every middle fetched from the top
     stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
     rnd = 10
-    full = torch.empty(P * world, dtype=dt, device=dev) if world > 1 else None
-    full_cpu = torch.empty(P * world, dtype=dt) if world > 1 else None
     mid_opts = [optimizer_provider.get("fedbuff") for _ in range(M)]
     top_opt = optimizer_provider.get("fedbuff")
     torch.cuda.synchronize()
@@ -617,16 +824,6 @@ def bench_hier(args, world, rank, dev):
             cache[f"mid{m:03d}"] = TR(res[m][1], C, rnd - (m % 2))
             top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
-        gather()
-
-    def gather():
-        # config 5 is parameter-sharded: every rank reassembles the global bf16 model
-        if world > 1:
-            import torch.distributed as dist
-            if dist.get_backend() == "gloo":
-                dist.all_gather_into_tensor(full_cpu, gw.cpu())
-            else:
-                dist.all_gather_into_tensor(full, gw)
 
     def step_serial():
         top_agg = None
@@ -645,7 +842,6 @@ def bench_hier(args, world, rank, dev):
             cache[f"mid{m:03d}"] = TR(delta, C, rnd - (m % 2))
             top_agg = top_opt.do(top_agg, cache, total=C, version=rnd)
         top_opt.scale_add_agg_weights({"model": gw}, top_agg, M)
-        gather()
 
     from flame_amd.optimizer.fedbuff import hierarchy_round
 
@@ -665,7 +861,6 @@ def bench_hier(args, world, rank, dev):
         hierarchy_round([({"model": gw_fetched if fetched else mids[m]}, aggs[m], C, rnd - (m % 2))
                          for m in range(M)], None, version=rnd, top_weights={"model": gw}, top_goal=M,
                         update_middle_weights=not fetched)
-        gather()
 
     from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
     counts = [int(c) for c in synth.counts(args.seed + 4, M * C)]
@@ -684,7 +879,6 @@ def bench_hier(args, world, rank, dev):
         # synchronous hierarchy (syncfl middles -> syncfl top): every middle's FedAvg,
         # its delta and the top's FedAvg over the deltas in ONE launch (FLAME_HIER_SYNC)
         sync_hierarchy_round(sync_caches(), {"model": gw})
-        gather()
 
     fedavg_opt = optimizer_provider.get("fedavg")
 
@@ -698,7 +892,6 @@ def bench_hier(args, world, rank, dev):
             mids[m].copy_(new["model"])
             totals += total
         fedavg_opt.do({"model": gw}, top_cache, total=totals)
-        gather()
 
     step = {"fused": step_fused, "group": step_group, "serial": step_serial, "sync": step_sync,
             "sync_serial": step_sync_serial}[args.hier_mode]

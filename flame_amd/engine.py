@@ -736,18 +736,34 @@ class _Target:
             self.orig.copy_(self.dev)
 
 
-def accumulate(agg: dict, entries, *, device=None) -> None:
+def accumulate(agg: dict, entries, *, device=None, key_groups=None, after_group=None) -> None:
     """agg[k] += round(v_i[k] * rate_i) for entries (weights, rate) in order, in place.
 
     Restates the per-client / per-key loop of fedavg.py:79-104 and fedbuff.py:89-97,
     136-157 (agg not None) as one launch per dtype over all keys and clients.
+
+    ``key_groups`` (a partition of agg's keys, e.g. a parameter-sharded plan's waves):
+    one launch per dtype per group, in group order, calling ``after_group(i)`` as soon
+    as group ``i``'s launches are queued (the sharded path starts that group's
+    all-gather there).  Pointer rows are still built once for all keys.
     """
     if not entries:
         return
     if device is None:   # the aggregate's own device first (no per-entry list for the common case)
         device = next((t.device for t in agg.values() if isinstance(t, torch.Tensor) and t.is_cuda), None) \
             or pick_device(*[w for w, _ in entries])
-    if _accumulate_slab(agg, entries, device):
+    if _accumulate_slab(agg, entries, device, key_groups, after_group):
+        return
+    if key_groups is not None:
+        for w, _ in entries:
+            for k in w.keys():
+                if k not in agg:
+                    raise KeyError(k)
+        for gi, g in enumerate(key_groups):
+            accumulate({k: agg[k] for k in g}, [({k: w[k] for k in g if k in w}, r) for w, r in entries],
+                       device=device)
+            if after_group is not None:
+                after_group(gi)
         return
     keys = list(agg.keys())
     per_key = collections.OrderedDict()
@@ -775,77 +791,101 @@ def accumulate(agg: dict, entries, *, device=None) -> None:
             _accumulate_promoted(agg, k, [entries[ci] for ci in cis], device)
 
 
-def _accumulate_slab(agg: dict, entries, device) -> bool:
-    """Fast path: every entry is the SlotWeights of ONE UpdateSlab whose keys and dtypes are
-    exactly agg's.  Pointer rows are computed from slot numbers (numpy), without touching
-    the per-client views; returns False (nothing done) when the case does not apply."""
-    slab = getattr(entries[0][0], "slab", None)
-    if slab is None or slab.device != device or len(slab.keys) != len(agg):
-        return False
+def weight_dtype(weights, k) -> torch.dtype:
+    """dtype of ``weights[k]`` without making a view (slab slots know it from the slab)."""
+    slab = getattr(weights, "slab", None)
+    if slab is not None:
+        rng = getattr(weights, "ranges", None)
+        return slab.meta[rng[k][0] if rng is not None else k][0]
+    return weights[k].dtype
+
+
+def representatives(ws):
+    """One weights dict per distinct layout among ``ws``: slots of one slab (sharing one
+    ``ranges`` table) all carry the same keys and dtypes, so one of them stands for all;
+    any other dict stands for itself.  Lets per-key dtype checks skip thousands of slots."""
+    seen, out = set(), []
+    for w in ws:
+        slab = getattr(w, "slab", None)
+        if slab is not None:
+            tag = (id(slab), id(getattr(w, "ranges", None)), len(w))
+            if tag in seen:
+                continue
+            seen.add(tag)
+        out.append(w)
+    return out
+
+
+def slab_rows(ws, keys, numels, dtypes, device):
+    """Pointer rows of ``keys`` for client weights ``ws`` that all live in ONE UpdateSlab:
+    every ``w`` a whole :class:`~flame_amd.slab.SlotWeights` of the slab, or every ``w`` a
+    :class:`~flame_amd.slab.SlabRef` sharing one ``ranges`` table.  Addresses come from the
+    slot numbers (numpy), no per-client view is touched.  Returns ``{k: (uint64 pointers in
+    ``ws`` order, tile stride bytes)}``, or None when the case does not apply (the caller
+    then takes the per-view path)."""
+    if not ws:
+        return None
+    first = ws[0]
+    slab = getattr(first, "slab", None)
+    if slab is None or slab.device != device:
+        return None
+    ranges = getattr(first, "ranges", None)
     nk = len(slab.keys)
-    # one pass: every entry a full SlotWeights of this slab (SlotWeights carry .slab/.slot)
-    try:
-        slot_list = [w.slot for w, _ in entries if w.slab is slab and len(w) == nk]
-    except AttributeError:
+    for w in ws:
+        if getattr(w, "slab", None) is not slab or getattr(w, "ranges", None) is not ranges:
+            return None
+        if ranges is None and len(w) != nk:
+            return None
+    slots = np.fromiter((w.slot for w in ws), dtype=np.uint64, count=len(ws))
+    rows = {}
+    for k in keys:
+        if ranges is not None:
+            if k not in ranges:
+                return None
+            key, lo, hi = ranges[k]
+        else:
+            if k not in slab.meta:
+                return None
+            key, lo, hi = k, 0, slab.meta[k][2]
+        dt, _, base, slot_bytes, tile_bytes = slab.key_layout(key)
+        T = slab.storage[dt].shape[2]
+        if dt != dtypes[k] or hi - lo != numels[k] or lo % T:
+            return None
+        rows[k] = (np.uint64(base + (lo // T) * tile_bytes) + slots * np.uint64(slot_bytes), tile_bytes)
+    return rows
+
+
+def _accumulate_slab(agg: dict, entries, device, key_groups=None, after_group=None) -> bool:
+    """Fast path: every entry lives in ONE UpdateSlab (whole slots, or :class:`SlabRef`
+    ranges sharing one table) and carries exactly agg's keys in agg's dtypes.  Pointer rows
+    are computed from slot numbers (numpy), without touching the per-client views; returns
+    False (nothing done) when the case does not apply."""
+    w0 = entries[0][0]
+    if getattr(w0, "slab", None) is None or len(w0) != len(agg):
         return False
-    if len(slot_list) != len(entries):
+    rows = slab_rows([w for w, _ in entries], list(agg.keys()), {k: agg[k].numel() for k in agg},
+                     {k: agg[k].dtype for k in agg}, device)
+    if rows is None:
         return False
-    layouts = {}
-    for k in agg.keys():
-        if k not in slab.meta:
-            return False
-        lay = slab.key_layout(k)
-        if lay[0] != agg[k].dtype or agg[k].numel() != lay[1]:
-            return False
-        layouts[k] = lay
-    slots = np.array(slot_list, dtype=np.uint64)
     rates = [r for _, r in entries]
     targets = {k: _Target(agg[k], device) for k in agg.keys()}
-    groups = collections.OrderedDict()
-    for k in agg.keys():
-        groups.setdefault(dtype_code(agg[k].dtype), []).append(k)
     keep = []
-    for code, ks in groups.items():
-        segs = []
-        for k in ks:
-            _, n, base, slot_bytes, tile_bytes = layouts[k]
-            o = targets[k].dev
-            segs.append(Seg(n, out=o.data_ptr(), inp=o.data_ptr(),
-                            clients=np.uint64(base) + slots * np.uint64(slot_bytes), tile_stride=tile_bytes))
-        _launch_reduce(code, segs, rates, device, keep)
+    for gi, g in enumerate(key_groups if key_groups is not None else [list(agg.keys())]):
+        groups = collections.OrderedDict()
+        for k in g:
+            groups.setdefault(dtype_code(agg[k].dtype), []).append(k)
+        for code, ks in groups.items():
+            segs = []
+            for k in ks:
+                ptrs, tile_bytes = rows[k]
+                o = targets[k].dev
+                segs.append(Seg(o.numel(), out=o.data_ptr(), inp=o.data_ptr(), clients=ptrs, tile_stride=tile_bytes))
+            _launch_reduce(code, segs, rates, device, keep)
+        if after_group is not None:
+            after_group(gi)
     _keepalive(keep, device)
     for t in targets.values():
         t.writeback()
-    return True
-
-
-def reduce_slab_range(out: torch.Tensor, entries, key: str, lo: int, hi: int) -> bool:
-    """``out += Σ_i round(w_i[key][lo:hi] * rate_i)`` in order, for ``entries`` = (SlotWeights,
-    rate) of ONE UpdateSlab: the pointer row is computed from slot numbers (numpy) instead of
-    slicing every client's view (the sharded FedAvg's per-piece launches).  ``out`` is the
-    contiguous device slice [lo, hi) of the aggregate; ``lo`` must start a slab tile.
-    Returns False (nothing launched) when the case does not apply."""
-    if not entries:
-        return False
-    slab = getattr(entries[0][0], "slab", None)
-    if (slab is None or not out.is_cuda or slab.device != out.device or key not in slab.meta
-            or not out.is_contiguous()):
-        return False
-    if any(getattr(w, "slab", None) is not slab for w, _ in entries):
-        return False
-    dt, n, base, slot_bytes, tile_bytes = slab.key_layout(key)
-    code = dtype_code(dt)
-    T = chunk_elems(code)
-    if dt != out.dtype or not (0 <= lo <= hi <= n) or lo % T or out.numel() != hi - lo:
-        return False
-    if hi == lo:
-        return True
-    slots = np.fromiter((w.slot for w, _ in entries), dtype=np.uint64, count=len(entries))
-    ptrs = np.uint64(base + (lo // T) * tile_bytes) + slots * np.uint64(slot_bytes)
-    keep = []
-    _launch_reduce(code, [Seg(hi - lo, out=out.data_ptr(), inp=out.data_ptr(), clients=ptrs,
-                              tile_stride=tile_bytes)], [r for _, r in entries], out.device, keep)
-    _keepalive(keep, out.device)
     return True
 
 

@@ -518,13 +518,20 @@ class DeviceUpdateCache:
     ``iterkeys()`` yields keys in sorted order (diskcache's ``ORDER BY key``);
     ``pop`` hands back the TrainResult with its transfer ordered before any later
     work on the caller's stream.
+
+    ``shard=plan`` (a :class:`flame_amd.shard.ShardPlan`, e.g. ``ShardedOptimizer.plan``
+    or ``ShardedHierarchy.plan``): keep only this rank's ranges of every update -- each
+    arriving tensor's owned ranges are copied (strided H2D of those ranges only) into a
+    slab laid out for the rank's slices, so per-GPU memory and PCIe traffic scale with
+    1 / world.
     """
 
-    def __init__(self, device=None, placement: str = "slab", capacity: int = 256):
+    def __init__(self, device=None, placement: str = "slab", capacity: int = 256, shard=None):
         if placement not in ("slab", "hbm", "host"):
             raise ValueError("placement must be 'slab', 'hbm' or 'host'")
         self.placement = placement
         self.capacity = capacity
+        self.shard = shard
         self.device = torch.device(device) if device is not None else None
         self._d = collections.OrderedDict()
         self._stream = None
@@ -547,7 +554,8 @@ class DeviceUpdateCache:
     def _fits_slab(self, w):
         if self.slab is None:
             from .slab import UpdateSlab
-            self.slab = UpdateSlab(w, self.capacity, self._dev())
+            self.slab = UpdateSlab(self.shard.local_template() if self.shard is not None else w, self.capacity,
+                                   self._dev())
         sl = self.slab
         return (bool(sl._free) and list(w.keys()) == sl.keys
                 and all(isinstance(w[k], torch.Tensor) and w[k].dtype == sl.meta[k][0]
@@ -556,6 +564,8 @@ class DeviceUpdateCache:
     def __setitem__(self, key, tres):
         w = getattr(tres, "weights", None)
         ev = None
+        if self.shard is not None and isinstance(w, dict) and w:
+            w = self.shard.slice_update(w)       # this rank's ranges only (views / host slices)
         if isinstance(w, dict) and w and self.placement in ("slab", "hbm"):
             # host-resident updates (the channel's case) need no ordering behind the caller's
             # stream, so back-to-back arrivals keep the copy engine busy while the

@@ -39,5 +39,8 @@ class FedAvg(AbstractOptimizer):
         if len(cache) == 0 or total == 0:
             return None
         entries = self._pop_entries(cache, total)
-        engine.accumulate(self.agg_weights, entries)
+        # flame_amd.shard passes its plan's waves: one launch per wave, its all-gather started
+        # right behind it (callers from flame pass no such kwargs)
+        engine.accumulate(self.agg_weights, entries, key_groups=kwargs.get("flame_amd_key_groups"),
+                          after_group=kwargs.get("flame_amd_after_group"))
         return self.agg_weights

@@ -210,7 +210,8 @@ def _fused_scale_add(base_weights, agg, agg_goal, delta) -> bool:
 # ---------------------------------------------------------------- co-located middle aggregators
 def _uniform(agg: DeferredAggregate) -> bool:
     """Every queued arrival carries every key in the aggregate's dtype (the one-launch case)."""
-    return all(k in w and w[k].dtype == agg._meta[k][1] for w, _ in agg._pending for k in agg._keys)
+    return all(k in w and engine.weight_dtype(w, k) == agg._meta[k][1]
+               for w in engine.representatives([w for w, _ in agg._pending]) for k in agg._keys)
 
 
 def flush_aggregates(aggs):
@@ -299,17 +300,10 @@ def _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_de
 
 def _hier_rows(aggs, keys, device):
     """Per key: (arrival pointers middle-major, tile stride), or None if no single stride fits."""
-    first = aggs[0]._pending[0][0]
-    slab = getattr(first, "slab", None)
-    if (slab is not None and slab.device == device
-            and all(getattr(w, "slab", None) is slab for a in aggs for w, _ in a._pending)
-            and all(k in slab.meta and slab.meta[k][0] == aggs[0]._meta[k][1]
-                    and slab.meta[k][2] == math.prod(aggs[0]._meta[k][0]) for k in keys)):
-        slots = np.fromiter((w.slot for a in aggs for w, _ in a._pending), dtype=np.uint64)
-        rows = {}
-        for k in keys:
-            _, _, base, slot_bytes, tile_bytes = slab.key_layout(k)
-            rows[k] = (np.uint64(base) + slots * np.uint64(slot_bytes), tile_bytes)
+    meta = aggs[0]._meta
+    rows = engine.slab_rows([w for a in aggs for w, _ in a._pending], keys,
+                            {k: math.prod(meta[k][0]) for k in keys}, {k: meta[k][1] for k in keys}, device)
+    if rows is not None:
         return rows, []
     rows, keep = {}, []
     for k in keys:
@@ -328,7 +322,7 @@ def _hier_rows(aggs, keys, device):
 
 
 def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, top_goal=None,
-                    with_delta: bool = False, update_middle_weights: bool = True):
+                    with_delta: bool = False, update_middle_weights: bool = True, key_groups=None, after_group=None):
     """A node's co-located two-level FedBuff hierarchy in ONE pass per dtype.
 
     ``middles``: sequence of ``(mid_weights, mid_agg, mid_goal, mid_version)`` in the order
@@ -351,6 +345,10 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
     hierarchy as the reference composes it: a middle's updated weights only feed its
     upload delta (asyncfl/middle_aggregator.py:244-246) and are replaced by the top's
     model at its next fetch (:119-120) -- here the delta goes straight to the top.
+
+    ``key_groups`` / ``after_group``: as for ``engine.accumulate`` -- one launch per dtype
+    per group of keys, ``after_group(i)`` called once group ``i`` is queued (the sharded
+    hierarchy all-gathers the top model's pieces of that group there).
     """
     middles = list(middles)
     if not middles:
@@ -360,11 +358,13 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
     # the top's rates, computed as FedBuff.do does (stale versions raise here, fedbuff.py:96)
     top_rates = [1 / math.sqrt(1 + version - mv) for *_, mv in middles]
     aggs = [a for _, a, _, _ in middles]
+    # the middles' weights name the keys of this round: all of the aggregates' keys, or a
+    # subset of them (a parameter-sharded round runs the keys of one wave at a time)
     keys = list(middles[0][0].keys())
     fusable = (all(isinstance(a, DeferredAggregate) and a._data is None and a._pending and _uniform(a)
                    for a in aggs)
                and len({len(a._pending) for a in aggs}) == 1
-               and all(list(w.keys()) == keys and a._keys == keys for w, a, _, _ in middles))
+               and all(list(w.keys()) == keys and set(keys) <= set(a._keys) for w, a, _, _ in middles))
     device = None
     if fusable:
         device = engine.pick_device(middles[0][0])
@@ -389,8 +389,12 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
         rows, keep = _hier_rows(aggs, keys, device)
         fusable = rows is not None
     if not fusable:
-        return _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta,
-                                  update_middle_weights)
+        res = _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_delta,
+                                 update_middle_weights)
+        for gi in range(len(key_groups or ())):
+            if after_group is not None:
+                after_group(gi)
+        return res
 
     top_accum = top_agg is not None
     if isinstance(top_agg, DeferredAggregate):
@@ -409,21 +413,24 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
                   for w, _, _, _ in middles]
     mid_rates = [[r for _, r in a._pending] for a in aggs]
     mid_goals = [g for _, _, g, _ in middles]
-    groups = collections.OrderedDict()
-    for k in keys:
-        groups.setdefault(engine.dtype_code(aggs[0]._meta[k][1]), []).append(k)
-    for code, ks in groups.items():
-        segs = []
-        for k in ks:
-            ptrs, stride = rows[k]
-            t_out = top_out[k]
-            segs.append(engine.HierSeg(
-                numel=t_out.numel(), mid_w=[w[k].data_ptr() for w, _, _, _ in middles], clients=ptrs,
-                mid_delta=[d[k].data_ptr() for d in deltas] if deltas is not None else None,
-                top_w=top_weights[k].data_ptr() if top_weights is not None else 0,
-                top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride))
-        engine.hier_fedbuff_(segs, code, mid_rates, mid_goals, top_rates, top_accum=top_accum,
-                             top_goal=top_goal if top_weights is not None else None, device=device, keep=keep,
-                             mid_readonly=not update_middle_weights)
+    for gi, g in enumerate(key_groups if key_groups is not None else [keys]):
+        groups = collections.OrderedDict()
+        for k in g:
+            groups.setdefault(engine.dtype_code(aggs[0]._meta[k][1]), []).append(k)
+        for code, ks in groups.items():
+            segs = []
+            for k in ks:
+                ptrs, stride = rows[k]
+                t_out = top_out[k]
+                segs.append(engine.HierSeg(
+                    numel=t_out.numel(), mid_w=[w[k].data_ptr() for w, _, _, _ in middles], clients=ptrs,
+                    mid_delta=[d[k].data_ptr() for d in deltas] if deltas is not None else None,
+                    top_w=top_weights[k].data_ptr() if top_weights is not None else 0,
+                    top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride))
+            engine.hier_fedbuff_(segs, code, mid_rates, mid_goals, top_rates, top_accum=top_accum,
+                                 top_goal=top_goal if top_weights is not None else None, device=device, keep=keep,
+                                 mid_readonly=not update_middle_weights)
+        if after_group is not None:
+            after_group(gi)
     engine._keepalive(keep, device)
     return result, deltas

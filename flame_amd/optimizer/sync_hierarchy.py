@@ -38,7 +38,8 @@ def _drain(cache, total):
     return entries
 
 
-def sync_hierarchy_round(middles, top_weights, *, with_delta: bool = False, update_middle_weights: bool = True):
+def sync_hierarchy_round(middles, top_weights, *, with_delta: bool = False, update_middle_weights: bool = True,
+                         key_groups=None, after_group=None):
     """One synchronous round of a node's co-located hierarchy.
 
     ``middles``: ``(mid_weights, cache, total)`` per middle, in the order the top's
@@ -50,6 +51,9 @@ def sync_hierarchy_round(middles, top_weights, *, with_delta: bool = False, upda
 
     Every middle needs at least one update and ``total > 0`` (a middle whose FedAvg
     returns None uploads nothing new in the reference; leave it out of ``middles``).
+
+    ``key_groups`` / ``after_group``: one launch per dtype per group of keys, in order,
+    ``after_group(i)`` called once group ``i`` is final (as for ``engine.accumulate``).
     """
     middles = list(middles)
     if not middles:
@@ -69,11 +73,19 @@ def sync_hierarchy_round(middles, top_weights, *, with_delta: bool = False, upda
 
     fused = _fusable_keys(keys, mids, entries, top_weights, device, update_middle_weights)
     deltas = [collections.OrderedDict() for _ in middles] if with_delta else None
-    if fused:
-        _fused(fused, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights)
     rest = [k for k in keys if k not in fused]
-    if rest:
+    if rest:     # the op sequence of the separate calls for the keys the kernel does not take
         _compose(rest, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights)
+    fused_set = set(fused)
+    # every arrival in one UpdateSlab: pointer rows from slot numbers, once for all keys
+    fast = engine.slab_rows([w for e in entries for w, _ in e], fused, {k: top_weights[k].numel() for k in fused},
+                            {k: top_weights[k].dtype for k in fused}, device) if fused else None
+    for gi, g in enumerate(key_groups if key_groups is not None else [keys]):
+        gk = [k for k in g if k in fused_set]
+        if gk:
+            _fused(gk, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights, fast)
+        if after_group is not None:
+            after_group(gi)
     if deltas is not None:
         deltas = [collections.OrderedDict((k, d[k]) for k in keys) for d in deltas]
     return top_weights, deltas
@@ -82,6 +94,7 @@ def sync_hierarchy_round(middles, top_weights, *, with_delta: bool = False, upda
 def _fusable_keys(keys, mids, entries, top_weights, device, update_middle_weights):
     if len({len(e) for e in entries}) != 1:
         return []
+    reps = engine.representatives([w for e in entries for w, _ in e])
     out = []
     for k in keys:
         t = top_weights[k]
@@ -95,7 +108,7 @@ def _fusable_keys(keys, mids, entries, top_weights, device, update_middle_weight
         if any(x is None or x.dtype != t.dtype or x.numel() != t.numel() or x.device != device
                or not x.is_contiguous() for x in tensors):
             continue
-        if any(k not in w or w[k].dtype != t.dtype for e in entries for w, _ in e):
+        if any(k not in w or engine.weight_dtype(w, k) != t.dtype for w in reps):
             continue
         if update_middle_weights and len({w[k].data_ptr() for w in mids}) != len(mids):
             continue   # middles updated in place must not share a tensor
@@ -103,7 +116,8 @@ def _fusable_keys(keys, mids, entries, top_weights, device, update_middle_weight
     return out
 
 
-def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights):
+def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights, fast=None):
+    """``fast``: slab pointer rows of every key (engine.slab_rows) or None (per-view rows)."""
     keep = []
     mid_rates = [[r for _, r in e] for e in entries]
     groups = collections.OrderedDict()
@@ -115,7 +129,7 @@ def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_m
             t = top_weights[k]
             ptrs, stride = [], None
             ok = True
-            for e in entries:
+            for e in (entries if fast is None else ()):
                 row, ts = engine._client_row([w[k] for w, _ in e], t, device, keep)
                 if stride is None:
                     stride = ts
@@ -123,7 +137,9 @@ def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_m
                     ok = False
                     break
                 ptrs.extend(row)
-            if not ok:
+            if fast is not None:
+                ptrs, stride = fast[k]
+            elif not ok:
                 ptrs, stride = [], 0
                 for e in entries:
                     for w, _ in e:

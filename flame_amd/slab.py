@@ -26,6 +26,7 @@ write into the slot waits for that event.
 from __future__ import annotations
 
 import collections
+import collections.abc
 from typing import Dict, List
 
 import torch
@@ -47,6 +48,34 @@ class SlotWeights(dict):
                 rel()
             except Exception:  # noqa: BLE001  (interpreter shutdown)
                 pass
+
+
+class SlabRef(collections.abc.Mapping):
+    """Named element ranges of ONE slab slot: ``{name: (slab_key, lo, hi)}`` -- e.g. this
+    rank's slices of a client update (flame_amd.shard).  Tiled views are made only when a
+    value is read; the engine computes pointer rows from ``slab`` / ``slot`` / ``ranges``
+    without touching them.  ``lo`` must start a slab tile.  Holds the slot's
+    :class:`SlotWeights` (``owner``) so the slot is not recycled while this is alive."""
+
+    __slots__ = ("slab", "slot", "ranges", "shapes", "_owner")
+
+    def __init__(self, slab: "UpdateSlab", slot: int, ranges, shapes, owner=None):
+        self.slab, self.slot, self.ranges, self.shapes, self._owner = slab, slot, ranges, shapes, owner
+
+    def __getitem__(self, name):
+        key, lo, hi = self.ranges[name]
+        v = self.slab.slot_view(self.slot, key)
+        T = v.shape[1]
+        return v[lo // T: max(lo // T + 1, -(-hi // T))]
+
+    def __iter__(self):
+        return iter(self.ranges)
+
+    def __len__(self):
+        return len(self.ranges)
+
+    def __contains__(self, name):
+        return name in self.ranges
 
 
 class UpdateSlab:

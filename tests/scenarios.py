@@ -445,3 +445,51 @@ def assert_same_nonfinite(label, got, exp):
     gn, en = torch.isnan(g), torch.isnan(e)
     assert torch.equal(gn, en), f"{label}: NaN positions differ ({int((gn ^ en).sum())} elements)"
     assert torch.equal(g[~gn], e[~en]), f"{label}: non-NaN values differ"
+
+
+# ---------------------------------------------------------------- oracle hierarchies (per-rank stand-ins)
+def oracle_hierarchy_round(middles, top_agg=None, *, version, top_weights=None, top_goal=None, with_delta=False,
+                           update_middle_weights=True, key_groups=None, after_group=None):
+    """flame_amd.optimizer.fedbuff.hierarchy_round restated with the oracle FedBuff, op for op
+    as the roles issue it: per middle scale_add (fedbuff.py:101-127) + delta
+    (asyncfl/middle_aggregator.py:221-226,246), the top's do per delta (top_aggregator.py:85-92),
+    then the top's scale_add."""
+    from oracle import oracle as O
+    top = O.OracleFedBuff()
+    deltas = []
+    for i, (w, agg, goal, mv) in enumerate(middles):
+        mw = w if update_middle_weights else {k: v.clone() for k, v in w.items()}
+        prev = {k: v.clone() for k, v in mw.items()}
+        O.OracleFedBuff().scale_add_agg_weights(mw, {k: agg[k] for k in mw}, goal)
+        d = {k: mw[k] - prev[k] for k in mw}
+        deltas.append(d)
+        c = SortedCache()
+        c[f"mid{i:05d}"] = TR(d, 1, mv)
+        top_agg = top.do(top_agg, c, total=1, version=version)
+    if top_weights is not None:
+        top.scale_add_agg_weights(top_weights, top_agg, top_goal)
+    for gi in range(len(key_groups or ())):
+        after_group(gi)
+    return top_agg, (deltas if with_delta else None)
+
+
+def oracle_sync_hierarchy_round(middles, top_weights, *, with_delta=False, update_middle_weights=True,
+                                key_groups=None, after_group=None):
+    """flame_amd.optimizer.sync_hierarchy.sync_hierarchy_round restated with the oracle FedAvg:
+    per middle FedAvg.do(deepcopy(w)) + delta (syncfl/middle_aggregator.py:163-229), the top's
+    FedAvg over the deltas with rate total_m / sum (syncfl/top_aggregator.py:122-176)."""
+    from oracle import oracle as O
+    top_cache, deltas, totals = SortedCache(), [], []
+    for i, (w, cache, total) in enumerate(middles):
+        new = O.OracleFedAvg().do({k: v.clone() for k, v in w.items()}, cache, total=total)
+        d = {k: new[k] - w[k] for k in w}
+        if update_middle_weights:
+            for k in w:
+                w[k].copy_(new[k])
+        deltas.append(d)
+        top_cache[f"mid{i:05d}"] = TR(d, total)
+        totals.append(total)
+    O.OracleFedAvg().do(top_weights, top_cache, total=sum(totals))
+    for gi in range(len(key_groups or ())):
+        after_group(gi)
+    return top_weights, (deltas if with_delta else None)

@@ -950,32 +950,6 @@ def test_hierarchy_round_launch_count_and_fallback():
         hierarchy_round(mids, None, version=rnd)
 
 
-def test_reduce_slab_range_pieces_equal_full_reduce():
-    """engine.reduce_slab_range (the sharded FedAvg's per-piece launches over slab slots,
-    pointer rows from slot numbers) == one full reduction, bitwise; inapplicable cases
-    return False without launching."""
-    from flame_amd import engine
-    from flame_amd.slab import UpdateSlab
-    g = torch.Generator().manual_seed(47)
-    n, P = 9, 5 * 1024 + 333
-    slab = UpdateSlab({"a": torch.empty(P), "b": torch.empty(7, 3)}, capacity=16, device=DEV)
-    ws = [slab.put({"a": (torch.randn(P, generator=g) * 1e-2).to(DEV), "b": torch.randn(7, 3, generator=g).to(DEV)})
-          for _ in range(n)]
-    rates = [(i + 1) / 45 for i in range(n)]
-    base = torch.randn(P, generator=g).to(DEV)
-    full = base.clone()
-    engine.reduce_([full], [full], [[w["a"] for w in ws]], rates)
-    pieced = base.clone()
-    entries = list(zip(ws, rates))
-    for lo, hi in ((0, 2048), (2048, 4096), (4096, P)):
-        assert engine.reduce_slab_range(pieced[lo:hi], entries, "a", lo, hi)
-    torch.cuda.synchronize()
-    assert torch.equal(pieced.cpu(), full.cpu())
-    assert not engine.reduce_slab_range(pieced[100:200], entries, "a", 100, 200)      # not tile-aligned
-    assert not engine.reduce_slab_range(pieced[:10], [({"a": base}, 1.0)], "a", 0, 10)  # not slab slots
-    assert not engine.reduce_slab_range(pieced[:21], entries, "zz", 0, 21)             # unknown key
-
-
 def test_metric_collector_receives_kernel_metrics():
     """optimizer.metric_collector gets runtime / hbm_GBps / launches per kernel of each call
     (saved once the kernels are done; metrics.flush() waits for them)."""

@@ -1,0 +1,297 @@
+"""GPU parity of the parameter-sharded paths (flame_amd.shard) through the HIP kernels.
+
+Two gloo ranks share the one MI355X of a test box (the driver's 8-GPU runs use RCCL):
+each rank keeps only its slices of every update (``DeviceUpdateCache(shard=plan)``),
+runs the HIP drop-ins on them wave by wave and all-gathers the model in place.  The
+gathered model must equal one process's result bitwise, and the reference-generated
+hierarchy fixture.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native_loaded():
+    from flame_amd import _native
+    _native.lib()
+    assert torch.cuda.is_available()
+
+
+def _eq(a, b):
+    a, b = a.detach().cpu(), b.detach().cpu()
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.dtype in (torch.bfloat16, torch.float16):
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a, b)
+
+
+def _two_ranks(target, world=2, timeout=150):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=timeout) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert res == {r: True for r in range(world)}, res
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # ranks share the one GPU
+    return dist
+
+
+def _model(g, P):
+    return {"w": torch.randn(P, generator=g), "m": torch.randn(31, 129, generator=g),
+            "bf": torch.randn(9001, generator=g).bfloat16(), "h": torch.randn(777, generator=g).half(),
+            "d": torch.randn(2051, generator=g).double(), "nbt": torch.tensor(3, dtype=torch.int64)}
+
+
+def _update(g, tmpl, i, scale=1e-2):
+    return {k: (torch.randn(v.shape, generator=g) * scale).to(v.dtype) if v.is_floating_point()
+            else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
+
+
+# ---------------------------------------------------------------- single process
+def test_slabref_rows_equal_full_reduce():
+    """Every rank's SlabRef slices of full-model slab slots (pointer rows from slot numbers)
+    reduce to exactly the full reduction's elements, for every rank of a 3-way plan."""
+    from flame_amd import engine, shard
+    from flame_amd.slab import UpdateSlab
+    g = torch.Generator().manual_seed(47)
+    n, P = 9, 3 * 3 * 2048 * 5 + 333
+    tmpl = {"a": torch.empty(P), "b": torch.empty(P // 2, dtype=torch.bfloat16), "c": torch.empty(7, 3)}
+    slab = UpdateSlab(tmpl, capacity=16, device=DEV)
+    ws = [slab.put({k: (torch.randn(v.shape, generator=g) * 1e-2).to(v.dtype).to(DEV) for k, v in tmpl.items()})
+          for _ in range(n)]
+    rates = [(i + 1) / 45 for i in range(n)]
+    base = {k: torch.randn(v.shape, generator=g).to(v.dtype).to(DEV) for k, v in tmpl.items()}
+    full = {k: v.clone() for k, v in base.items()}
+    engine.accumulate(full, list(zip(ws, rates)))
+    for rank in range(3):
+        plan = shard.ShardPlan(tmpl, 3, rank)
+        assert any(not s.tail for s in plan.subs) and any(s.tail for s in plan.subs)
+        mine = {k: v.clone().reshape(-1) for k, v in base.items()}
+        local = plan.views(mine)
+        refs = [plan.local(w) for w in ws]
+        assert all(type(r).__name__ == "SlabRef" for r in refs)
+        assert engine.slab_rows(refs, plan.names, plan.local_numel, {n_: plan.dtypes[plan.by_name[n_].key]
+                                                                      for n_ in plan.names}, torch.device(DEV))
+        engine.accumulate(local, list(zip(refs, rates)))
+        waved = {k: v.clone().reshape(-1) for k, v in base.items()}
+        lw = plan.views(waved)
+        for wave in range(plan.n_waves):     # restricted to one wave (one launch per dtype)
+            engine.accumulate({n_: lw[n_] for n_ in plan.wave_names[wave]},
+                              [(plan.restrict(r, wave), x) for r, x in zip(refs, rates)])
+        torch.cuda.synchronize()
+        for s in plan.subs:
+            assert _eq(mine[s.key][s.lo:s.hi], full[s.key].reshape(-1)[s.lo:s.hi]), (rank, s.name)
+            assert _eq(waved[s.key][s.lo:s.hi], full[s.key].reshape(-1)[s.lo:s.hi]), (rank, s.name)
+
+
+# ---------------------------------------------------------------- FedAvg waves, two ranks
+def _fedavg_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from flame_amd import engine, shard
+        from flame_amd.ingest import DeviceUpdateCache
+        from flame_amd.optimizers import optimizer_provider
+        g = torch.Generator().manual_seed(51)
+        tmpl = _model(g, 300_007)
+        opt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=torch.device(DEV))
+        opt.set_layout(tmpl)
+        cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=16, shard=opt.plan)
+        single = optimizer_provider.get("fedavg")
+        ws = {k: v.to(DEV) for k, v in tmpl.items()}
+        wr = {k: v.clone() for k, v in ws.items()}
+        ok = opt.plan.n_waves == 3
+        for r in range(3):
+            ups = [_update(g, tmpl, 3 * r + i) for i in range(7)]
+            counts = [11 + 7 * i for i in range(7)]
+            cb = S.SortedCache()
+            for i, u in enumerate(ups):
+                cache[f"t{i}"] = S.TR(u, counts[i])        # host update: H2D of this rank's ranges only
+                cb[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, counts[i])
+            mine = {k: v.clone() for k, v in ws.items()}
+            engine.kernel_events = []
+            out = opt.do(mine, cache, total=sum(counts), num_trainers=7)
+            names = [e[0] for e in engine.kernel_events]
+            engine.kernel_events = None
+            ok = ok and out is mine and len(cache) == 0 and names.count("flame_agg_reduce") >= opt.plan.n_waves
+            wr = single.do({k: v.clone() for k, v in wr.items()}, cb, total=sum(counts))
+            torch.cuda.synchronize()
+            ok = ok and all(_eq(out[k], wr[k]) for k in wr)
+            ws = out
+        q.put((rank, bool(ok)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fedavg_waves_two_ranks_one_gpu():
+    """ShardedOptimizer(FedAvg) with rank-local slab caches: three waves, in-place gathers,
+    bitwise == one process over 3 rounds (f32 / bf16 / f16 / f64 / int64 keys)."""
+    _two_ranks(_fedavg_worker)
+
+
+# ---------------------------------------------------------------- config 5, two ranks
+def _hier_fixture_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from fixture_io import Fixture
+        from flame_amd import engine, shard
+        from flame_amd.ingest import DeviceUpdateCache
+        fx = Fixture(os.path.join(GOLD, "hier_fedbuff_small.npz"))
+        rnd = fx.meta["round"]
+        top_w0 = S.to_dev(fx.weights("top_w0"), DEV)
+        hier = shard.ShardedHierarchy(top_w0, align=8)
+        ok = hier.plan.n_waves == 3
+        dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=hier.plan)
+        middles = []
+        for mid in range(2):
+            opt, agg = hier.middle_optimizer(), None
+            for t in range(3):
+                key = f"m{mid}t{t}"
+                dc[key] = S.TR(fx.weights(f"m{mid}/update{t}"), 10 + t, rnd - t % 2)
+                c = S.SortedCache()
+                c[key] = dc.pop(key)
+                agg = opt.do(agg, c, total=10 + t, version=rnd)
+            middles.append(({k: v.clone() for k, v in top_w0.items()}, agg, 3, rnd - mid))
+        top = {k: v.clone() for k, v in top_w0.items()}
+        engine.kernel_events = []
+        _, deltas = hier.round(middles, None, version=rnd, top_weights=top, top_goal=2, with_delta=True)
+        names = [e[0] for e in engine.kernel_events]
+        engine.kernel_events = None
+        ok = ok and names == ["flame_hier_fedbuff"] * hier.plan.n_waves      # one pass per wave
+        torch.cuda.synchronize()
+        ok = ok and all(_eq(top[k], fx.weights("top_out")[k]) for k in top)
+        for mid in range(2):
+            exp = hier.plan.slice_update(fx.weights(f"m{mid}/delta"))
+            ok = ok and all(_eq(deltas[mid][n], exp[n]) for n in exp)
+        q.put((rank, bool(ok)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_hierarchy_fixture_two_ranks_one_gpu():
+    """ShardedHierarchy on the reference-generated hier_fedbuff_small fixture: every rank's
+    top model == the reference's, bitwise; its middle deltas == its slices of the reference's."""
+    _two_ranks(_hier_fixture_worker)
+
+
+def _hier_random_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from flame_amd import shard
+        from flame_amd.ingest import DeviceUpdateCache
+        from flame_amd.optimizer.fedbuff import FedBuff, hierarchy_round
+        from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+        from flame_amd.slab import UpdateSlab
+        g = torch.Generator().manual_seed(77)
+        tmpl = {"w": torch.randn(300_007, generator=g).bfloat16(), "b": torch.randn(37, generator=g).bfloat16()}
+        M, C, rnd = 3, 4, 9
+        ups = [[_update(g, tmpl, 0) for _ in range(C)] for _ in range(M)]
+        stale = [[(m + t) % 4 for t in range(C)] for m in range(M)]
+        hier = shard.ShardedHierarchy(tmpl, device=torch.device(DEV))
+        ok = hier.plan.n_waves == 3
+        for own in (True, False):
+            # sharded: rank-local slab caches
+            dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=M * C, shard=hier.plan)
+            mids_s = []
+            shared = {k: v.to(DEV) for k, v in tmpl.items()}
+            for m in range(M):
+                opt, agg = hier.middle_optimizer(), None
+                for t in range(C):
+                    key = f"m{m}t{t}"
+                    dc[key] = S.TR(ups[m][t], 1, rnd - stale[m][t])
+                    c = S.SortedCache()
+                    c[key] = dc.pop(key)
+                    agg = opt.do(agg, c, total=1, version=rnd)
+                mids_s.append(({k: v.to(DEV) for k, v in tmpl.items()} if own else shared, agg, C, rnd - m % 2))
+            top_s = {k: v.to(DEV) for k, v in tmpl.items()}
+            agg_s, d_s = hier.round(mids_s, None, version=rnd, top_weights=top_s, top_goal=M, with_delta=True,
+                                    update_middle_weights=own)
+            # one process: full slab, one hierarchy_round
+            slab = UpdateSlab(tmpl, capacity=M * C, device=DEV)
+            mids_1 = []
+            for m in range(M):
+                opt, agg = FedBuff(), None
+                for t in range(C):
+                    c = S.SortedCache()
+                    c[f"m{m}t{t}"] = S.TR(slab.put({k: v.to(DEV) for k, v in ups[m][t].items()}), 1,
+                                          rnd - stale[m][t])
+                    agg = opt.do(agg, c, total=1, version=rnd)
+                mids_1.append(({k: v.to(DEV) for k, v in tmpl.items()}, agg, C, rnd - m % 2))
+            top_1 = {k: v.to(DEV) for k, v in tmpl.items()}
+            agg_1, d_1 = hierarchy_round(mids_1, None, version=rnd, top_weights=top_1, top_goal=M, with_delta=True,
+                                         update_middle_weights=own)
+            torch.cuda.synchronize()
+            ok = ok and all(_eq(top_s[k], top_1[k]) for k in tmpl)
+            exp_agg = hier.plan.slice_update(agg_1)
+            ok = ok and all(_eq(agg_s[n], exp_agg[n]) for n in exp_agg)
+            for m in range(M):
+                exp = hier.plan.slice_update(d_1[m])
+                ok = ok and all(_eq(d_s[m][n], exp[n]) for n in exp)
+                if own:   # the middles' weights: this rank's ranges updated as one process does
+                    got, want = hier.plan.slice_update(mids_s[m][0]), hier.plan.slice_update(mids_1[m][0])
+                    ok = ok and all(_eq(got[n], want[n]) for n in want)
+        # the synchronous hierarchy, same arrivals with sample counts
+        counts = [[10 + 3 * m + t for t in range(C)] for m in range(M)]
+        dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=M * C, shard=hier.plan)
+        specs_s, specs_1 = [], []
+        slab = UpdateSlab(tmpl, capacity=M * C, device=DEV)
+        for m in range(M):
+            cs, c1 = S.SortedCache(), S.SortedCache()
+            for t in range(C):
+                dc[f"m{m}t{t}"] = S.TR(ups[m][t], counts[m][t])
+                cs[f"m{m}t{t}"] = dc.pop(f"m{m}t{t}")
+                c1[f"m{m}t{t}"] = S.TR(slab.put({k: v.to(DEV) for k, v in ups[m][t].items()}), counts[m][t])
+            specs_s.append(({k: v.to(DEV) for k, v in tmpl.items()}, cs, sum(counts[m])))
+            specs_1.append(({k: v.to(DEV) for k, v in tmpl.items()}, c1, sum(counts[m])))
+        top_s = {k: v.to(DEV) for k, v in tmpl.items()}
+        top_1 = {k: v.to(DEV) for k, v in tmpl.items()}
+        hier.sync_round(specs_s, top_s)
+        sync_hierarchy_round(specs_1, top_1)
+        torch.cuda.synchronize()
+        ok = ok and all(_eq(top_s[k], top_1[k]) for k in tmpl)
+        for (ws, _, _), (w1, _, _) in zip(specs_s, specs_1):
+            got, want = hier.plan.slice_update(ws), hier.plan.slice_update(w1)
+            ok = ok and all(_eq(got[n], want[n]) for n in want)
+        q.put((rank, bool(ok)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_hierarchy_random_two_ranks_one_gpu():
+    """ShardedHierarchy (async, own and fetched middle weights; and sync) with rank-local
+    slab caches == one process's hierarchy_round / sync_hierarchy_round, bitwise: top model
+    on every rank, each rank's slices of the top aggregate, deltas and middle weights."""
+    _two_ranks(_hier_random_worker)

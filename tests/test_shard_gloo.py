@@ -1,8 +1,10 @@
-"""Parameter-sharded FedAvg over a world_size-2 gloo group on CPU.
+"""Parameter sharding (flame_amd.shard) over world-size-2 gloo groups on CPU.
 
-The partition + all-gather logic of flame_amd.shard must reproduce the
-single-process reference result bitwise; the per-rank reducer is the oracle
-here (no GPU), the HIP kernel in the product path.
+The plan / slicing / replay / in-place all-gather logic of ShardedOptimizer and
+ShardedHierarchy must reproduce the single-process result bitwise.  The per-rank
+arithmetic is the oracle here (no GPU); the product runs the HIP drop-ins per rank
+(tests/test_gpu_parity.py runs the same compositions with two ranks on the GPU).
+A small ``align`` makes the tiny fixture models shard (the product default is 2048).
 """
 import os
 import socket
@@ -14,18 +16,6 @@ import torch.multiprocessing as mp
 from flame_amd import shard
 
 
-def test_shard_bounds_aligned_and_covering():
-    for numel in [0, 1, 1023, 1024, 25_000_000, 1_199_882]:
-        for world in [1, 2, 3, 8]:
-            for isz in [2, 4, 8]:
-                b = shard.shard_bounds(numel, world, isz)
-                assert len(b) == world and b[0][0] == 0 and b[-1][1] == numel
-                for (l0, h0), (l1, h1) in zip(b, b[1:]):
-                    assert h0 == l1
-                for lo, _ in b:
-                    assert (lo * isz) % 4096 == 0 or lo == numel
-
-
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -34,107 +24,171 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _run(target, world=2, timeout=180):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=timeout) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}, res
+
+
+def _init(rank, world, port):
     import torch.distributed as dist
-    from oracle import oracle as O
-    import scenarios as S
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _eq(a, b):
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.dtype in (torch.bfloat16, torch.float16):
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a, b)
+
+
+def _model(g, shapes, scale):
+    return {k: (torch.randn(s, generator=g) * scale).to(dt) if dt.is_floating_point else torch.tensor(5, dtype=dt)
+            for k, (s, dt) in shapes.items()}
+
+
+# ---------------------------------------------------------------- the plan (no process group)
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("align", [8, 2048])
+def test_shard_plan_partitions_every_key(world, align):
+    shapes = {"conv": ((32, 1, 3, 3), torch.float32), "bias": ((32,), torch.float32),
+              "fc1": ((128, 9216), torch.float32), "big": ((3, 1_000_003), torch.bfloat16),
+              "nbt": ((), torch.int64), "fc2": ((10, 128), torch.float16)}
+    model = {k: torch.empty(s, dtype=dt, device="meta") for k, (s, dt) in shapes.items()}
+    plans = [shard.ShardPlan(model, world, r, align=align) for r in range(world)]
+    unit = world * align
+    for k, t in model.items():
+        n = t.numel()
+        cover = torch.zeros(n, dtype=torch.int32)
+        for p in plans:
+            for s in p.subs:
+                if s.key != k:
+                    continue
+                if s.tail:
+                    assert (s.lo, s.hi) == (s.g0, s.g1) and s.g0 == n // unit * unit and s.wave == 0
+                    if p.rank == 0:
+                        cover[s.lo:s.hi] += 1
+                else:
+                    assert (s.g1 - s.g0) % unit == 0 and s.lo % align == 0 and (s.hi - s.lo) * world == s.g1 - s.g0
+                    assert s.lo == s.g0 + p.rank * (s.hi - s.lo)
+                    cover[s.lo:s.hi] += 1
+        assert bool((cover == 1).all()), k
+    for p in plans:   # the same local names on every rank; waves are 1..3 and non-empty
+        assert p.names == plans[0].names and 1 <= p.n_waves <= 3 and all(p.wave_names)
+        assert sum(len(w) for w in p.wave_names) == len(p.names)
+        assert p.owned_elements() == sum(p.local_numel.values())
+    # wave sizes follow the 75 / 20 / 5 split of the main parts
+    if align == 2048 and world == 8:
+        sizes = [sum(plans[0].by_name[n].g1 - plans[0].by_name[n].g0 for n in w if not plans[0].by_name[n].tail)
+                 for w in plans[0].wave_names]
+        assert sizes[0] > sizes[1] > sizes[2] > 0
+
+
+def test_shard_plan_slices_and_restrict():
+    g = torch.Generator().manual_seed(3)
+    w = {"a": torch.randn(100, 37, generator=g), "b": torch.randn(37, generator=g)}
+    p = shard.ShardPlan(w, 2, 1, align=8)
+    loc = p.slice_update(w)
+    assert list(loc) == p.names
+    for n, v in loc.items():
+        s = p.by_name[n]
+        assert torch.equal(v, w[s.key].reshape(-1)[s.lo:s.hi])
+    for wave in range(p.n_waves):
+        r = p.restrict(loc, wave)
+        assert list(r) == p.wave_names[wave]
+    with pytest.raises(KeyError):
+        p.slice_update({"a": w["a"], "zz": w["b"]})
+    # no process group: a ShardedOptimizer is a world-1 pass-through that still shards into waves
+    from oracle import oracle as O
+    import scenarios as S
+    opt = shard.ShardedOptimizer(O.OracleFedAvg(), device=torch.device("cpu"), waves=True, align=8)
+    c1, c2 = S.SortedCache(), S.SortedCache()
+    ups = [{k: v * 1e-2 + i for k, v in w.items()} for i in range(3)]
+    for i, u in enumerate(ups):
+        c1[f"{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 5 + i)
+        c2[f"{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 5 + i)
+    a = {k: v.clone() for k, v in w.items()}
+    b = {k: v.clone() for k, v in w.items()}
+    assert opt.do(a, c1, total=18) is a and len(c1) == 0
+    O.OracleFedAvg().do(b, c2, total=18)
+    assert all(_eq(a[k], b[k]) for k in w)
+    assert opt.do(a, S.SortedCache(), total=18) is None
+
+
+# ---------------------------------------------------------------- FedAvg (waves) / FedOPT / FedBuff
+SHAPES = {"a": ((600, 37), torch.float32), "bf": ((5001,), torch.bfloat16), "b": ((37,), torch.float32),
+          "nbt": ((), torch.int64), "h": ((3001,), torch.float16)}
+
+
+def _fedavg_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
     try:
+        from oracle import oracle as O
+        import scenarios as S
         g = torch.Generator().manual_seed(7)
-        shapes = {"a": (1000, 37), "b": (37,), "c": (5000,), "h": (3001,)}
-        dts = {"a": torch.float32, "b": torch.float32, "c": torch.bfloat16, "h": torch.float32}
-        base = {k: torch.randn(s, generator=g).to(dts[k]) for k, s in shapes.items()}
-        n = 11
-        clients = [{k: (torch.randn(s, generator=g) * 1e-2).to(dts[k]) for k, s in shapes.items()} for _ in range(n)]
-        counts = torch.randint(1, 1000, (n,), generator=g).tolist()
-        cache = S.SortedCache()
-        for i in range(n):
-            cache[f"{i:02d}"] = S.TR(clients[i], counts[i])
-
-        def oracle_reducer(acc, cl, rates):
-            O.reduce_tensor(acc, cl, rates)
-        sf = shard.ShardedFedAvg(device=torch.device("cpu"), reducer=oracle_reducer)
-        mine = {k: v.clone() for k, v in base.items()}
-        out = sf.do(mine, cache, total=sum(counts))
-        assert out is mine and len(cache) == 0
-        # single-process oracle FedAvg
-        ref = {k: v.clone() for k, v in base.items()}
-        c2 = S.SortedCache()
-        for i in range(n):
-            c2[f"{i:02d}"] = S.TR(clients[i], counts[i])
-        O.OracleFedAvg().do(ref, c2, total=sum(counts))
-        ok = all(torch.equal(out[k].view(torch.int16) if out[k].dtype == torch.bfloat16 else out[k],
-                             ref[k].view(torch.int16) if ref[k].dtype == torch.bfloat16 else ref[k]) for k in ref)
-        # slice mode + pipelined gather: each rank gets only its slice of one flat vector
-        P = 10_000
-        glob_base = torch.randn(P * world, generator=g)
-        glob_cl = [torch.randn(P * world, generator=g) * 1e-2 for _ in range(n)]
-        fr = (0.75, 0.2, 0.05)
-        pieces = shard.piece_bounds(P, fr, 1024)
-
-        def local(v):  # rank's local slice in piece-major global order
-            return torch.cat([v[world * lo + rank * (hi - lo): world * lo + (rank + 1) * (hi - lo)] for lo, hi in pieces])
-        ss = shard.ShardedSliceFedAvg(fracs=fr, reducer=oracle_reducer)
-        c3 = S.SortedCache()
-        for i in range(n):
-            c3[f"{i:02d}"] = S.TR({"m": local(glob_cl[i])}, counts[i])
-        lb = {"m": local(glob_base)}
-        ss.do(lb, c3, total=sum(counts))
-        ref3 = glob_base.clone()
-        O.reduce_tensor(ref3, glob_cl, [c / sum(counts) for c in counts])
-        ok = ok and torch.equal(ss.global_flat, ref3) and torch.equal(lb["m"], local(ref3))
-        q.put((rank, ok))
+        base = _model(g, SHAPES, 1.0)
+        ok = True
+        opt = shard.ShardedOptimizer(O.OracleFedAvg(), device=torch.device("cpu"), align=8, waves=True)
+        for r in range(2):
+            n = 11
+            clients = [_model(g, SHAPES, 1e-2) for _ in range(n)]
+            for i, c in enumerate(clients):
+                c["nbt"] = torch.tensor(r + i)
+            counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+            ca, cb = S.SortedCache(), S.SortedCache()
+            for i in range(n):
+                ca[f"{i:02d}"] = S.TR({k: v.clone() for k, v in clients[i].items()}, counts[i])
+                cb[f"{i:02d}"] = S.TR({k: v.clone() for k, v in clients[i].items()}, counts[i])
+            mine = {k: v.clone() for k, v in base.items()}
+            out = opt.do(mine, ca, total=sum(counts), num_trainers=n)
+            ok = ok and out is mine and len(ca) == 0 and opt.plan.n_waves == 3
+            ref = {k: v.clone() for k, v in base.items()}
+            O.OracleFedAvg().do(ref, cb, total=sum(counts))
+            ok = ok and all(_eq(out[k], ref[k]) for k in ref)
+            base = ref
+        # None results (fedavg.py:76-77)
+        ok = ok and opt.do({k: v.clone() for k, v in base.items()}, S.SortedCache(), total=3) is None
+        c = S.SortedCache()
+        c["x"] = S.TR({k: v.clone() for k, v in base.items()}, 0)
+        ok = ok and opt.do({k: v.clone() for k, v in base.items()}, c, total=0) is None
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_fedavg_gloo_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=180) for _ in ps)
-    for p in ps:
-        p.join(timeout=60)
-    assert res == {0: True, 1: True}
-
-
-def test_piece_bounds():
-    assert shard.piece_bounds(10_000, (0.75, 0.2, 0.05), 1024) == [(0, 7168), (7168, 9216), (9216, 10_000)]
-    assert shard.piece_bounds(100, (0.75, 0.2, 0.05), 1024) == [(0, 100)]
-    b = shard.piece_bounds(25_000_000, (0.75, 0.2, 0.05), 1024)
-    assert b[0][0] == 0 and b[-1][1] == 25_000_000 and all(lo % 1024 == 0 for lo, _ in b)
+def test_sharded_fedavg_waves_gloo_world2():
+    _run(_fedavg_worker)
 
 
 def _opt_worker(rank, world, port, q):
-    """ShardedOptimizer over FedAdam (3 rounds, f32 + bf16 + int64 buffer that FedOPT promotes)
-    and FedBuff (sharded aggregate, staleness, scale_add); oracle optimizers as the wrapped
-    per-rank optimizer -- every element's arithmetic is the single-process one."""
-    import torch.distributed as dist
-    from oracle import oracle as O
-    import scenarios as S
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    """ShardedOptimizer over FedAdam (3 rounds + an empty round, f32 / bf16 / f16 + an int64
+    buffer that FedOPT promotes) and FedBuff (sharded aggregate, staleness, scale_add)."""
+    dist = _init(rank, world, port)
     ok = True
     try:
+        from oracle import oracle as O
+        import scenarios as S
         g = torch.Generator().manual_seed(11)
-        shapes = {"a": ((600, 37), torch.float32), "bf": ((5001,), torch.bfloat16), "b": ((37,), torch.float32),
-                  "nbt": ((), torch.int64)}
-
-        def model(scale):
-            return {k: (torch.randn(s, generator=g) * scale).to(dt) if dt != torch.int64 else torch.tensor(5)
-                    for k, (s, dt) in shapes.items()}
-        w0 = model(1.0)
+        w0 = _model(g, SHAPES, 1.0)
         hyper = dict(beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
-        sharded = shard.ShardedOptimizer(O.OracleFedOPT("fedadam", **hyper), device=torch.device("cpu"))
+        sharded = shard.ShardedOptimizer(O.OracleFedOPT("fedadam", **hyper), device=torch.device("cpu"), align=8)
         single = O.OracleFedOPT("fedadam", **hyper)
         ws, wr = {k: v.clone() for k, v in w0.items()}, {k: v.clone() for k, v in w0.items()}
         for r in range(3):
             n = 5
-            ups = [model(1e-2) for _ in range(n)]
+            ups = [_model(g, SHAPES, 1e-2) for _ in range(n)]
             for i, u in enumerate(ups):
                 u["nbt"] = torch.tensor(r + i)
             counts = torch.randint(1, 100, (n,), generator=g).tolist()
@@ -145,44 +199,108 @@ def _opt_worker(rank, world, port, q):
             ws = sharded.do({k: v.clone() for k, v in ws.items()}, ca, total=sum(counts))
             wr = single.do({k: v.clone() for k, v in wr.items()}, cb, total=sum(counts))
             ok = ok and len(ca) == 0 and list(ws) == list(wr)
-            for k in wr:
-                a, b = ws[k], wr[k]
-                ok = ok and a.dtype == b.dtype and a.shape == b.shape and torch.equal(
-                    a.view(torch.int16) if a.dtype == torch.bfloat16 else a,
-                    b.view(torch.int16) if b.dtype == torch.bfloat16 else b)
-        # FedBuff: the aggregate stays sharded; scale_add gathers
-        fs = shard.ShardedOptimizer(O.OracleFedBuff(), device=torch.device("cpu"), accumulate_only=True)
+            ok = ok and all(_eq(ws[k], wr[k]) for k in wr)
+        # an empty round returns the previous round's (full-model) result, as the reference
+        # returns current_weights (fedopt.py:84-85)
+        again = sharded.do({k: v.clone() for k, v in ws.items()}, S.SortedCache(), total=7)
+        ok = ok and again is ws and all(again[k].shape == w0[k].shape for k in w0)
+        # FedBuff: the aggregate stays sharded; scale_add gathers in place
         fm = {k: v.clone() for k, v in w0.items() if k != "nbt"}
+        fs = shard.ShardedOptimizer(O.OracleFedBuff(), device=torch.device("cpu"), accumulate_only=True, align=8)
         fs.set_layout(fm)
         f1 = O.OracleFedBuff()
         agg_s = agg_r = None
         for i in range(4):
-            u = {k: v for k, v in model(1e-2).items() if k != "nbt"}
+            u = {k: v for k, v in _model(g, SHAPES, 1e-2).items() if k != "nbt"}
             ca, cb = S.SortedCache(), S.SortedCache()
             ca[f"u{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 3, 7 - i % 3)
             cb[f"u{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 3, 7 - i % 3)
             agg_s = fs.do(agg_s, ca, total=3, version=7)
             agg_r = f1.do(agg_r, cb, total=3, version=7)
+        ok = ok and list(agg_s) == fs.plan.names
         ms, mr = {k: v.clone() for k, v in fm.items()}, {k: v.clone() for k, v in fm.items()}
-        fs.scale_add_agg_weights(ms, agg_s, 4)
+        out = fs.scale_add_agg_weights(ms, agg_s, 4)
         f1.scale_add_agg_weights(mr, agg_r, 4)
-        for k in mr:
-            a, b = ms[k], mr[k]
-            ok = ok and torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a,
-                                    b.view(torch.int16) if b.dtype == torch.bfloat16 else b)
+        ok = ok and out is ms and all(_eq(ms[k], mr[k]) for k in mr)
         q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
 def test_sharded_optimizer_fedopt_fedbuff_gloo_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_opt_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=180) for _ in ps)
-    for p in ps:
-        p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    _run(_opt_worker)
+
+
+# ---------------------------------------------------------------- config 5: the sharded hierarchy
+def _hier_worker(rank, world, port, q):
+    """ShardedHierarchy (oracle per-rank hierarchy) on the reference-generated
+    hier_fedbuff_small fixture: top model == the fixture's (bitwise) on every rank, each
+    rank's middle deltas == its slices of the fixture's deltas; and the synchronous round
+    on hier_fedavg_small (f32 / bf16 / f16 / int64, 2 rounds)."""
+    dist = _init(rank, world, port)
+    ok = True
+    try:
+        from fixture_io import Fixture
+        from oracle import oracle as O
+        import scenarios as S
+        gold = os.path.join(os.path.dirname(__file__), "golden")
+        fx = Fixture(os.path.join(gold, "hier_fedbuff_small.npz"))
+        rnd = fx.meta["round"]
+        top_w0 = fx.weights("top_w0")
+        hier = shard.ShardedHierarchy(top_w0, device=torch.device("cpu"), align=8,
+                                      round_fn=S.oracle_hierarchy_round)
+        ok = ok and hier.plan.n_waves == 3 and any(not s.tail for s in hier.plan.subs)
+        middles = []
+        for mid in range(2):
+            opt, agg = hier.middle_optimizer(O.OracleFedBuff()), None
+            for t in range(3):
+                c = S.SortedCache()
+                c[f"m{mid}t{t}"] = S.TR(fx.weights(f"m{mid}/update{t}"), 10 + t, rnd - t % 2)
+                agg = opt.do(agg, c, total=10 + t, version=rnd)
+            middles.append(({k: v.clone() for k, v in top_w0.items()}, agg, 3, rnd - mid))
+        top = {k: v.clone() for k, v in top_w0.items()}
+        top_agg, deltas = hier.round(middles, None, version=rnd, top_weights=top, top_goal=2, with_delta=True)
+        ok = ok and all(_eq(top[k], fx.weights("top_out")[k]) for k in top)
+        ok = ok and list(top_agg) == hier.plan.names
+        for mid in range(2):
+            exp = hier.plan.slice_update(fx.weights(f"m{mid}/delta"))
+            ok = ok and all(_eq(deltas[mid][n], exp[n]) for n in exp)
+
+        # synchronous hierarchy (syncfl middles -> syncfl top) vs the reference fixture
+        fs = Fixture(os.path.join(gold, "hier_fedavg_small.npz"))
+        m = fs.meta
+        tw = fs.weights("top_w0")
+        hs = shard.ShardedHierarchy(tw, device=torch.device("cpu"), align=8,
+                                    sync_round_fn=S.oracle_sync_hierarchy_round)
+        top = {k: v.clone() for k, v in tw.items()}
+        mids = [{k: v.clone() for k, v in tw.items()} for _ in range(3)]
+        for r, rm in enumerate(m["rounds"]):
+            specs = []
+            for j, mm in enumerate(rm["mids"]):
+                cache = S.SortedCache()
+                for i, (e, c) in enumerate(zip(mm["ids"], mm["counts"])):
+                    cache[e] = S.TR(fs.weights(f"r{r}/m{j}/client{i}"), c)
+                specs.append((mids[j], cache, sum(mm["counts"])))
+            out, _ = hs.sync_round(specs, top)
+            ok = ok and out is top and all(_eq(top[k], fs.weights(f"r{r}/top")[k]) for k in top)
+            # keys whose middle weights this rank updated in full (the tails) match the reference
+            for j in range(3):
+                exp = hs.plan.slice_update(fs.weights(f"r{r}/m{j}/new"))
+                got = hs.plan.slice_update(mids[j])
+                ok = ok and all(_eq(got[n], exp[n]) for n in exp)
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_hierarchy_gloo_world2():
+    _run(_hier_worker)
+
+
+def test_sharded_hierarchy_gloo_world3():
+    _run(_hier_worker, world=3)
