@@ -682,7 +682,9 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
         hier.round([(mids[m], aggs[m], C, rnd - (m % 2)) for m in range(M)], None, version=rnd,
                    top_weights={"model": gw}, top_goal=M, update_middle_weights=not fetched)
 
-    def step_sync():
+    def sync_specs():
+        # every middle's cache of received updates (syncfl/middle_aggregator.py:136-160), filled
+        # as the updates arrive -- before the aggregation starts, as in the FedAvg bench
         specs = []
         for m in range(M):
             cache = Cache()
@@ -690,7 +692,11 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                 i = m * C + t
                 cache[f"{i:05d}"] = TR(client_w[i], counts[i])
             specs.append((mids[m], cache, sum(counts[m * C:(m + 1) * C])))
-        hier.sync_round(specs, {"model": gw}, update_middle_weights=not fetched)
+        return specs
+    arrived = [sync_specs() for _ in range(args.warmup + args.steps)] if args.hier_mode == "sync" else []
+
+    def step_sync():
+        hier.sync_round(arrived.pop(), {"model": gw}, update_middle_weights=not fetched)
 
     elapsed, events = timed(world, args.steps, args.warmup, step_sync if args.hier_mode == "sync" else step_fused)
     ks = kernel_stats(events, "flame_hier_fedbuff")
@@ -875,10 +881,13 @@ def bench_hier(args, world, rank, dev):
             specs.append(({"model": mids[m]}, cache, sum(counts[m * C:(m + 1) * C])))
         return specs
 
+    # the middles' caches fill as updates arrive, before the aggregation starts
+    pre = [sync_caches() for _ in range(args.warmup + args.steps)] if args.hier_mode.startswith("sync") else []
+
     def step_sync():
         # synchronous hierarchy (syncfl middles -> syncfl top): every middle's FedAvg,
         # its delta and the top's FedAvg over the deltas in ONE launch (FLAME_HIER_SYNC)
-        sync_hierarchy_round(sync_caches(), {"model": gw})
+        sync_hierarchy_round(pre.pop(), {"model": gw})
 
     fedavg_opt = optimizer_provider.get("fedavg")
 
@@ -886,7 +895,7 @@ def bench_hier(args, world, rank, dev):
         # the same round as the roles issue it: FedAvg.do per middle, delta, FedAvg.do at the top
         top_cache = Cache()
         totals = 0
-        for m, (w, cache, total) in enumerate(sync_caches()):
+        for m, (w, cache, total) in enumerate(pre.pop()):
             new = fedavg_opt.do({"model": w["model"].clone()}, cache, total=total)
             top_cache[f"mid{m:03d}"] = TR({"model": new["model"] - w["model"]}, total)
             mids[m].copy_(new["model"])

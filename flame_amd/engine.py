@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from . import shm_lease
 
 DTYPE_CODE = {
     torch.float32: N.FLAME_F32, torch.bfloat16: N.FLAME_BF16, torch.float16: N.FLAME_F16,
@@ -183,9 +184,14 @@ class _Staging:
             ev.synchronize()
 
     def hold(self, host_tensor: torch.Tensor, device) -> None:
-        """Keep a host tensor a kernel reads directly alive until the stream passes this point."""
+        """Keep a host tensor a kernel reads directly alive until the stream passes this point.
+        A view into a sender's shared-memory segment is instead waited for here: the sender
+        may rewrite the segment once the launching call has returned (shm_lease)."""
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(device))
+        if shm_lease.aliases(host_tensor):
+            ev.synchronize()
+            return
         self._inflight.append((ev, host_tensor))
 
 
@@ -252,9 +258,12 @@ ZERO_COPY_PINNED = os.environ.get("FLAME_AMD_ZERO_COPY", "1") != "0"
 
 def _as_device(t: torch.Tensor, device) -> torch.Tensor:
     if t.device != device:
+        if t.device.type == "cpu":
+            shm_lease.check_live(t)     # a view of a sender's segment that has been rewritten raises
         if ZERO_COPY_PINNED and t.device.type == "cpu" and t.is_contiguous() and t.is_pinned():
             return t  # kept alive past the launch by _keepalive
-        t = t.to(device, non_blocking=True)
+        # a copy out of a sender's shared-memory segment completes before the call returns
+        t = t.to(device, non_blocking=not shm_lease.aliases(t))
     return t.contiguous()
 
 

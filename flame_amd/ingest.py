@@ -441,11 +441,14 @@ class ShmReceiver:
     views into the shared segment that the reduction kernel streams over PCIe, or that
     :class:`DeviceUpdateCache` copies to HBM, without any host copy.
 
-    Lifetime: the sender rewrites its segment for its next message
-    (``backend/shm.py:393-403``), so a message's views are valid until that sender
-    writes again -- hand them to a DeviceUpdateCache (which copies to HBM as they
-    arrive) or aggregate before acknowledging the sender.  A segment that grew is
-    re-opened (and re-registered) transparently.
+    Lifetime (``flame_amd.shm_lease``): the sender rewrites its segment for its next
+    message (``backend/shm.py:393-403``), and nothing tells the receiver when.  So no
+    consumer keeps a view past the call it was handed to: a kernel streaming the views
+    zero-copy is waited for before ``do()`` returns, a FedBuff arrival queued for a
+    deferred reduction and a ``DeviceUpdateCache`` entry are copied to HBM before their
+    call returns, and a view used after its sender delivered a newer message raises
+    instead of reading torn data.  A segment that grew is re-opened (and re-registered)
+    transparently.
     """
 
     def __init__(self, self_id: str, register: bool = True, untrack: bool = True):
@@ -472,18 +475,30 @@ class ShmReceiver:
             reg = RegisteredBuffer(shm.buf) if self.register else None
             seg = (shm, reg)
             self._segs[name] = seg
+            import numpy as np
+            from . import shm_lease
+            shm_lease.add(name, np.frombuffer(shm.buf, dtype=np.uint8).ctypes.data, shm.size)
         return seg
 
     def get_data(self, other: str, msg_size: int) -> memoryview:
-        """The message bytes in place (the reference returns a copy)."""
+        """The message bytes in place (the reference returns a copy).  Views of the sender's
+        previous message become stale (``shm_lease.check_live`` raises on them)."""
+        from . import shm_lease
         shm, _ = self._segment(other, msg_size)
+        shm_lease.next_generation(other + "-" + self.self_id)
         return shm.buf[:msg_size]
 
     def loads(self, other: str, msg_size: int):
-        """get_data + zero-copy decode (falls back to cloudpickle for non-update messages)."""
-        return loads(self.get_data(other, msg_size))
+        """get_data + zero-copy decode (falls back to cloudpickle for non-update messages);
+        the message's tensors are stamped with the segment's generation."""
+        from . import shm_lease
+        name = other + "-" + self.self_id
+        msg = loads(self.get_data(other, msg_size))
+        return shm_lease.stamp(msg, name, shm_lease._gen[name])
 
     def _close_one(self, name):
+        from . import shm_lease
+        shm_lease.remove(name)
         shm, reg = self._segs.pop(name)
         if reg is not None:
             reg.close()
@@ -564,6 +579,13 @@ class DeviceUpdateCache:
     def __setitem__(self, key, tres):
         w = getattr(tres, "weights", None)
         ev = None
+        shm = False
+        if isinstance(w, dict) and w:
+            from . import shm_lease
+            for v in w.values():
+                if isinstance(v, torch.Tensor) and not v.is_cuda:
+                    shm_lease.check_live(v)
+                    shm = shm or shm_lease.aliases(v)
         if self.shard is not None and isinstance(w, dict) and w:
             w = self.shard.slice_update(w)       # this rank's ranges only (views / host slices)
         if isinstance(w, dict) and w and self.placement in ("slab", "hbm"):
@@ -580,10 +602,16 @@ class DeviceUpdateCache:
                         for k, v in w.items())
             ev = torch.cuda.Event()
             ev.record(st)
+            if shm:       # the sender may rewrite its segment once this returns: finish the copy
+                ev.synchronize()
         elif isinstance(w, dict) and w and self.placement == "host" and torch.cuda.is_available():
-            tres.weights = w.__class__(
-                (k, v if (not isinstance(v, torch.Tensor) or v.is_cuda or v.is_pinned()) else v.pin_memory())
-                for k, v in w.items())
+            def pinned(v):
+                if not isinstance(v, torch.Tensor) or v.is_cuda:
+                    return v
+                if shm:           # a view of a sender's segment: copy it out (registered = pinned)
+                    return torch.empty(v.shape, dtype=v.dtype, pin_memory=True).copy_(v)
+                return v if v.is_pinned() else v.pin_memory()
+            tres.weights = w.__class__((k, pinned(v)) for k, v in w.items())
         if key in self._d:
             self._d.pop(key)
         self._d[key] = (tres, ev)

@@ -38,20 +38,30 @@ logger = logging.getLogger(__name__)
 class DeferredAggregate(collections.abc.Mapping):
     """FedBuff aggregate whose queued arrivals are reduced on first read."""
 
-    def __init__(self, weights, max_pending):
+    def __init__(self, weights, max_pending, max_pending_bytes=None):
         self._keys = list(weights.keys())
-        self._meta = {k: (engine.logical_shape(weights, k), weights[k].dtype) for k in self._keys}
+        self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
         self._pending = []         # [(weights, rate)] in arrival order
         self._max_pending = max_pending
+        self._max_bytes = max_pending_bytes
+        self._held = 0             # bytes of queued arrivals that own their memory (not slab slots)
+        self._arrival_bytes = sum(math.prod(s) * torch.empty(0, dtype=dt).element_size()
+                                  for s, dt in self._meta.values())
 
     def _queue(self, entries):
         for w, _ in entries:
             for k in w.keys():
                 if k not in self._meta:
                     raise KeyError(k)
+        # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
+        # before do() returns: the sender may rewrite the segment while it waits in the queue
+        entries = [(_own_shm_views(w), r) for w, r in entries]
         self._pending.extend(entries)
-        if len(self._pending) >= self._max_pending:
+        # a queued arrival keeps its update alive (the reference frees it once folded in); slab
+        # slots are preallocated, anything else counts against max_pending_bytes
+        self._held += sum(self._arrival_bytes for w, _ in entries if getattr(w, "slab", None) is None)
+        if len(self._pending) >= self._max_pending or (self._max_bytes is not None and self._held > self._max_bytes):
             self.flush()
 
     def flush(self):
@@ -69,6 +79,7 @@ class DeferredAggregate(collections.abc.Mapping):
         else:
             engine.accumulate(self._data, self._pending)
         self._pending = []
+        self._held = 0
 
     def __getitem__(self, k):
         self.flush()
@@ -90,15 +101,34 @@ class DeferredAggregate(collections.abc.Mapping):
         return dict(self._data)
 
 
+def _own_shm_views(weights):
+    """``weights`` with every tensor that aliases a sender's shared-memory segment copied to
+    the device (synchronously); the dict itself when there is none."""
+    from .. import shm_lease
+    hit = [k for k, v in weights.items() if isinstance(v, torch.Tensor) and shm_lease.aliases(v)]
+    if not hit:
+        return weights
+    device = engine.pick_device()
+    out = collections.OrderedDict()
+    for k, v in weights.items():
+        if k in hit:
+            shm_lease.check_live(v)
+            v = v.to(device, non_blocking=False)
+        out[k] = v
+    return out
+
+
 class FedBuff(AbstractOptimizer):
     """FedBuff class."""
 
-    def __init__(self, defer: bool = True, max_pending: int = 256, fuse_scale_add: bool = True):
+    def __init__(self, defer: bool = True, max_pending: int = 256, fuse_scale_add: bool = True,
+                 max_pending_bytes: int = 16 << 30):
         self.agg_goal_weights = None
         self.is_agg_weights_none = True
         self.regularizer = Regularizer()
         self.defer = defer
         self.max_pending = max_pending
+        self.max_pending_bytes = max_pending_bytes
         self.fuse_scale_add = fuse_scale_add
 
     def do(self, agg_goal_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
@@ -125,7 +155,7 @@ class FedBuff(AbstractOptimizer):
             # each cached entry re-creates the aggregate: only the last one survives (fedbuff.py:139-140)
             weights, rate = entries[-1]
             if self.defer:
-                agg = DeferredAggregate(weights, self.max_pending)
+                agg = DeferredAggregate(weights, self.max_pending, self.max_pending_bytes)
                 agg._queue([(weights, rate)])
                 self.agg_goal_weights = agg
             else:

@@ -33,6 +33,10 @@ from .fedavg import FedAvg
 logger = logging.getLogger(__name__)
 
 
+def _same_storage(a, b) -> bool:
+    return a is b or (a.device == b.device and a.numel() > 0 and a.data_ptr() == b.data_ptr())
+
+
 class FedOPT(FedAvg):
     """FedOPT class."""
 
@@ -85,7 +89,11 @@ class FedOPT(FedAvg):
         float_dts = (torch.float32, torch.bfloat16, torch.float16)
         for k in keys:
             dt = base_weights[k].dtype
-            ok = (dt in float_dts and k in current
+            # the eager caller hands the same base dict to every do() of a round, so after the
+            # round-1 passthrough current IS base (eager_syncfl/top_aggregator.py:42,75): the
+            # reference's d = avg - current is then 0; such keys take the op-sequence path
+            aliased = k in current and _same_storage(current[k], base_weights[k])
+            ok = (dt in float_dts and k in current and not aliased
                   and current[k].dtype == dt and current[k].shape == base_weights[k].shape
                   and all(k in w and w[k].dtype == dt for w, _ in entries)
                   and (self.m_t is None or (k in self.m_t and self.m_t[k].dtype == dt

@@ -506,7 +506,47 @@ def hier_fedavg_small():
     print("wrote hier_fedavg_small.npz")
 
 
-CASES = {"feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def fedopt_eager():
+    """FedAdam / FedYogi driven by the EAGER top aggregator (eager_syncfl/top_aggregator.py:
+    36-90): base = deepcopy(weights) once per round, then do(base, cache, total=running)
+    per arrival on that same object.  From the second arrival of a round on, FedOPT's
+    current_weights IS base (round 1: the passthrough aliases agg_weights = base), so the
+    reference's d = avg - current is 0 there.  2 rounds x 3 arrivals; f32 + bf16 keys."""
+    for sort in ("fedadam", "fedyogi"):
+        gen = torch.Generator().manual_seed(13 if sort == "fedadam" else 14)
+        shapes = {"w": ((30, 20), torch.float32), "b": ((20,), torch.float32), "bf": ((99,), torch.bfloat16)}
+        weights = small_weights(gen, shapes, 1.0)
+        opt = optimizer_provider.get(sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+        fw = FixtureWriter()
+        fw.put_weights("weights0", weights)
+        counts = []
+        for r in range(2):
+            base = deepcopy(weights)
+            cache = Cache()
+            total = 0
+            rc = []
+            for i in range(3):
+                u = small_weights(gen, shapes, 1e-2)
+                c = 50 + 17 * i + r
+                rc.append(c)
+                fw.put_weights(f"r{r}/client{i}", u)
+                total += c
+                cache[f"r{r}e{i}"] = TrainResult(u, c)
+                out = opt.do(base, cache, total=total, num_trainers=3)
+                fw.put_weights(f"r{r}/a{i}/out", deepcopy(out))
+                fw.put_weights(f"r{r}/a{i}/base", deepcopy(base))
+                if opt.m_t is not None:
+                    fw.put_weights(f"r{r}/a{i}/m", deepcopy(opt.m_t))
+                    fw.put_weights(f"r{r}/a{i}/v", deepcopy(opt.v_t))
+            weights = out
+            counts.append(rc)
+        fw.meta.update({"kind": "fedopt_eager", "sort": sort, "counts": counts,
+                        "beta_1": 0.9, "beta_2": 0.99, "eta": 1e-2, "tau": 1e-3})
+        fw.save(os.path.join(HERE, f"{sort}_eager.npz"))
+        print(f"wrote {sort}_eager.npz")
+
+
+CASES = {"fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -531,6 +571,7 @@ def main():
         fedopt_rounds(s)
     hier_fedbuff_small()
     fedopt_mixed_rounds()
+    fedopt_eager()
 
 
 if __name__ == "__main__":

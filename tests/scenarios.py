@@ -75,6 +75,9 @@ def assert_close_fedopt(label, got, exp, rtol=1e-6, elementwise=True):
         g = got[k].detach().cpu().double()
         e = exp[k].double()
         den = e.abs()
+        if den.max() == 0:       # an all-zero reference (e.g. m_t after d = 0): exactly zero
+            assert torch.equal(g, e), f"{label}/{k}: expected all zeros"
+            continue
         mask = den >= rtol * den.max()
         rel = ((g - e).abs()[mask] / den[mask]).max().item() if mask.any() else 0.0
         l2 = ((g - e).norm() / e.norm().clamp_min(1e-300)).item()
@@ -196,6 +199,40 @@ def run_fedopt(fx, make_opt, device):
             res.append((f"r{r}/m", to_cpu(opt.m_t), fx.weights(f"r{r}/m")))
             res.append((f"r{r}/v", to_cpu(opt.v_t), fx.weights(f"r{r}/v")))
     return res
+
+
+def run_fedopt_eager(fx, make_opt, device):
+    """The eager top aggregator's FedOPT calls (make_golden.fedopt_eager): per round one
+    base = deepcopy(weights), then do(base, cache, total=running) per arrival."""
+    m = fx.meta
+    opt = make_opt(m["sort"], beta_1=m["beta_1"], beta_2=m["beta_2"], eta=m["eta"], tau=m["tau"])
+    weights = to_dev(fx.weights("weights0"), device)
+    res = []
+    for r, rc in enumerate(m["counts"]):
+        base = deepcopy(weights)
+        cache = SortedCache()
+        total = 0
+        for i, c in enumerate(rc):
+            total += c
+            cache[f"r{r}e{i}"] = TR(to_dev(fx.weights(f"r{r}/client{i}"), device), c)
+            out = opt.do(base, cache, total=total, num_trainers=len(rc))
+            res.append((r, f"r{r}/a{i}/out", to_cpu(out), fx.weights(f"r{r}/a{i}/out")))
+            res.append((r, f"r{r}/a{i}/base", to_cpu(base), fx.weights(f"r{r}/a{i}/base")))
+            if f"r{r}/a{i}/m" in m["keys"]:
+                res.append((r, f"r{r}/a{i}/m", to_cpu(opt.m_t), fx.weights(f"r{r}/a{i}/m")))
+                res.append((r, f"r{r}/a{i}/v", to_cpu(opt.v_t), fx.weights(f"r{r}/a{i}/v")))
+        weights = out
+    return res
+
+
+FEDOPT_EAGER_FIXTURES = ["fedadam_eager.npz", "fedyogi_eager.npz"]
+
+
+def check_fedopt_eager(res):
+    """Round 0 (passthrough, then d = 0 while current aliases base, then one adaptive step
+    from identical state): the §8(c) single-round contract; round 1: rel-L2 (state drift)."""
+    for r, label, got, exp in res:
+        assert_close_fedopt(label, got, exp, elementwise=(r == 0))
 
 
 def run_hier(fx, make_opt, device, delta_fn):

@@ -67,6 +67,13 @@ def test_golden_fedopt_single_round_elementwise(golden, name):
             S.assert_close_fedopt(f"{name}:r{r}/{key}", S.to_cpu(got), exp[key])
 
 
+@pytest.mark.parametrize("name", S.FEDOPT_EAGER_FIXTURES)
+def test_golden_fedopt_eager(golden, name):
+    """FedAdam / FedYogi driven by the eager top aggregator (same base object every arrival):
+    the key whose current_weights aliases base takes d = 0 as the reference does."""
+    S.check_fedopt_eager(S.run_fedopt_eager(golden(name), make_amd, DEV))
+
+
 def test_golden_hier_torch_delta(golden):
     for label, got, exp in S.run_hier(golden("hier_fedbuff_small.npz"), make_amd, DEV, S.delta_torch):
         S.assert_bitwise(label, got, exp)

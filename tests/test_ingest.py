@@ -162,3 +162,33 @@ def test_shm_receiver_decodes_in_place():
     finally:
         seg.close()
         seg.unlink()
+
+
+def test_shm_lease_registry_and_generations():
+    """flame_amd.shm_lease: address ranges of open segments, message generations, and the
+    stale-view check the consumers apply (no GPU: an unregistered receiver)."""
+    import cloudpickle
+    from multiprocessing import shared_memory
+    from flame_amd import ingest, shm_lease
+    w = {"w": torch.arange(1000, dtype=torch.float32)}
+    blob = cloudpickle.dumps({"weights": w, "dataset_size": 3})
+    seg = shared_memory.SharedMemory(name="flamelease_cpu-agg", create=True, size=len(blob) + 64)
+    try:
+        seg.buf[:len(blob)] = blob
+        rx = ingest.ShmReceiver("agg", register=False, untrack=False)
+        m1 = rx.loads("flamelease_cpu", len(blob))
+        t = m1["weights"]["w"]
+        assert shm_lease.aliases(t) and shm_lease.segment_of(t.data_ptr()) == "flamelease_cpu-agg"
+        assert not shm_lease.aliases(torch.zeros(4))
+        shm_lease.check_live(t)                       # current message: fine
+        shm_lease.check_live(t.reshape(-1)[:10])      # untagged derived view: not checked
+        m2 = rx.loads("flamelease_cpu", len(blob))    # the sender's next message
+        shm_lease.check_live(m2["weights"]["w"])
+        with pytest.raises(RuntimeError, match="stale"):
+            shm_lease.check_live(t)
+        del m1, m2, t
+        rx.close()
+        assert shm_lease.segment_of(np.frombuffer(seg.buf, dtype=np.uint8).ctypes.data) is None
+    finally:
+        seg.close()
+        seg.unlink()

@@ -71,3 +71,13 @@ def test_oracle_synth_matches_numpy():
         a = O.synth_f32(seed, stream, start, n, synth.scale_for_sigma(0.01))
         b = synth.synth_f32(seed, stream, np.arange(start, start + n), 0.01)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", S.FEDOPT_EAGER_FIXTURES)
+def test_oracle_fedopt_eager(golden, name):
+    """FedOPT under the eager caller (current aliases base after the round-1 passthrough)."""
+    from oracle import oracle as O
+
+    def make(sort, **kw):
+        return O.OracleFedOPT(sort, **kw)
+    S.check_fedopt_eager(S.run_fedopt_eager(golden(name), make, "cpu"))
