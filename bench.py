@@ -68,6 +68,9 @@ def parse():
                          "fetched = the middles hold the top model they fetched this round (one shared "
                          "tensor, read-only: their updated weights only feed the upload delta and are "
                          "replaced at the next fetch, asyncfl/middle_aggregator.py:119-120,244-246)")
+    ap.add_argument("--hier-mid-layout", default="tiled", choices=["tiled", "row"],
+                    help="hier_fedbuff own middles (fused / sync modes): the middles' weights as the slots of "
+                         "one tiled UpdateSlab (a chunk's middles are one contiguous block) or one tensor each")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "hier_fedbuff", "feddyn",
                              "scaffold"])
@@ -663,7 +666,12 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
         own = collections.OrderedDict((nm, torch.empty(plan.local_numel[nm], dtype=dt, device=dev)) for nm in plan.names)
         for sub in plan.subs:
             engine.synth_fill_(own[sub.name], args.seed + 4, 0, sub.lo, 1.0)
-        mids = [collections.OrderedDict((k, v.clone()) for k, v in own.items()) for _ in range(M)]
+        if args.hier_mid_layout == "tiled":     # the middles' weights as the slots of one tiled store
+            from flame_amd.slab import UpdateSlab
+            mid_store = UpdateSlab(plan.local_template(), capacity=M, device=dev)
+            mids = [mid_store.put(own) for _ in range(M)]
+        else:
+            mids = [collections.OrderedDict((k, v.clone()) for k, v in own.items()) for _ in range(M)]
     stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
     counts = [int(c) for c in synth.counts(args.seed + 4, M * C)]
     rnd = 10
@@ -716,6 +724,7 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                                    f"bf16 params, parameter-sharded over {world} rank(s) "
                                    f"(flame_amd.shard.ShardedHierarchy, {plan.owned_elements()} params per rank)",
                        "middles": args.hier_mode, "middle_weights": args.hier_middles,
+                       "middle_layout": args.hier_mid_layout,
                        "params_per_gpu": P, "global_params": G, "parallelism": f"param-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "traffic": None,
@@ -804,6 +813,13 @@ def bench_hier(args, world, rank, dev):
     gw = torch.empty(P, dtype=dt, device=dev)
     engine.synth_fill_(gw, args.seed + 4, rank * 100_000, 0, 1.0)
     mids = [gw.clone() for _ in range(M)]
+    # fused / sync modes: the middles' own weights as the slots of one tiled store (a chunk's
+    # middles form one contiguous block, flame_hier_segment.mid_tile_stride) or one tensor each
+    if args.hier_mid_layout == "tiled" and args.hier_mode in ("fused", "sync"):
+        mid_store = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M, device=dev)
+        mid_w = [mid_store.put({"model": gw}) for _ in range(M)]
+    else:
+        mid_w = [{"model": mids[m]} for m in range(M)]
     gw_fetched = gw.clone()   # --hier-middles fetched: the model every middle fetched from the top
     stale = [int(x) % 4 for x in synth.counts(args.seed + 4, M * C)]
     rnd = 10
@@ -864,7 +880,7 @@ def bench_hier(args, world, rank, dev):
                 cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
                 aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
         fetched = args.hier_middles == "fetched"
-        hierarchy_round([({"model": gw_fetched if fetched else mids[m]}, aggs[m], C, rnd - (m % 2))
+        hierarchy_round([({"model": gw_fetched} if fetched else mid_w[m], aggs[m], C, rnd - (m % 2))
                          for m in range(M)], None, version=rnd, top_weights={"model": gw}, top_goal=M,
                         update_middle_weights=not fetched)
 
@@ -878,7 +894,7 @@ def bench_hier(args, world, rank, dev):
             for t in range(C):
                 i = m * C + t
                 cache[f"{i:05d}"] = TR(client_w[i], counts[i])
-            specs.append(({"model": mids[m]}, cache, sum(counts[m * C:(m + 1) * C])))
+            specs.append((mid_w[m], cache, sum(counts[m * C:(m + 1) * C])))
         return specs
 
     # the middles' caches fill as updates arrive, before the aggregation starts

@@ -64,7 +64,8 @@ namespace {
 #define FLAME_DEFER_ST 0  // 1: store a workgroup's FLAME_WGC output chunks together at its end
 #endif
 #ifndef FLAME_HCU16
-#define FLAME_HCU16 FLAME_CU16  // client unroll of the hierarchy kernel for 16-bit dtypes
+#define FLAME_HCU16 4     // client unroll of the hierarchy kernel for 16-bit dtypes (with FLAME_HBATCH 8:
+                          // 90 VGPRs, 5 waves/SIMD; unroll 8 needs 123 VGPRs for the same time)
 #endif
 #ifndef FLAME_HWPE
 #define FLAME_HWPE 0      // hierarchy kernel: minimum waves per SIMD to compile for (0 = compiler's choice)
@@ -74,6 +75,10 @@ namespace {
 #endif
 #ifndef FLAME_HDIAG
 #define FLAME_HDIAG 0     // DIAGNOSTIC sweep variants only: 1 = skip middle-weight stores, 2 = also skip their loads
+#endif
+#ifndef FLAME_HBATCH
+#define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
+                          // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
 #endif
 #ifndef FLAME_HST
 #define FLAME_HST FLAME_ST_NT  // hierarchy kernel: store policy of the middle weights (encoding of FLAME_ST_NT)
@@ -97,6 +102,7 @@ namespace {
 #endif
 
 constexpr int kBlock = FLAME_BLOCK;
+constexpr int kHB = FLAME_HBATCH;
 constexpr int kVPT = FLAME_VPT;
 constexpr int kWGC = FLAME_WGC;
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
@@ -810,6 +816,11 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
     const uint64_t* drow = mid_delta ? mid_delta + static_cast<int64_t>(s) * n_mids : nullptr;
     const uint64_t* crow = clients + static_cast<int64_t>(s) * n_mids * n_clients;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    // byte offset of this lane's elements inside every middle's weights: contiguous or tiled
+    const int64_t woff = sg.mid_tile_stride
+        ? (chunk - sg.chunk_begin) * sg.mid_tile_stride + static_cast<int64_t>(threadIdx.x) * EPT * sizeof(T)
+        : e0 * static_cast<int64_t>(sizeof(T));
+    auto mid_ptr = [&](int m) { return reinterpret_cast<T*>(reinterpret_cast<char*>(wrow[m]) + woff); };
     A top[kVPT][EPT];
     bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
     const T* tin = reinterpret_cast<const T*>(sg.top_agg_in) + e0;
@@ -823,9 +834,17 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                 for (int j = 0; j < EPT; ++j) top[v][j] = X::ld(b[j]);
             }
         }
+        // middles in groups of kHB: a group's middle-weight stores are issued together after
+        // its reductions (FLAME_HBATCH; 1 = store each middle's weights right after its reduction)
 #pragma unroll 1
-        for (int m = 0; m < n_mids; ++m) {
-            T* wp = reinterpret_cast<T*>(wrow[m]) + e0;
+        for (int m0 = 0; m0 < n_mids; m0 += kHB) {
+            V16 pend[kHB][kVPT];
+            const int nb = n_mids - m0 < kHB ? n_mids - m0 : kHB;   // middles in this group
+#pragma unroll
+            for (int u = 0; u < kHB; ++u) {
+            const int m = m0 + u;
+            if (kHB > 1 && m >= n_mids) break;
+            T* wp = mid_ptr(m);
 #if FLAME_HPF
             V16 wv[kVPT];
 #pragma unroll
@@ -856,31 +875,41 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                         d[j] = X::st(rnd<DT>(__fsub_rn(X::ld(w[j]), X::ld(wo[v][j]))));
                         top[v][j] = X::add(top[v][j], X::tmp(d[j], rt, 0.0));
                     }
-                    if (!(flags & FLAME_HIER_MID_READONLY)) st_pol<FLAME_HST>(wp + v * VS, pack<T, EPT>(w));
-                    if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
-                    continue;
-                }
+                } else {
 #if FLAME_HPF
-                unpack<T, EPT>(wv[v], w);
+                    unpack<T, EPT>(wv[v], w);
 #elif FLAME_HDIAG == 2
 #pragma unroll
-                for (int j = 0; j < EPT; ++j) w[j] = T(0);
+                    for (int j = 0; j < EPT; ++j) w[j] = T(0);
 #else
-                unpack<T, EPT>(ld_v(wp + v * VS), w);
+                    unpack<T, EPT>(ld_v(wp + v * VS), w);
 #endif
 #pragma unroll
-                for (int j = 0; j < EPT; ++j) {
-                    S::op(w[j], X::st(acc[v][j]), g, static_cast<double>(g), &d[j]);
-                    const A t = X::tmp(d[j], rt, 0.0);
-                    top[v][j] = have_top ? X::add(top[v][j], t) : t;
+                    for (int j = 0; j < EPT; ++j) {
+                        S::op(w[j], X::st(acc[v][j]), g, static_cast<double>(g), &d[j]);
+                        const A t = X::tmp(d[j], rt, 0.0);
+                        top[v][j] = have_top ? X::add(top[v][j], t) : t;
+                    }
                 }
-#if FLAME_HDIAG
-                if (__builtin_expect(w[0] == T(0x1234) && w[1] == T(0x4321), 0))   // keeps the math live
-#endif
-                if (!(flags & FLAME_HIER_MID_READONLY)) st_pol<FLAME_HST>(wp + v * VS, pack<T, EPT>(w));
+                pend[u][v] = pack<T, EPT>(w);
                 if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
             }
             have_top = true;
+            }
+            if (!(flags & FLAME_HIER_MID_READONLY)) {
+#pragma unroll
+                for (int u = 0; u < kHB; ++u) {
+                    if (u >= nb) break;
+                    T* wp = mid_ptr(m0 + u);       // re-read from the (scalar) pointer table
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) {
+#if FLAME_HDIAG
+                        if (__builtin_expect(pend[u][v].w[0] == 0x12345u && pend[u][v].w[1] == 0x54321u, 0))
+#endif
+                        st_pol<FLAME_HST>(wp + v * VS, pend[u][v]);
+                    }
+                }
+            }
         }
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
@@ -910,7 +939,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
 #pragma unroll 1
     for (int m = 0; m < n_mids; ++m) {
         A acc[kVPT][EPT];
-        T* wp = reinterpret_cast<T*>(wrow[m]) + e0;
+        T* wp = mid_ptr(m);
         if constexpr (SYNC) {
 #pragma unroll
             for (int v = 0; v < kVPT; ++v)

@@ -529,6 +529,7 @@ class HierSeg:
     top_in: int = 0
     top_out: int = 0
     tile_stride: int = 0
+    mid_tile_stride: int = 0   # bytes between chunks of one middle's weights (0 = contiguous)
 
 
 @dataclass
@@ -578,7 +579,8 @@ def plan_hier(code: int, segs: Sequence[HierSeg], mid_rates, mid_goals, top_rate
         fixed = [s.top_w, s.top_in, s.top_out]
         unaligned = (bool(np.any(ctab[i] % VEC_BYTES)) or bool(np.any(wtab[i] % VEC_BYTES))
                      or bool(np.any(dtab[i] % VEC_BYTES)) or any(p % VEC_BYTES for p in fixed if p))
-        head[i] = (*fixed, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride, 0)
+        head[i] = (*fixed, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride,
+                   s.mid_tile_stride)
         begin += -(-s.numel // chunk) if s.numel > 0 else 0
     if begin == 0:
         begin = 1

@@ -317,15 +317,38 @@ def _compose_hierarchy(middles, top_agg, version, top_weights, top_goal, with_de
     top = FedBuff(fuse_scale_add=False)     # the separate launches, as the roles issue them
     deltas = []
     for w, agg, goal, mv in middles:
-        if not update_middle_weights:
-            w = {k: v.clone() for k, v in w.items()}
-        _, d = FedBuff(fuse_scale_add=False).scale_add_agg_weights_with_delta(w, agg, goal)
+        lw = {k: engine.logical_tensor(w, k) for k in w.keys()}
+        tiled = [k for k in lw if lw[k] is not w[k]]       # slab-slot middles: work on logical copies
+        if not update_middle_weights or tiled:
+            lw = {k: v.clone() for k, v in lw.items()}
+        _, d = FedBuff(fuse_scale_add=False).scale_add_agg_weights_with_delta(lw, agg, goal)
+        if update_middle_weights:
+            for k in tiled:
+                _write_tiled(w[k], lw[k])
         deltas.append(d)
         cache = _OneEntryCache(mid=TrainResult(d, 1, mv))
         top_agg = top.do(top_agg, cache, total=1, version=version)
     if top_weights is not None:
         top.scale_add_agg_weights(top_weights, top_agg, top_goal)
     return top_agg, (deltas if with_delta else None)
+
+
+def _write_tiled(view, logical):
+    """Store a logical tensor back into its tiled slab view (padding past numel zeroed)."""
+    flat = torch.zeros(view.numel(), dtype=view.dtype, device=view.device)
+    flat[:logical.numel()] = logical.reshape(-1)
+    view.copy_(flat.view(view.shape))
+
+
+def _tiled_stride(ts, n):
+    """0 if every tensor is a contiguous n-element tensor; the common tile stride (bytes) if
+    every one is a tiled slab view of n logical elements with one shape; else None."""
+    st = {engine.tiled_stride(t, n) if t.is_cuda else 0 for t in ts}
+    if st == {0}:
+        return 0 if all(t.is_contiguous() and t.numel() == n for t in ts) else None
+    if len(st) == 1 and len({tuple(t.shape) for t in ts}) == 1:
+        return st.pop()
+    return None
 
 
 def _hier_rows(aggs, keys, device):
@@ -396,12 +419,20 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
                and len({len(a._pending) for a in aggs}) == 1
                and all(list(w.keys()) == keys and set(keys) <= set(a._keys) for w, a, _, _ in middles))
     device = None
+    mid_stride = {}
     if fusable:
         device = engine.pick_device(middles[0][0])
         for k in keys:
             shape, dt = aggs[0]._meta[k]
-            n = middles[0][0][k].numel()
-            tensors = [w[k] for w, _, _, _ in middles]
+            n = math.prod(shape)
+            # middle weights: every middle contiguous, or every middle a tiled slot view of one
+            # layout (an UpdateSlab holding the middles: a chunk's middles are one block)
+            mw = [w[k] for w, _, _, _ in middles]
+            st = mid_stride[k] = _tiled_stride(mw, n)
+            if st is None or (st and any(t.dtype != dt or t.device != device for t in mw)):
+                fusable = False
+                break
+            tensors = [] if st else mw
             if isinstance(top_agg, collections.abc.Mapping):
                 tensors.append(top_agg[k])
             if top_weights is not None:
@@ -439,8 +470,8 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
         result = top_out
     deltas = None
     if with_delta:
-        deltas = [{k: torch.empty(w[k].shape, dtype=w[k].dtype, device=device) for k in keys}
-                  for w, _, _, _ in middles]
+        deltas = [{k: torch.empty(aggs[0]._meta[k][0], dtype=aggs[0]._meta[k][1], device=device) for k in keys}
+                  for _ in middles]
     mid_rates = [[r for _, r in a._pending] for a in aggs]
     mid_goals = [g for _, _, g, _ in middles]
     for gi, g in enumerate(key_groups if key_groups is not None else [keys]):
@@ -456,7 +487,8 @@ def hierarchy_round(middles, top_agg=None, *, version: int, top_weights=None, to
                     numel=t_out.numel(), mid_w=[w[k].data_ptr() for w, _, _, _ in middles], clients=ptrs,
                     mid_delta=[d[k].data_ptr() for d in deltas] if deltas is not None else None,
                     top_w=top_weights[k].data_ptr() if top_weights is not None else 0,
-                    top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride))
+                    top_in=t_out.data_ptr() if top_accum else 0, top_out=t_out.data_ptr(), tile_stride=stride,
+                    mid_tile_stride=mid_stride[k]))
             engine.hier_fedbuff_(segs, code, mid_rates, mid_goals, top_rates, top_accum=top_accum,
                                  top_goal=top_goal if top_weights is not None else None, device=device, keep=keep,
                                  mid_readonly=not update_middle_weights)

@@ -25,6 +25,7 @@ import torch
 
 from .. import _native as N
 from .. import engine
+from .fedbuff import _tiled_stride, _write_tiled
 
 _KERNEL_DTYPES = (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16)
 
@@ -104,8 +105,14 @@ def _fusable_keys(keys, mids, entries, top_weights, device, update_middle_weight
             continue
         if code not in _KERNEL_DTYPES:
             continue
-        tensors = [t] + [w.get(k) for w in mids]
-        if any(x is None or x.dtype != t.dtype or x.numel() != t.numel() or x.device != device
+        mw = [w.get(k) for w in mids]
+        if any(x is None for x in mw):
+            continue
+        st = _tiled_stride(mw, t.numel())       # middles contiguous (0) or slots of one tiled store
+        if st is None or any(x.dtype != t.dtype or x.device != device for x in mw):
+            continue
+        tensors = [t] + ([] if st else mw)
+        if any(x.dtype != t.dtype or x.numel() != t.numel() or x.device != device
                or not x.is_contiguous() for x in tensors):
             continue
         if any(k not in w or engine.weight_dtype(w, k) != t.dtype for w in reps):
@@ -148,12 +155,13 @@ def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_m
                         ptrs.append(c.data_ptr())
             d_ptrs = None
             if deltas is not None:
-                for d, w in zip(deltas, mids):
-                    d[k] = torch.empty_like(w[k])
+                for d in deltas:
+                    d[k] = torch.empty_like(t)
                 d_ptrs = [d[k].data_ptr() for d in deltas]
             segs.append(engine.HierSeg(numel=t.numel(), mid_w=[w[k].data_ptr() for w in mids],
                                        clients=np.asarray(ptrs, dtype=np.uint64), mid_delta=d_ptrs,
-                                       top_in=t.data_ptr(), top_out=t.data_ptr(), tile_stride=stride))
+                                       top_in=t.data_ptr(), top_out=t.data_ptr(), tile_stride=stride,
+                                       mid_tile_stride=_tiled_stride([w[k] for w in mids], t.numel())))
         engine.hier_fedbuff_(segs, code, mid_rates, [1] * len(mids), top_rates, top_accum=True, top_goal=None,
                              device=device, keep=keep, mid_readonly=not update_middle_weights, sync=True)
     engine._keepalive(keep, device)
@@ -164,12 +172,16 @@ def _compose(keys, mids, entries, top_weights, top_rates, device, deltas, update
     sub, common/util.py:152-159), FedAvg of the deltas at the top (kernel)."""
     top_entries = []
     for i, (w, e) in enumerate(zip(mids, entries)):
-        new = {k: w[k].clone() for k in keys}                    # deepcopy(self.weights)
+        lw = {k: engine.logical_tensor(w, k) for k in keys}      # slab-slot middles: logical copies
+        new = {k: lw[k].clone() for k in keys}                   # deepcopy(self.weights)
         engine.accumulate(new, [({k: x[k] for k in keys}, r) for x, r in e], device=device)
-        d = {k: new[k] - w[k] for k in keys}
+        d = {k: new[k] - lw[k] for k in keys}
         if update_middle_weights:
             for k in keys:
-                w[k].copy_(new[k])
+                if lw[k] is w[k]:
+                    w[k].copy_(new[k])
+                else:
+                    _write_tiled(w[k], new[k])
         if deltas is not None:
             deltas[i].update(d)
         top_entries.append((d, top_rates[i]))

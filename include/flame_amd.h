@@ -211,7 +211,10 @@ typedef struct flame_hier_segment {
     int64_t chunk_begin;      /* prefix sum of ceil(numel / flame_chunk_elems(dtype)) */
     int64_t flags;            /* FLAME_SEG_UNALIGNED */
     int64_t client_tile_stride;  /* as flame_segment.client_tile_stride, shared by every arrival */
-    int64_t reserved;
+    int64_t mid_tile_stride;  /* bytes between consecutive chunks of one middle's weights (0 = each
+                                 middle's weights contiguous); nonzero: every middle's weights are
+                                 tiled like the arrivals (slots of one flame_amd UpdateSlab), so a
+                                 chunk's middle weights form one contiguous [n_mids][chunk] block */
 } flame_hier_segment;
 
 /*

@@ -310,39 +310,60 @@ def test_fedbuff_stream_vs_oracle(dtype):
     S.assert_bitwise(f"fedbuff/{dtype}/delta", S.to_cpu(delta), {"w": wo["w"] - prev})
 
 
+def _full_size_columns(P, T, seed):
+    """Elements a full-size test checks against the oracle: 65,536 random ones, plus EVERY
+    element of whole kernel chunks / slab tiles -- the first two, those at 1/4, 1/2 and 3/4
+    of the tensor, and the last two (the last one ragged) -- where tiled addressing
+    (client_offset: tile * tile stride + slot) or the chunk -> segment map could go wrong
+    without random sampling noticing."""
+    n_t = -(-P // T)
+    tiles = sorted({0, 1, n_t // 4, n_t // 2, 3 * n_t // 4, n_t - 2, n_t - 1})
+    whole = np.concatenate([np.arange(t * T, min((t + 1) * T, P)) for t in tiles])
+    rand = np.random.default_rng(seed).choice(P, 65_536, replace=False)
+    return np.unique(np.concatenate([whole, rand, [0, P - 1]])), len(whole)
+
+
 def test_c3_full_size_sampled_columns():
-    """Config 3 at full size (1024 x 25M fp32 = 102.4 GB in HBM): the kernel's
-    output at 65,536 random elements equals the oracle run on those columns."""
+    """Config 3 at full size (1024 x 25M fp32 = 102.4 GB in HBM, the tiled slab the
+    headline runs on): the kernel's output equals the oracle on 65,536 random elements and
+    on every element of 7 whole chunks (first, quartiles, last incl. the ragged tail)."""
     from flame_amd import synth, engine
+    from flame_amd.slab import UpdateSlab
     O = _oracle()
     n, P = 1024, 25_000_000
     free, _ = torch.cuda.mem_get_info()
     if free < (n + 4) * P * 4:
         pytest.skip(f"needs {(n + 4) * P * 4 / 1e9:.1f} GB of HBM, {free / 1e9:.1f} GB free")
-    slab = torch.empty((n, P), dtype=torch.float32, device=DEV)
+    slab = UpdateSlab({"model": torch.empty(P)}, capacity=n, device=DEV)
+    tmp = torch.empty(P, device=DEV)
+    ws = []
     for i in range(n):
-        engine.synth_fill_(slab[i], 2, 1 + i, 0, 1e-2)
+        engine.synth_fill_(tmp, 2, 1 + i, 0, 1e-2)
+        ws.append(slab.put({"model": tmp}))
+    del tmp
     base = _synth_dev(2, 0, P, 1.0)
     base0 = base.clone()
     counts = synth.counts(2, n)
     total = int(counts.sum())
     cache = S.SortedCache()
     for i in range(n):
-        cache[f"{i:05d}"] = S.TR({"model": slab[i]}, int(counts[i]))
+        cache[f"{i:05d}"] = S.TR(ws[i], int(counts[i]))
     out = make_amd("fedavg").do({"model": base}, cache, total=total)
     torch.cuda.synchronize()
-    idx = torch.from_numpy(np.random.default_rng(0).choice(P, 65_536, replace=False)).to(DEV)
-    idx = torch.cat([idx, torch.tensor([0, P - 1], device=DEV)])
-    cols = slab[:, idx].cpu()                                     # [n, 65538]
+    T = slab.storage[torch.float32].shape[2]
+    idx_np, n_whole = _full_size_columns(P, T, 0)
+    assert n_whole >= 6 * T
+    idx = torch.from_numpy(idx_np).to(DEV)
+    cols = slab.storage[torch.float32][idx // T, :, idx % T].t().cpu()     # [n, columns]
     exp = base0[idx].cpu().clone()
     O.reduce_tensor(exp, [cols[i].contiguous() for i in range(n)], [int(c) / total for c in counts])
     got = out["model"][idx].cpu()
     assert torch.equal(got.view(torch.int32), exp.view(torch.int32))
     # the device data is the counter generator's: spot-check one column against the host restatement
-    j = int(idx[5])
+    j = int(idx_np[5])
     host = np.array([synth.synth_f32(2, 1 + i, np.array([j]), 1e-2)[0] for i in range(0, n, 97)])
     assert np.array_equal(host.view(np.uint32), cols[::97, 5].numpy().view(np.uint32))
-    del slab
+    del slab, ws, cache
     torch.cuda.empty_cache()
 
 
@@ -1176,7 +1197,7 @@ def test_sharded_fedadam_two_ranks_one_gpu():
 
 def test_c4_full_size_fedadam_sampled_columns():
     """Config 4 at full size (FedAdam, 1024 x 25M fp32 in a tiled slab, round 1 passthrough then
-    an adaptive round): cur / m / v at 65,538 sampled elements vs the oracle FedOPT run on
+    an adaptive round): cur / m / v at 65,536 random elements and 7 whole chunks vs the oracle FedOPT run on
     those columns (round 1 bitwise; the adaptive round within the §8(c) contract)."""
     from flame_amd import synth, engine
     from flame_amd.slab import UpdateSlab
@@ -1193,9 +1214,8 @@ def test_c4_full_size_fedadam_sampled_columns():
         ws.append(slab.put({"model": tmp}))
     del tmp
     base = _synth_dev(3, 0, P, 1.0)
-    idx = np.sort(np.random.default_rng(1).choice(P, 65_536, replace=False))
-    idx = np.concatenate([[0], idx, [P - 1]])
     T = slab.storage[torch.float32].shape[2]
+    idx, _ = _full_size_columns(P, T, 1)
     it = torch.from_numpy(idx).to(DEV)
     cols = slab.storage[torch.float32][it // T, :, it % T].t().cpu()        # [n, 65538]
     base_cols = base[it].cpu()
@@ -1228,7 +1248,8 @@ def test_c4_full_size_fedadam_sampled_columns():
 def test_c5_full_size_hierarchy_sampled_columns():
     """Config 5's per-GPU shard at full size (64 middles x 64 arrivals x 15.625M bf16 = 128 GB
     in a tiled slab, staleness 0..3): ONE hierarchy_round launch; middle weights, top weights
-    and the top aggregate at 65,538 sampled elements == the oracle's FedBuff op sequence
+    and the top aggregate at 65,536 random elements and every element of 7 whole chunks
+    (first, quartiles, last incl. the ragged tail) == the oracle's FedBuff op sequence
     (per-arrival do, scale_add + delta per middle, top do per delta, top scale_add), bitwise."""
     from flame_amd import synth, engine
     from flame_amd.optimizer.fedbuff import hierarchy_round
@@ -1253,11 +1274,10 @@ def test_c5_full_size_hierarchy_sampled_columns():
     top_w = tmp.clone()
     del tmp
     stale = [int(x) % 4 for x in synth.counts(6, M * C)]
-    idx = np.sort(np.random.default_rng(2).choice(P, 65_536, replace=False))
-    idx = np.concatenate([[0], idx, [P - 1]])
-    it = torch.from_numpy(idx).to(DEV)
     T = slab.storage[dt].shape[2]
-    cols = slab.storage[dt][it // T, :, it % T].t().cpu()                  # [M*C, 65538]
+    idx, _ = _full_size_columns(P, T, 2)
+    it = torch.from_numpy(idx).to(DEV)
+    cols = slab.storage[dt][it // T, :, it % T].t().cpu()                  # [M*C, columns]
     mid_cols = [x[it].cpu() for x in mids]
     top_cols = top_w[it].cpu()
     opts, aggs = [make_amd("fedbuff") for _ in range(M)], [None] * M

@@ -295,3 +295,65 @@ def test_sharded_hierarchy_random_two_ranks_one_gpu():
     slab caches == one process's hierarchy_round / sync_hierarchy_round, bitwise: top model
     on every rank, each rank's slices of the top aggregate, deltas and middle weights."""
     _two_ranks(_hier_random_worker)
+
+
+# ---------------------------------------------------------------- tiled middle weights
+@pytest.mark.parametrize("mode", ["own", "fetched_rows", "sync", "fallback"])
+def test_hierarchy_tiled_middles_equal_rows(mode):
+    """Middle weights held as the slots of one tiled UpdateSlab (a chunk's middles are one
+    block, flame_hier_segment.mid_tile_stride) == separate tensors, bitwise: middle weights,
+    deltas, top aggregate and top weights; async FedBuff and sync FedAvg hierarchies, and the
+    composed fallback (one middle's aggregate already flushed)."""
+    from flame_amd.optimizer.fedbuff import FedBuff, hierarchy_round
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    from flame_amd.slab import UpdateSlab
+    g = torch.Generator().manual_seed(91)
+    tmpl = {"w": torch.randn(100_003, generator=g).bfloat16(), "b": torch.randn(37, generator=g).bfloat16(),
+            "f": torch.randn(3000, generator=g)}
+    M, C, rnd = 5, 3, 8
+    ups = [[_update(g, tmpl, 0) for _ in range(C)] for _ in range(M)]
+    store = UpdateSlab(tmpl, capacity=M * C, device=DEV)
+    arrivals = [[store.put({k: v.to(DEV) for k, v in u.items()}) for u in row] for row in ups]
+    mstore = UpdateSlab(tmpl, capacity=M, device=DEV)
+    starts = [{k: (v + 0.5 * m).to(v.dtype) for k, v in tmpl.items()} for m in range(M)]
+    res = {}
+    for lay in ("rows", "tiled"):
+        if lay == "rows":
+            mids = [{k: v.to(DEV) for k, v in st.items()} for st in starts]
+        else:
+            mids = [mstore.put({k: v.to(DEV) for k, v in st.items()}) for st in starts]
+        top = {k: v.to(DEV) for k, v in tmpl.items()}
+        if mode == "sync":
+            specs = []
+            for m in range(M):
+                c = S.SortedCache()
+                for t in range(C):
+                    c[f"{m}{t}"] = S.TR(arrivals[m][t], 10 + m + t)
+                specs.append((mids[m], c, sum(10 + m + t for t in range(C))))
+            _, deltas = sync_hierarchy_round(specs, top, with_delta=True)
+            agg = None
+        else:
+            aggs = []
+            for m in range(M):
+                opt, a = FedBuff(), None
+                for t in range(C):
+                    c = S.SortedCache()
+                    c[f"{m}{t}"] = S.TR(arrivals[m][t], 1, rnd - (m + t) % 3)
+                    a = opt.do(a, c, total=1, version=rnd)
+                aggs.append(a)
+            if mode == "fallback":
+                aggs[2].flush()
+            agg, deltas = hierarchy_round([(mids[m], aggs[m], C, rnd - m % 2) for m in range(M)], None, version=rnd,
+                                          top_weights=top, top_goal=M, with_delta=True,
+                                          update_middle_weights=(mode != "fetched_rows"))
+        torch.cuda.synchronize()
+        res[lay] = ({k: v.cpu() for k, v in top.items()}, [S.to_cpu(d) for d in deltas],
+                    None if agg is None else S.to_cpu(agg),
+                    [{k: (mstore.read(w.slot, k) if lay == "tiled" else w[k]).cpu() for k in tmpl} for w in mids])
+    a, b = res["rows"], res["tiled"]
+    S.assert_bitwise("top", a[0], b[0])
+    for m in range(M):
+        S.assert_bitwise(f"delta{m}", a[1][m], b[1][m])
+        S.assert_bitwise(f"mid{m}", a[3][m], b[3][m])
+    if a[2] is not None:
+        S.assert_bitwise("top agg", a[2], b[2])

@@ -34,6 +34,14 @@ VARIANTS = {
     "hst2": {"FLAME_HST": 2},
     "hst3": {"FLAME_HST": 3},
     "hst5": {"FLAME_HST": 5},
+    "hb2": {"FLAME_HBATCH": 2},
+    "hb4": {"FLAME_HBATCH": 4},
+    "hb8": {"FLAME_HBATCH": 8},
+    "hb8cu4": {"FLAME_HBATCH": 8, "FLAME_HCU16": 4},
+    "hb8wpe5": {"FLAME_HBATCH": 8, "FLAME_HWPE": 5},
+    "hb4cu4": {"FLAME_HBATCH": 4, "FLAME_HCU16": 4},
+    "hb6": {"FLAME_HBATCH": 6},
+    "hb4hst0": {"FLAME_HBATCH": 4, "FLAME_HST": 0},
     "hdiag1": {"FLAME_HDIAG": 1},   # diagnostic: middle weights not stored (output not checked)
     "hdiag2": {"FLAME_HDIAG": 2},   # diagnostic: middle weights neither loaded nor stored
 }
@@ -68,6 +76,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--mid-layout", default="row", choices=["row", "tiled"],
+                    help="middle weights: one tensor each, or the slots of one tiled [tiles][M][T] block")
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
@@ -85,24 +95,45 @@ def main():
     tiles = -(-P // T)
     slab = torch.empty((tiles, M * C, T), dtype=tdt, device=dev)
     engine.synth_fill_(slab.view(-1), 6, 7, 0, 1e-2)
-    mids0 = torch.empty((M, P), dtype=tdt, device=dev)
+    tiled_mids = args.mid_layout == "tiled"
+    mids0 = torch.empty((tiles, M, T) if tiled_mids else (M, P), dtype=tdt, device=dev)
     engine.synth_fill_(mids0.view(-1), 6, 8, 0, 1.0)
+    # "<variant>:tiled" in a row-layout run: the same middles also held as one tiled block,
+    # timed in the same process (layouts compared without process-to-process spread)
+    tmids0 = None
+    if not tiled_mids and any(nm.endswith(":tiled") for nm in names):
+        tmids0 = torch.zeros((tiles, M, T), dtype=tdt, device=dev)
+        tv = tmids0.permute(1, 0, 2).reshape(M, tiles * T)
+        tv[:, :P].copy_(mids0)
+        tmids0 = tv.view(M, tiles, T).permute(1, 0, 2).contiguous()
     gw0 = torch.empty(P, dtype=tdt, device=dev)
     engine.synth_fill_(gw0, 6, 9, 0, 1.0)
     mids, gw, top = mids0.clone(), gw0.clone(), torch.empty_like(gw0)
+    tmids = tmids0.clone() if tmids0 is not None else None
     isz = slab.element_size()
-    seg = engine.HierSeg(P, mid_w=[mids[m].data_ptr() for m in range(M)],
+    mid_ptrs = ([mids.data_ptr() + m * T * isz for m in range(M)] if tiled_mids
+                else [mids[m].data_ptr() for m in range(M)])
+    mts = M * T * isz if tiled_mids else 0
+    seg = engine.HierSeg(P, mid_w=mid_ptrs,
                          clients=[slab.data_ptr() + i * T * isz for i in range(M * C)],
-                         top_w=gw.data_ptr(), top_out=top.data_ptr(), tile_stride=M * C * T * isz)
+                         top_w=gw.data_ptr(), top_out=top.data_ptr(), tile_stride=M * C * T * isz,
+                         mid_tile_stride=mts)
     mid_rates = [[1 / (1 + (m + t) % 4) ** 0.5 for t in range(C)] for m in range(M)]
     p = engine.plan_hier(code, [seg], mid_rates, [C] * M, [1 / (1 + m % 2) ** 0.5 for m in range(M)])
     dm = torch.from_numpy(p.meta).to(dev)
     b = dm.data_ptr()
+    if tmids is not None:
+        tseg = engine.HierSeg(P, mid_w=[tmids.data_ptr() + m * T * isz for m in range(M)], clients=seg.clients,
+                              top_w=gw.data_ptr(), top_out=top.data_ptr(), tile_stride=seg.tile_stride,
+                              mid_tile_stride=M * T * isz)
+        pt = engine.plan_hier(code, [tseg], mid_rates, [C] * M, [1 / (1 + m % 2) ** 0.5 for m in range(M)])
+        dmt = torch.from_numpy(pt.meta).to(dev)
+        bt = dmt.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
     libs = {nm: load(nm.split(":")[0]) for nm in names if nm != "probe"}
     # "<variant>:sync" = the same build in FLAME_HIER_SYNC mode (FedAvg middles + top FedAvg, same bytes)
     sseg = engine.HierSeg(P, mid_w=seg.mid_w, clients=seg.clients, top_in=gw.data_ptr(), top_out=top.data_ptr(),
-                          tile_stride=seg.tile_stride)
+                          tile_stride=seg.tile_stride, mid_tile_stride=mts)
     ps = engine.plan_hier(code, [sseg], mid_rates, [C] * M, [1 / (1 + m % 2) ** 0.5 for m in range(M)])
     dms = torch.from_numpy(ps.meta).to(dev)
     bs = dms.data_ptr()
@@ -119,10 +150,11 @@ def main():
             if rc:
                 raise RuntimeError(libs[nm].flame_last_error())
             return
-        rc = libs[nm].flame_hier_fedbuff(code, N.FLAME_HIER_TOP_APPLY, b + p.offs["segs"], p.n_segs, p.n_chunks,
-                                         M, C, b + p.offs["mid_w"], None, b + p.offs["clients"],
-                                         b + p.offs["mid_rates"], b + p.offs["mid_goal"], b + p.offs["top_rates"],
-                                         float(M), stream)
+        pp, bb = (pt, bt) if nm.endswith(":tiled") else (p, b)
+        rc = libs[nm].flame_hier_fedbuff(code, N.FLAME_HIER_TOP_APPLY, bb + pp.offs["segs"], pp.n_segs,
+                                         pp.n_chunks, M, C, bb + pp.offs["mid_w"], None, bb + pp.offs["clients"],
+                                         bb + pp.offs["mid_rates"], bb + pp.offs["mid_goal"],
+                                         bb + pp.offs["top_rates"], float(M), stream)
         if rc:
             raise RuntimeError(libs[nm].flame_last_error())
 
@@ -138,9 +170,15 @@ def main():
             continue
         mids.copy_(mids0)
         gw.copy_(gw0)
+        if tmids is not None:
+            tmids.copy_(tmids0)
         launch(nm)
         torch.cuda.synchronize()
-        got = (mids.clone(), gw.clone(), top.clone())
+        if nm.endswith(":tiled"):
+            mlog = tmids.permute(1, 0, 2).reshape(M, tiles * T)[:, :P].clone()
+        else:
+            mlog = mids.clone() if not tiled_mids else mids.permute(1, 0, 2).reshape(M, tiles * T)[:, :P].clone()
+        got = (mlog, gw.clone(), top.clone())
         if nm.startswith("hdiag") or nm.endswith(":sync"):
             continue
         if ref is None:
