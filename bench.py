@@ -78,6 +78,9 @@ def parse():
                     help="fedbuff: scale_add straight from the queued arrivals (on) or flush + scale_add (off)")
     ap.add_argument("--feddyn-order", default="sorted", choices=["sorted", "shuffled"],
                     help="feddyn: active_ends order (sorted = the cache order: one merged pass)")
+    ap.add_argument("--feddyn-history", default="pingpong", choices=["pingpong", "rows"],
+                    help="feddyn: per-end histories in two tiled stores written alternately, or one "
+                         "tensor per end updated in place")
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")
     ap.add_argument("--params", type=int, default=None,
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
@@ -373,7 +376,7 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
     from flame_amd.optimizers import optimizer_provider
     keys = [f"{i:05d}" for i in range(n)]
     if args.workload == "feddyn":
-        opt = optimizer_provider.get("feddyn", alpha=0.01)
+        opt = optimizer_provider.get("feddyn", alpha=0.01, history=args.feddyn_history)
         # the role's active_ends are the channel's join order (feddyn/top_aggregator.py:137);
         # "shuffled" makes it differ from the cache's sorted order (two-phase program)
         ends = list(keys)
@@ -411,7 +414,8 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
             "value": n * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
             "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32",
             "config": {"workload": f"{args.workload}: {n} clients x {P} fp32 params, {args.layout} layout"
-                                   + (f", active_ends {args.feddyn_order}" if args.workload == "feddyn" else "")},
+                                   + (f", active_ends {args.feddyn_order}, {args.feddyn_history} histories"
+                                      if args.workload == "feddyn" else "")},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,

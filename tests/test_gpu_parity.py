@@ -74,6 +74,14 @@ def test_golden_fedopt_eager(golden, name):
     S.check_fedopt_eager(S.run_fedopt_eager(golden(name), make_amd, DEV))
 
 
+def test_golden_feddyn_pingpong(golden):
+    """FedDyn with ping-pong tiled history stores == the reference fixture, bitwise."""
+    def make(sort, **kw):
+        return make_amd(sort, history="pingpong", **kw)
+    for label, got, exp in S.run_feddyn(golden("feddyn_rounds.npz"), make, DEV):
+        S.assert_bitwise(f"feddyn_pingpong:{label}", got, exp)
+
+
 def test_golden_hier_torch_delta(golden):
     for label, got, exp in S.run_hier(golden("hier_fedbuff_small.npz"), make_amd, DEV, S.delta_torch):
         S.assert_bitwise(label, got, exp)
@@ -655,14 +663,16 @@ def _dyn_update(g, tmpl, i, scale=1e-2):
             else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
 
 
-@pytest.mark.parametrize("placement,order", [("hbm", "sorted"), ("slab", "sorted"), ("hbm", "shuffled"),
-                                             ("slab", "shuffled")])
-def test_feddyn_vs_oracle_partial_participation(placement, order):
+@pytest.mark.parametrize("placement,order,history", [
+    ("hbm", "sorted", "rows"), ("slab", "sorted", "rows"), ("hbm", "shuffled", "rows"), ("slab", "shuffled", "rows"),
+    ("hbm", "sorted", "pingpong"), ("slab", "shuffled", "pingpong")])
+def test_feddyn_vs_oracle_partial_participation(placement, order, history):
     """FedDyn drop-in == oracle bitwise over 4 rounds with ends dropping out, returning and
     one untracked end; updates device-resident or tiled UpdateSlab views (history copies
     are untiled).  ~1M params x 24 ends.  ``sorted`` active_ends = the cache order (one
     merged flame_feddyn_round program); ``shuffled`` = the channel's join order differs, so
-    the mean re-reads the updated histories in a second phase."""
+    the mean re-reads the updated histories in a second phase.  ``pingpong``: histories in
+    two tiled stores, each round writing the other one (the end that leaves frees its slot)."""
     from flame_amd.slab import UpdateSlab
     O = _oracle()
     g = torch.Generator().manual_seed(23)
@@ -675,7 +685,7 @@ def test_feddyn_vs_oracle_partial_participation(placement, order):
     from flame_amd import engine
     launches = []
     engine._recorders.append(launches)
-    amd, ora = make_amd("feddyn", alpha=0.01), O.OracleFedDyn(alpha=0.01)
+    amd, ora = make_amd("feddyn", alpha=0.01, history=history), O.OracleFedDyn(alpha=0.01)
     ca_w, co_w = {k: v.to(DEV) for k, v in tmpl.items()}, {k: v.clone() for k, v in tmpl.items()}
     for r, ends in enumerate(rounds):
         amd.save_state(S._PRE, active_ends=all_ends)

@@ -15,6 +15,9 @@ step() {  # step <tag> <timeout> <cmd...>
 TAIL=3 step pytest_gpu 900 python -u -m pytest tests -m gpu -q --durations=8 --timeout 300 --timeout-method thread
 step hier_tiled 400 python bench.py --workload hier_fedbuff --steps 10 --warmup 3 --cpu-clients 0
 step hier_row 400 python bench.py --workload hier_fedbuff --steps 10 --warmup 3 --cpu-clients 0 --hier-mid-layout row
+step feddyn_pp 400 python bench.py --workload feddyn --steps 8 --warmup 2
+step feddyn_rows 400 python bench.py --workload feddyn --steps 8 --warmup 2 --feddyn-history rows
+step feddyn_pp_shuf 400 python bench.py --workload feddyn --steps 8 --warmup 2 --feddyn-order shuffled
 step hier_sync 400 python bench.py --workload hier_fedbuff --hier-mode sync --steps 10 --warmup 3 --cpu-clients 0
 export MASTER_ADDR=127.0.0.1
 TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541"
