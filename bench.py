@@ -78,7 +78,7 @@ def parse():
                     help="fedbuff: scale_add straight from the queued arrivals (on) or flush + scale_add (off)")
     ap.add_argument("--feddyn-order", default="sorted", choices=["sorted", "shuffled"],
                     help="feddyn: active_ends order (sorted = the cache order: one merged pass)")
-    ap.add_argument("--feddyn-history", default="pingpong", choices=["pingpong", "rows"],
+    ap.add_argument("--feddyn-history", default="rows", choices=["pingpong", "pingpong_rows", "rows"],
                     help="feddyn: per-end histories in two tiled stores written alternately, or one "
                          "tensor per end updated in place")
     ap.add_argument("--clients", type=int, default=None, help="default 1024 (hier_fedbuff: 64 x 64)")

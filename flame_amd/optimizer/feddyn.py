@@ -48,16 +48,20 @@ def _is_pre(state) -> bool:
 
 
 class _PingPongHistories:
-    """Per-end FedDyn histories of the fused keys in two tiled stores.  An end keeps one
-    slot index in both; ``cur[end]`` names the store holding its current history; a round
-    reads ``cur`` and writes ``1 - cur`` (then flips it)."""
+    """Per-end FedDyn histories of the fused keys in two stores.  ``cur[end]`` names the
+    store holding an end's current history; a round reads ``cur`` and writes ``1 - cur``
+    (then flips it).  ``tiled``: each store is one UpdateSlab (an end = one slot index in
+    both); else every end owns two contiguous tensors per key."""
 
-    def __init__(self, template, device, capacity):
+    def __init__(self, template, device, capacity, tiled=True):
         from ..slab import UpdateSlab
         self.template = template
         self.device = device
         self.capacity = capacity
-        self.stores = [UpdateSlab(template, capacity, device), UpdateSlab(template, capacity, device)]
+        self.tiled = tiled
+        self.stores = [UpdateSlab(template, capacity, device), UpdateSlab(template, capacity, device)] if tiled \
+            else None
+        self.rows = {}            # untiled: end -> ({k: tensor}, {k: tensor})
         self.slot, self.cur = {}, {}
         self.free = list(range(capacity - 1, -1, -1))
 
@@ -65,7 +69,14 @@ class _PingPongHistories:
         return list(self.template.keys())
 
     def ensure(self, ends):
-        need = [e for e in ends if e not in self.slot]
+        need = list(dict.fromkeys(e for e in ends if e not in self.slot))
+        if not self.tiled:
+            for e in need:
+                self.slot[e] = 0
+                self.cur[e] = 0
+                self.rows[e] = tuple({k: torch.empty(t.shape, dtype=t.dtype, device=self.device)
+                                      for k, t in self.template.items()} for _ in range(2))
+            return
         if len(need) > len(self.free):
             self._grow(len(self.slot) + len(need))
         for e in need:
@@ -74,8 +85,12 @@ class _PingPongHistories:
 
     def release(self, keep):
         for e in [e for e in self.slot if e not in keep]:
-            self.free.append(self.slot.pop(e))
+            s = self.slot.pop(e)
             self.cur.pop(e)
+            if self.tiled:
+                self.free.append(s)
+            else:
+                self.rows.pop(e)
 
     def _grow(self, need):
         old = self.stores
@@ -90,14 +105,18 @@ class _PingPongHistories:
         self.capacity = cap
 
     def ptr(self, store, k, end) -> int:
+        if not self.tiled:
+            return self.rows[end][store][k].data_ptr()
         _, _, base, slot_bytes, _ = self.stores[store].key_layout(k)
         return base + self.slot[end] * slot_bytes
 
     def tile_stride(self, k) -> int:
-        return self.stores[0].key_layout(k)[4]
+        return self.stores[0].key_layout(k)[4] if self.tiled else 0
 
     def read(self, end, k):
         """The end's current history of key ``k`` (a contiguous copy in the model's shape)."""
+        if not self.tiled:
+            return self.rows[end][self.cur[end]][k].clone()
         st = self.stores[self.cur[end]]
         return st.read(self.slot[end], k)
 
@@ -136,8 +155,8 @@ class FedDyn(FedAvg):
 
     def __init__(self, alpha, history: str = "rows"):
         super().__init__()
-        if history not in ("rows", "pingpong"):
-            raise ValueError("history must be 'rows' or 'pingpong'")
+        if history not in ("rows", "pingpong", "pingpong_rows"):
+            raise ValueError("history must be 'rows', 'pingpong' or 'pingpong_rows'")
         self.alpha = alpha
         self.local_param_dict = dict()
         self.cld_model = None
@@ -171,7 +190,7 @@ class FedDyn(FedAvg):
             if end not in self.local_param_dict:
                 logger.debug(f"adding untracked end {end} to hist terms")
                 self.local_param_dict[end] = None
-        pp = self.history == "pingpong"
+        pp = self.history.startswith("pingpong")
         if pp and self._pp is None:
             self._init_pingpong(arrivals, device)
         fused = [k for k in base_weights if (self._fusable_pp(k, arrivals) if pp
@@ -219,7 +238,8 @@ class FedDyn(FedAvg):
                 if a.is_floating_point() and all(k in w and w[k].dtype == a.dtype for _, w in arrivals)]
         template = collections.OrderedDict((k, torch.empty(self.agg_weights[k].shape, dtype=self.agg_weights[k].dtype,
                                                            device="meta")) for k in keys)
-        self._pp = _PingPongHistories(template, device, max(len(self.local_param_dict), 1))
+        self._pp = _PingPongHistories(template, device, max(len(self.local_param_dict), 1),
+                                      tiled=self.history == "pingpong")
 
     def _fusable_pp(self, k, arrivals) -> bool:
         a = self.agg_weights[k]

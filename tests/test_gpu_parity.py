@@ -665,7 +665,7 @@ def _dyn_update(g, tmpl, i, scale=1e-2):
 
 @pytest.mark.parametrize("placement,order,history", [
     ("hbm", "sorted", "rows"), ("slab", "sorted", "rows"), ("hbm", "shuffled", "rows"), ("slab", "shuffled", "rows"),
-    ("hbm", "sorted", "pingpong"), ("slab", "shuffled", "pingpong")])
+    ("hbm", "sorted", "pingpong"), ("slab", "shuffled", "pingpong"), ("slab", "shuffled", "pingpong_rows")])
 def test_feddyn_vs_oracle_partial_participation(placement, order, history):
     """FedDyn drop-in == oracle bitwise over 4 rounds with ends dropping out, returning and
     one untracked end; updates device-resident or tiled UpdateSlab views (history copies
