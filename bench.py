@@ -86,6 +86,8 @@ def parse():
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--shard-fracs", default=None,
+                    help="N>1: element fractions of the waves, e.g. 0.9,0.1 (default: flame_amd.shard's)")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the N>1 code path (process group + sharded FedAvg + all-gather) even at N=1 "
                          "(rehearses the RCCL path on a one-GPU box under torchrun)")
@@ -567,6 +569,14 @@ def _local_slab(plan, n, dev, seed, sigma):
     return store, ws
 
 
+def _fracs(args, shard, default=None):
+    if args.no_overlap:
+        return (1.0,)
+    if args.shard_fracs:
+        return tuple(float(x) for x in args.shard_fracs.split(","))
+    return default or shard.DEFAULT_FRACS
+
+
 def _collective_note(plan, world, itemsize):
     recv = sum((s.g1 - s.g0) - (s.hi - s.lo) for s in plan.subs if not s.tail) * itemsize
     return {"kind": "in-place all_gather_into_tensor per wave (RCCL over xGMI)" if world > 1 else "none (world 1)",
@@ -583,8 +593,7 @@ def bench_sharded(args, world, rank, dev, n, P):
     from flame_amd import engine, shard, synth
     from flame_amd.optimizers import optimizer_provider
     G = P * world
-    opt = shard.ShardedOptimizer(optimizer_provider.get(args.workload), device=dev,
-                                 fracs=(1.0,) if args.no_overlap else shard.DEFAULT_FRACS)
+    opt = shard.ShardedOptimizer(optimizer_provider.get(args.workload), device=dev, fracs=_fracs(args, shard))
     opt.set_layout({"model": torch.empty(G, dtype=torch.float32, device="meta")})
     plan = opt.plan
     store, client_w = _local_slab(plan, n, dev, args.seed, 1e-2)
@@ -657,7 +666,7 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
     if args.hier_mode not in ("fused", "sync"):
         raise SystemExit("multi-GPU hier bench: --hier-mode fused or sync (the product's ShardedHierarchy)")
     hier = shard.ShardedHierarchy({"model": torch.empty(G, dtype=dt, device="meta")}, device=dev,
-                                  fracs=(1.0,) if args.no_overlap else shard.DEFAULT_FRACS)
+                                  fracs=_fracs(args, shard, shard.HIER_FRACS))
     plan = hier.plan
     store, client_w = _local_slab(plan, M * C, dev, args.seed + 4, 1e-2)
     gw = torch.empty(G, dtype=dt, device=dev)

@@ -28,7 +28,7 @@ import math
 import numpy as np
 import torch
 
-from .. import engine
+from .. import engine, shm_lease
 from .abstract import AbstractOptimizer
 from .regularizer import Regularizer
 
@@ -104,7 +104,8 @@ class DeferredAggregate(collections.abc.Mapping):
 def _own_shm_views(weights):
     """``weights`` with every tensor that aliases a sender's shared-memory segment copied to
     the device (synchronously); the dict itself when there is none."""
-    from .. import shm_lease
+    if not shm_lease.active() or getattr(weights, "slab", None) is not None:
+        return weights            # no segment open, or a slab slot (device memory)
     hit = [k for k, v in weights.items() if isinstance(v, torch.Tensor) and shm_lease.aliases(v)]
     if not hit:
         return weights

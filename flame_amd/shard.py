@@ -49,6 +49,9 @@ from . import engine
 
 ALIGN_ELEMS = 2048               # a multiple of every kernel chunk / slab tile (1024 fp32, 2048 bf16 / fp16)
 DEFAULT_FRACS = (0.75, 0.20, 0.05)
+# the hierarchy's workgroups are long (a chunk's 4096 arrivals): every extra launch costs a
+# ramp-down tail, so it pipelines in two waves
+HIER_FRACS = (0.9, 0.1)
 
 
 @dataclass(frozen=True)
@@ -598,7 +601,7 @@ class ShardedHierarchy:
     * ``sync_round(middles, top_weights)``: the synchronous hierarchy.
     """
 
-    def __init__(self, model, group=None, device: Optional[torch.device] = None, *, fracs=DEFAULT_FRACS,
+    def __init__(self, model, group=None, device: Optional[torch.device] = None, *, fracs=HIER_FRACS,
                  align: int = ALIGN_ELEMS, round_fn=None, sync_round_fn=None):
         self.comm = _Comm(group)
         self.plan = ShardPlan(model, self.comm.world, self.comm.rank, align=align, fracs=fracs)

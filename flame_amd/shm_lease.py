@@ -55,6 +55,11 @@ def remove(name: str) -> None:
         _remove_locked(name)
 
 
+def active() -> bool:
+    """Is any shared-memory segment open (could any host tensor alias one)?"""
+    return bool(_starts)
+
+
 def segment_of(ptr: int):
     """Name of the open segment containing host address ``ptr`` (or None)."""
     if not _starts:

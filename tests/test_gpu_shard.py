@@ -167,7 +167,7 @@ def _hier_fixture_worker(rank, world, port, q):
         rnd = fx.meta["round"]
         top_w0 = S.to_dev(fx.weights("top_w0"), DEV)
         hier = shard.ShardedHierarchy(top_w0, align=8)
-        ok = hier.plan.n_waves == 3
+        ok = hier.plan.n_waves == 2
         dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=hier.plan)
         middles = []
         for mid in range(2):
@@ -218,7 +218,7 @@ def _hier_random_worker(rank, world, port, q):
         ups = [[_update(g, tmpl, 0) for _ in range(C)] for _ in range(M)]
         stale = [[(m + t) % 4 for t in range(C)] for m in range(M)]
         hier = shard.ShardedHierarchy(tmpl, device=torch.device(DEV))
-        ok = hier.plan.n_waves == 3
+        ok = hier.plan.n_waves == 2
         for own in (True, False):
             # sharded: rank-local slab caches
             dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=M * C, shard=hier.plan)

@@ -251,7 +251,7 @@ def _hier_worker(rank, world, port, q):
         top_w0 = fx.weights("top_w0")
         hier = shard.ShardedHierarchy(top_w0, device=torch.device("cpu"), align=8,
                                       round_fn=S.oracle_hierarchy_round)
-        ok = ok and hier.plan.n_waves == 3 and any(not s.tail for s in hier.plan.subs)
+        ok = ok and hier.plan.n_waves == 2 and any(not s.tail for s in hier.plan.subs)
         middles = []
         for mid in range(2):
             opt, agg = hier.middle_optimizer(O.OracleFedBuff()), None
