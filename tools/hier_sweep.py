@@ -22,6 +22,7 @@ VDIR = os.path.join(ROOT, "build", "hvariants")
 
 VARIANTS = {
     "base": {},
+    "r01": {"FLAME_HBATCH": 1, "FLAME_HCU16": 8},     # round 1's kernel: stores per middle, unroll 8
     "hcu4": {"FLAME_HCU16": 4},
     "hcu2": {"FLAME_HCU16": 2},
     "pf": {"FLAME_HPF": 1},
