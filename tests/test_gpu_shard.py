@@ -357,3 +357,67 @@ def test_hierarchy_tiled_middles_equal_rows(mode):
         S.assert_bitwise(f"mid{m}", a[3][m], b[3][m])
     if a[2] is not None:
         S.assert_bitwise("top agg", a[2], b[2])
+
+
+# ---------------------------------------------------------------- the RCCL code path
+def _rccl_world1_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from flame_amd import engine, shard
+        from flame_amd.ingest import DeviceUpdateCache
+        from flame_amd.optimizers import optimizer_provider
+        g = torch.Generator().manual_seed(57)
+        # several large keys: every wave holds pieces of more than one key -> one coalesced
+        # group of in-place all-gathers per wave (RCCL's allgather_into_tensor_coalesced)
+        tmpl = {"a": torch.randn(300_001, generator=g), "b": torch.randn(200_003, generator=g),
+                "c": torch.randn(150_000, generator=g).bfloat16(), "d": torch.randn(99_999, generator=g)}
+        opt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=torch.device(DEV), align=1024)
+        opt.set_layout(tmpl)
+        multi = [w for w in range(opt.plan.n_waves)
+                 if len({opt.plan.by_name[n].key for n in opt.plan.wave_names[w] if not opt.plan.by_name[n].tail}) > 1]
+        ok = bool(multi)
+        cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=opt.plan)
+        single = optimizer_provider.get("fedavg")
+        ws = {k: v.to(DEV) for k, v in tmpl.items()}
+        wr = {k: v.clone() for k, v in ws.items()}
+        for r in range(2):
+            ups = [_update(g, tmpl, i) for i in range(5)]
+            cb = S.SortedCache()
+            for i, u in enumerate(ups):
+                cache[f"t{i}"] = S.TR(u, 3 + i)
+                cb[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, 3 + i)
+            ws = opt.do(ws, cache, total=25)
+            wr = single.do(wr, cb, total=25)
+            torch.cuda.synchronize()
+            ok = ok and all(_eq(ws[k], wr[k]) for k in tmpl)
+        # FedAdam: current_weights gathered into new tensors through the same coalesced path
+        fa = shard.ShardedOptimizer(optimizer_provider.get("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3),
+                                    device=torch.device(DEV), align=1024)
+        fb = optimizer_provider.get("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+        wa, wb = {k: v.clone() for k, v in ws.items()}, {k: v.clone() for k, v in ws.items()}
+        for r in range(3):
+            ups = [_update(g, tmpl, i) for i in range(4)]
+            ca, cb = S.SortedCache(), S.SortedCache()
+            for i, u in enumerate(ups):
+                ca[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, 2 + i)
+                cb[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, 2 + i)
+            wa = fa.do({k: v.clone() for k, v in wa.items()}, ca, total=14)
+            wb = fb.do({k: v.clone() for k, v in wb.items()}, cb, total=14)
+            torch.cuda.synchronize()
+            ok = ok and all(_eq(wa[k], wb[k]) for k in tmpl)
+        q.put((rank, bool(ok)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rccl_world1_coalesced_inplace_gathers():
+    """The product's RCCL path (backend nccl = RCCL) as a world-1 group: in-place
+    all_gather_into_tensor, coalesced across the keys of a wave, for FedAvg (into the
+    caller's tensors) and FedAdam (into new tensors) == one process, bitwise."""
+    _two_ranks(_rccl_world1_worker, world=1)
