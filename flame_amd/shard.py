@@ -170,7 +170,10 @@ class ShardPlan:
         * a dict of tensors (device, pinned or pageable host): views / slices.
         """
         slab = getattr(weights, "slab", None)
-        if slab is not None and getattr(weights, "ranges", None) is None:
+        rng = getattr(weights, "ranges", None)
+        if slab is not None and (rng is self.full_ranges or rng is self.self_ranges):
+            return weights                      # already this plan's slices (a SlabRef it made)
+        if slab is not None and rng is None:
             if self._is_local_slab(slab):
                 return weights
             if all(s.key in slab.meta and slab.meta[s.key][0] == self.dtypes[s.key]
