@@ -101,7 +101,7 @@ class ShardPlan:
                     per = (g1 - g0) // self.world
                     lo = g0 + self.rank * per
                     subs.append(Sub(f"{k}#{g0}", k, w, g0, g1, lo, lo + per, False))
-            if m < self.numel[k]:
+            if m < self.numel[k] or self.numel[k] == 0:      # (an empty key keeps an empty tail)
                 subs.append(Sub(f"{k}#tail", k, -1, m, self.numel[k], m, self.numel[k], True))
             off += m
         used = sorted({s.wave for s in subs if not s.tail})

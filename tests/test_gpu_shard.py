@@ -64,7 +64,8 @@ def _init(rank, world, port):
 def _model(g, P):
     return {"w": torch.randn(P, generator=g), "m": torch.randn(31, 129, generator=g),
             "bf": torch.randn(9001, generator=g).bfloat16(), "h": torch.randn(777, generator=g).half(),
-            "d": torch.randn(2051, generator=g).double(), "nbt": torch.tensor(3, dtype=torch.int64)}
+            "d": torch.randn(2051, generator=g).double(), "nbt": torch.tensor(3, dtype=torch.int64),
+            "z": torch.empty(0, 3)}
 
 
 def _update(g, tmpl, i, scale=1e-2):

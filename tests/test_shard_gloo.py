@@ -63,7 +63,7 @@ def _model(g, shapes, scale):
 def test_shard_plan_partitions_every_key(world, align):
     shapes = {"conv": ((32, 1, 3, 3), torch.float32), "bias": ((32,), torch.float32),
               "fc1": ((128, 9216), torch.float32), "big": ((3, 1_000_003), torch.bfloat16),
-              "nbt": ((), torch.int64), "fc2": ((10, 128), torch.float16)}
+              "nbt": ((), torch.int64), "fc2": ((10, 128), torch.float16), "empty": ((0, 4), torch.float32)}
     model = {k: torch.empty(s, dtype=dt, device="meta") for k, (s, dt) in shapes.items()}
     plans = [shard.ShardPlan(model, world, r, align=align) for r in range(world)]
     unit = world * align
