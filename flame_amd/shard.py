@@ -45,7 +45,7 @@ from typing import Dict, Optional
 
 import torch
 
-from . import engine
+from . import engine, shm_lease
 
 ALIGN_ELEMS = 2048               # a multiple of every kernel chunk / slab tile (1024 fp32, 2048 bf16 / fp16)
 DEFAULT_FRACS = (0.75, 0.20, 0.05)
@@ -142,9 +142,11 @@ class ShardPlan:
     def slice_update(self, weights):
         """This rank's slices of a full client update as plain views / host slices (what
         ``DeviceUpdateCache(shard=plan)`` copies to the device)."""
-        for k in weights.keys():
+        for k, t in weights.items():
             if k not in self.numel:
                 raise KeyError(k)
+            if isinstance(t, torch.Tensor) and not t.is_cuda:
+                shm_lease.check_live(t)     # the slices below no longer carry the segment's stamp
         out = collections.OrderedDict()
         for s in self.subs:
             if s.key in weights:
