@@ -76,6 +76,9 @@ namespace {
 #ifndef FLAME_HDIAG
 #define FLAME_HDIAG 0     // DIAGNOSTIC sweep variants only: 1 = skip middle-weight stores, 2 = also skip their loads
 #endif
+#ifndef FLAME_BUFLD
+#define FLAME_BUFLD 0     // sweep: client loads as buffer loads, cache policy FLAME_BUFLD - 1 (0 = global loads)
+#endif
 #ifndef FLAME_HBATCH
 #define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
                           // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
@@ -324,6 +327,27 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
     auto rate64 = [&](int c) -> double { if constexpr (DT == FLAME_F64) return r64[c]; else return 0.0; };
     auto load_client = [&](int c, T (&x)[kVPT][EPT]) {
         const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[c]) + coff);
+#if FLAME_BUFLD
+        if constexpr (VEC) {
+            // buffer loads: the client's chunk base (wave-uniform) in a scalar resource, the
+            // lane's byte offset in one VGPR; FLAME_BUFLD - 1 = cache policy (sc0 1, nt 2, sc1 16)
+            const int32_t lane_b = static_cast<int32_t>(threadIdx.x) * EPT * static_cast<int32_t>(sizeof(T));
+            const uint64_t wb = cp[c] + static_cast<uint64_t>(coff - lane_b);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb));
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb >> 32));
+            void* base = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) {
+                u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, lane_b + v * static_cast<int32_t>(VS * sizeof(T)), 0,
+                                                             FLAME_BUFLD - 1);
+                V16 t;
+                t.w[0] = q[0]; t.w[1] = q[1]; t.w[2] = q[2]; t.w[3] = q[3];
+                unpack<T, EPT>(t, x[v]);
+            }
+            return;
+        }
+#endif
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             if constexpr (VEC) {

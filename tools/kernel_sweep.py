@@ -62,6 +62,12 @@ VARIANTS = {
     "occ5": {"FLAME_OCC_LDS": 32768},
     "occ6": {"FLAME_OCC_LDS": 27136},
     "xcd": {"FLAME_XCD_SWIZZLE": 1},
+    # client loads as buffer loads with an explicit cache policy (sc0 1, nt 2, sc1 16; value - 1)
+    "bl_none": {"FLAME_BUFLD": 1},
+    "bl_nt": {"FLAME_BUFLD": 3},
+    "bl_sc1nt": {"FLAME_BUFLD": 19},
+    "bl_sc01nt": {"FLAME_BUFLD": 20},
+    "bl_sc0nt": {"FLAME_BUFLD": 4},
 }
 
 
