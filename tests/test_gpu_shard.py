@@ -422,3 +422,63 @@ def test_sharded_rccl_world1_coalesced_inplace_gathers():
     all_gather_into_tensor, coalesced across the keys of a wave, for FedAvg (into the
     caller's tensors) and FedAdam (into new tensors) == one process, bitwise."""
     _two_ranks(_rccl_world1_worker, world=1)
+
+
+def _resnetish(g):
+    """A ResNet-like state_dict: many keys of mixed sizes, BatchNorm buffers incl. int64."""
+    out = {}
+    shapes = [(64, 3, 7, 7)] + [(64, 64, 3, 3)] * 4 + [(128, 64, 3, 3), (128, 128, 3, 3), (128, 64, 1, 1)] + \
+        [(256, 128, 3, 3), (256, 256, 3, 3)] + [(1000, 256), (1000,)]
+    for i, s in enumerate(shapes):
+        out[f"layer{i}.weight"] = torch.randn(s, generator=g)
+        if len(s) == 4:
+            c = s[0]
+            out[f"bn{i}.weight"] = torch.randn(c, generator=g)
+            out[f"bn{i}.bias"] = torch.randn(c, generator=g)
+            out[f"bn{i}.running_mean"] = torch.randn(c, generator=g)
+            out[f"bn{i}.running_var"] = torch.rand(c, generator=g)
+            out[f"bn{i}.num_batches_tracked"] = torch.tensor(7, dtype=torch.int64)
+    return out
+
+
+def _many_keys_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from flame_amd import shard
+        from flame_amd.ingest import DeviceUpdateCache
+        from flame_amd.optimizers import optimizer_provider
+        g = torch.Generator().manual_seed(81)
+        tmpl = _resnetish(g)
+        ok = len(tmpl) > 50
+        for sort in ("fedavg", "fedadam"):
+            kw = dict(beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3) if sort == "fedadam" else {}
+            opt = shard.ShardedOptimizer(optimizer_provider.get(sort, **kw), device=torch.device(DEV))
+            opt.set_layout(tmpl)
+            ok = ok and sum(1 for s in opt.plan.subs if not s.tail) > 0
+            cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=opt.plan)
+            single = optimizer_provider.get(sort, **kw)
+            ws = {k: v.to(DEV) for k, v in tmpl.items()}
+            wr = {k: v.clone() for k, v in ws.items()}
+            for r in range(3):
+                ups = [_update(g, tmpl, 10 * r + i) for i in range(6)]
+                cb = S.SortedCache()
+                for i, u in enumerate(ups):
+                    cache[f"t{i}"] = S.TR(u, 5 + i)
+                    cb[f"t{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, 5 + i)
+                ws = opt.do({k: v.clone() for k, v in ws.items()}, cache, total=45)
+                wr = single.do({k: v.clone() for k, v in wr.items()}, cb, total=45)
+                torch.cuda.synchronize()
+                ok = ok and list(ws) == list(wr) and all(_eq(ws[k], wr[k]) for k in tmpl)
+        q.put((rank, bool(ok)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_many_keys_resnet_like_two_ranks_one_gpu():
+    """A ResNet-like state_dict (62 keys: conv / fc weights, BatchNorm affine + running stats +
+    int64 num_batches_tracked) through ShardedOptimizer(FedAvg) and (FedAdam, which promotes
+    the int64 buffers) with rank-local slab caches: == one process, bitwise, 3 rounds."""
+    _two_ranks(_many_keys_worker)
