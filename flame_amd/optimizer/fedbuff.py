@@ -68,7 +68,14 @@ class DeferredAggregate(collections.abc.Mapping):
         """Reduce every queued arrival (one launch per dtype)."""
         if not self._pending:
             return
-        if self._data is None:
+        if self._data is None and not _uniform(self):
+            # later arrivals carry a subset of the first one's keys, or other dtypes: the
+            # reference adds them key by key (fedbuff.py:143-157), so does accumulate()
+            (w0, r0), rest = self._pending[0], self._pending[1:]
+            self._data = collections.OrderedDict(engine.first_tmp(w0, r0))
+            if rest:
+                engine.accumulate(self._data, rest)
+        elif self._data is None:
             # None-start: agg = tmp(first) (fedbuff.py:139-140,154-155), then += the rest
             device = engine.pick_device(*[w for w, _ in self._pending])
             self._data = collections.OrderedDict(

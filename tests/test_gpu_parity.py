@@ -1552,3 +1552,83 @@ def test_fedopt_argmeta_equals_device_table(sort, dtype):
             engine.ARGMETA = True
     for r, (a, b) in enumerate(zip(results[True], results[False])):
         S.assert_bitwise(f"{sort}/{dtype}/round{r}", a, b)
+
+
+def test_key_subset_arrivals():
+    """Updates carrying a SUBSET of the model's keys (fedavg.py:93 / fedbuff.py:143 add
+    ``for k, v in tres.weights.items()``: a key a client did not send keeps its value).
+    FedAvg and FedBuff bitwise vs the oracle -- FedBuff's deferred None-start aggregate
+    with later arrivals lacking keys included -- FedAdam within the §8(c) tolerance; an
+    update naming a key the aggregate lacks raises KeyError like the reference's
+    ``agg[k] += tmp``."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(2024)
+    shapes = {"a": ((1000,), torch.float32), "b": ((37,), torch.bfloat16), "n": ((3,), torch.int64)}
+
+    def rnd(k, scale=1.0):
+        s, dt = shapes[k]
+        if dt == torch.int64:
+            return torch.randint(0, 50, s, generator=g)
+        return (torch.randn(s, generator=g, dtype=torch.float64) * scale).to(dt)
+
+    subsets = [("a", "b", "n"), ("a", "n"), ("b",), ("a", "b")]
+    base = {k: rnd(k) for k in shapes}
+    cl = [{k: rnd(k, 1e-2) for k in ks} for ks in subsets]
+    counts = [3, 5, 7, 11]
+    total = sum(counts)
+
+    def cache_of(ws, cnts, vers=None):
+        c = S.SortedCache()
+        for i, (w, n) in enumerate(zip(ws, cnts)):
+            c[f"{i:03d}"] = S.TR({k: v.to(DEV) for k, v in w.items()}, n, 0 if vers is None else vers[i])
+        return c
+
+    def cpu_cache(ws, cnts, vers=None):
+        c = S.SortedCache()
+        for i, (w, n) in enumerate(zip(ws, cnts)):
+            c[f"{i:03d}"] = S.TR({k: v.clone() for k, v in w.items()}, n, 0 if vers is None else vers[i])
+        return c
+
+    # FedAvg
+    got = make_amd("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache_of(cl, counts), total=total)
+    exp = O.OracleFedAvg().do({k: v.clone() for k, v in base.items()}, cpu_cache(cl, counts), total=total)
+    S.assert_bitwise("fedavg subsets", got, exp)
+
+    # FedBuff: None-start from the full arrival, then subset arrivals, one do() each; scale_add
+    vers = [2, 1, 0, 2]
+    for defer in (True, False):
+        opt, ref = make_amd("fedbuff", defer=defer), O.OracleFedBuff()
+        agg = eagg = None
+        for i in range(len(cl)):
+            agg = opt.do(agg, cache_of([cl[i]], [1], [vers[i]]), total=1, version=2)
+            eagg = ref.do(eagg, cpu_cache([cl[i]], [1], [vers[i]]), total=1, version=2)
+        S.assert_bitwise(f"fedbuff subsets defer={defer}", {k: agg[k] for k in shapes}, eagg)
+        bw = {k: v.to(DEV) for k, v in base.items() if v.is_floating_point()}
+        ebw = {k: v.clone() for k, v in base.items() if v.is_floating_point()}
+        opt.scale_add_agg_weights(bw, agg, 4)
+        ref.scale_add_agg_weights(ebw, eagg, 4)
+        S.assert_bitwise(f"fedbuff scale_add subsets defer={defer}", bw, ebw)
+    # several subset arrivals queued in ONE deferred aggregate before its first read
+    opt, ref = make_amd("fedbuff"), O.OracleFedBuff()
+    agg = opt.do(None, cache_of([cl[0]], [1], [1]), total=1, version=2)
+    eagg = ref.do(None, cpu_cache([cl[0]], [1], [1]), total=1, version=2)
+    agg = opt.do(agg, cache_of(cl[1:], [1] * 3, vers[1:]), total=3, version=2)
+    eagg = ref.do(eagg, cpu_cache(cl[1:], [1] * 3, vers[1:]), total=3, version=2)
+    S.assert_bitwise("fedbuff queued subsets", {k: agg[k] for k in shapes}, eagg)
+    with pytest.raises(KeyError):
+        opt.do(agg, cache_of([{"zz": torch.ones(2)}], [1]), total=1, version=2)
+
+    # FedAdam on fp32 keys (the kernel path; the SURVEY §8(c) contract is stated for fp32)
+    fl = {k: v.float() for k, v in base.items() if v.is_floating_point()}
+    fcl = [{k: v.float() for k, v in w.items() if k in fl} for w in cl]
+    opt = make_amd("fedadam")
+    ref = O.OracleFedOPT("fedadam")
+    cur = {k: v.to(DEV) for k, v in fl.items()}
+    ecur = {k: v.clone() for k, v in fl.items()}
+    for r in range(3):
+        cur = opt.do({k: v.clone() for k, v in cur.items()}, cache_of(fcl, counts), total=total)
+        ecur = ref.do({k: v.clone() for k, v in ecur.items()}, cpu_cache(fcl, counts), total=total)
+        if r == 0:
+            S.assert_bitwise("fedadam subsets r0", cur, ecur)
+        else:
+            S.assert_close_fedopt(f"fedadam subsets r{r}", cur, ecur, elementwise=r == 1)
