@@ -83,6 +83,22 @@ namespace {
 #define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
                           // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
 #endif
+#ifndef FLAME_HLDS
+#define FLAME_HLDS 1      // hierarchy kernel, launches with >= FLAME_HLDS_MIN_MIDS middles: 1 = hold a store
+                          // group of FLAME_HLDS_BATCH middles' weights in LDS (4 KiB each per workgroup,
+                          // 2 workgroups per CU) instead of FLAME_HBATCH in registers, arrivals unrolled
+                          // by FLAME_HLDS_CU16 (C5 shard: 20.99 -> 19.51 ms, 0.7 % above the no-store
+                          // diagnostic; tools/hier_sweep.py, profiles/r02_hier_lds_sweep.log)
+#endif
+#ifndef FLAME_HLDS_BATCH
+#define FLAME_HLDS_BATCH 16
+#endif
+#ifndef FLAME_HLDS_CU16
+#define FLAME_HLDS_CU16 6
+#endif
+#ifndef FLAME_HLDS_MIN_MIDS
+#define FLAME_HLDS_MIN_MIDS 16
+#endif
 #ifndef FLAME_HST
 #define FLAME_HST FLAME_ST_NT  // hierarchy kernel: store policy of the middle weights (encoding of FLAME_ST_NT)
 #endif
@@ -815,7 +831,10 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
 //   a = w_m + tmp(c_{m,0}, r_{m,0}) + ...;  w_m' = a;  d_m = w_m' - w_m
 // and the top's FedAvg adds tmp(d_m, top_rates[m]) to the top weights (top_agg_in).
 template <int DT> __device__ __forceinline__ float rnd(float x);
-template <int DT, int CU, bool SYNC>
+// (HL instantiations: the middle loop stays rolled -- its group lives in LDS, not registers)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
+template <int DT, int CU, bool SYNC, int HB, bool HL>
 __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __restrict__ segs, int n_segs,
                                                   int n_mids, int n_clients, const uint64_t* __restrict__ mid_w,
                                                   const uint64_t* __restrict__ mid_delta,
@@ -858,16 +877,19 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                 for (int j = 0; j < EPT; ++j) top[v][j] = X::ld(b[j]);
             }
         }
-        // middles in groups of kHB: a group's middle-weight stores are issued together after
-        // its reductions (FLAME_HBATCH; 1 = store each middle's weights right after its reduction)
+        // middles in groups of HB: a group's middle-weight stores are issued together after its
+        // reductions (1 = store each middle's weights right after its reduction).  HL: the group's
+        // weights wait in LDS (lane-private slots, no barrier) rather than in registers -- long
+        // store bursts at 2 workgroups per CU
+        __shared__ V16 held[HL ? HB * kVPT * kBlock : 1];
 #pragma unroll 1
-        for (int m0 = 0; m0 < n_mids; m0 += kHB) {
-            V16 pend[kHB][kVPT];
-            const int nb = n_mids - m0 < kHB ? n_mids - m0 : kHB;   // middles in this group
+        for (int m0 = 0; m0 < n_mids; m0 += HB) {
+            V16 pend[HL ? 1 : HB][kVPT];
+            const int nb = n_mids - m0 < HB ? n_mids - m0 : HB;   // middles in this group
 #pragma unroll
-            for (int u = 0; u < kHB; ++u) {
+            for (int u = 0; u < HB; ++u) {
             const int m = m0 + u;
-            if (kHB > 1 && m >= n_mids) break;
+            if (HB > 1 && m >= n_mids) break;
             T* wp = mid_ptr(m);
 #if FLAME_HPF
             V16 wv[kVPT];
@@ -915,22 +937,26 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                         top[v][j] = have_top ? X::add(top[v][j], t) : t;
                     }
                 }
-                pend[u][v] = pack<T, EPT>(w);
+                if constexpr (HL) held[(u * kVPT + v) * kBlock + threadIdx.x] = pack<T, EPT>(w);
+                else pend[u][v] = pack<T, EPT>(w);
                 if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
             }
             have_top = true;
             }
             if (!(flags & FLAME_HIER_MID_READONLY)) {
 #pragma unroll
-                for (int u = 0; u < kHB; ++u) {
+                for (int u = 0; u < HB; ++u) {
                     if (u >= nb) break;
                     T* wp = mid_ptr(m0 + u);       // re-read from the (scalar) pointer table
 #pragma unroll
                     for (int v = 0; v < kVPT; ++v) {
+                        V16 pv;
+                        if constexpr (HL) pv = held[(u * kVPT + v) * kBlock + threadIdx.x];
+                        else pv = pend[u][v];
 #if FLAME_HDIAG
-                        if (__builtin_expect(pend[u][v].w[0] == 0x12345u && pend[u][v].w[1] == 0x54321u, 0))
+                        if (__builtin_expect(pv.w[0] == 0x12345u && pv.w[1] == 0x54321u, 0))
 #endif
-                        st_pol<FLAME_HST>(wp + v * VS, pend[u][v]);
+                        st_pol<FLAME_HST>(wp + v * VS, pv);
                     }
                 }
             }
@@ -1013,7 +1039,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
         }
 }
 
-template <int DT, int CU, bool SYNC>
+template <int DT, int CU, bool SYNC, int HB, bool HL>
 __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
                                                     int n_mids, int n_clients, const uint64_t* __restrict__ mid_w,
                                                     const uint64_t* __restrict__ mid_delta,
@@ -1022,7 +1048,7 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __
                                                     const float* __restrict__ mid_goal,
                                                     const float* __restrict__ top_rates, float top_goal,
                                                     unsigned flags) {
-    hier_fedbuff_body<DT, CU, SYNC>(segs, n_segs, n_mids, n_clients, mid_w, mid_delta, clients, mid_rates, mid_goal,
+    hier_fedbuff_body<DT, CU, SYNC, HB, HL>(segs, n_segs, n_mids, n_clients, mid_w, mid_delta, clients, mid_rates, mid_goal,
                                     top_rates, top_goal, flags);
 }
 
@@ -1035,12 +1061,13 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel_argmeta(const ArgMeta meta, 
                                                             float top_goal, unsigned flags) {
     (void)sizeof(meta);     // read in place in the kernarg segment (see agg_reduce_kernel_argmeta)
     const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    hier_fedbuff_body<DT, CU, SYNC>(reinterpret_cast<const flame_hier_segment*>(w), n_segs, n_mids, n_clients,
+    hier_fedbuff_body<DT, CU, SYNC, kHB, false>(reinterpret_cast<const flame_hier_segment*>(w), n_segs, n_mids, n_clients,
                                     w + o_mid_w, o_mid_delta >= 0 ? w + o_mid_delta : nullptr, w + o_clients,
                                     reinterpret_cast<const float*>(w + o_mid_rates),
                                     reinterpret_cast<const float*>(w + o_mid_goal),
                                     reinterpret_cast<const float*>(w + o_top_rates), top_goal, flags);
 }
+#pragma clang diagnostic pop
 
 // ---------------------------------------------------------------- FedDyn server round
 // One pass over a FedDyn aggregation round (optimizer/feddyn.py:90-113,125-139), driven
@@ -1208,6 +1235,8 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 constexpr int kClientUnroll = FLAME_CU;
 constexpr int kClientUnroll16 = FLAME_CU16;
 constexpr int kHierUnroll16 = FLAME_HCU16;
+constexpr int kHierLdsUnroll16 = FLAME_HLDS_CU16;
+constexpr int kHBL = FLAME_HLDS_BATCH;
 
 int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
     if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
@@ -1462,18 +1491,24 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     auto w = reinterpret_cast<const uint64_t*>(mid_w);
     auto d = reinterpret_cast<const uint64_t*>(mid_delta);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-#define FLAME_HIER_LAUNCH(DT, CUV)                                                                             \
+#define FLAME_HIER_LAUNCH1(DT, CUV, HB, HL)                                                                    \
     if (sync)                                                                                                  \
-        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, n_mids,     \
-                           n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);              \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true, HB, HL>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, \
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);      \
     else                                                                                                       \
-        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, n_mids,    \
-                           n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false, HB, HL>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, \
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+    // many middles (config 5: 64 per GPU): LDS-held store groups; a few (a single FedBuff's fused
+    // scale_add, small hierarchies): register groups, no LDS, full occupancy
+#define FLAME_HIER_LAUNCH(DT, CUV, CUL)                                                                        \
+    if (FLAME_HLDS && n_mids >= FLAME_HLDS_MIN_MIDS) { FLAME_HIER_LAUNCH1(DT, CUL, kHBL, true) }             \
+    else { FLAME_HIER_LAUNCH1(DT, CUV, kHB, false) }
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
     switch (dtype) {
-    case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll) break;
-    case FLAME_BF16: FLAME_HIER_LAUNCH(FLAME_BF16, kHierUnroll16) break;
-    case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16) break;
+    case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll, kClientUnroll) break;
+    case FLAME_BF16: FLAME_HIER_LAUNCH(FLAME_BF16, kHierUnroll16, kHierLdsUnroll16) break;
+    case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16, kHierLdsUnroll16) break;
+#undef FLAME_HIER_LAUNCH1
 #undef FLAME_HIER_LAUNCH
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);

@@ -130,3 +130,43 @@ extern "C" int probe_mix_region(const void* p, void* dst, int64_t blocks, int R,
     else hipLaunchKernelGGL((mix_region_kernel<0>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)p, (uint8_t*)dst, R);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Burst variant: workgroup w reads B groups of R contiguous 4 KiB steps, keeps each group's
+// result in LDS, and writes its B output blocks back to back at the end (dst + (w*B + g) *
+// 4 KiB) -- the same bytes as B workgroups of mix_region_kernel, with the writes gathered
+// into one burst per workgroup instead of one write after every R reads.  Dynamic LDS: B*4 KiB.
+__global__ __launch_bounds__(256) void mix_burst_kernel(const uint8_t* __restrict__ p, uint8_t* __restrict__ dst,
+                                                        int R, int B) {
+    extern __shared__ u4 held[];
+    const int64_t region = (int64_t)R * 4096;
+    for (int g = 0; g < B; ++g) {
+        const uint8_t* src = p + ((int64_t)blockIdx.x * B + g) * region + threadIdx.x * 16;
+        u4 acc = {0u, 0u, 0u, 0u};
+        int i = 0;
+        for (; i + 8 <= R; i += 8) {
+            u4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(src + (int64_t)(i + u) * 4096));
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc ^= v[u];
+        }
+        for (; i < R; ++i)
+            acc ^= __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(src + (int64_t)i * 4096));
+        held[g * 256 + threadIdx.x] = acc;
+    }
+    for (int g = 0; g < B; ++g) {
+        uint8_t* o = dst + ((int64_t)blockIdx.x * B + g) * 4096 + threadIdx.x * 16;
+        u4 v = held[g * 256 + threadIdx.x];
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(o), "v"(v) : "memory");
+    }
+}
+
+extern "C" int probe_mix_burst(const void* p, void* dst, int64_t wgs, int R, int B, void* stream) {
+    if (R < 1 || B < 1 || B > 36 || wgs < 1 || wgs > 0x7FFFFFFF) return 2;
+    if (hipFuncSetAttribute((const void*)mix_burst_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, B * 4096) !=
+        hipSuccess) return 3;
+    hipLaunchKernelGGL(mix_burst_kernel, dim3((unsigned)wgs), dim3(256), (size_t)B * 4096, (hipStream_t)stream,
+                       (const uint8_t*)p, (uint8_t*)dst, R, B);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -22,6 +22,7 @@ VDIR = os.path.join(ROOT, "build", "hvariants")
 
 VARIANTS = {
     "base": {},
+    "nolds": {"FLAME_HLDS": 0},                        # before the LDS-held store groups (round 2 first half)
     "r01": {"FLAME_HBATCH": 1, "FLAME_HCU16": 8},     # round 1's kernel: stores per middle, unroll 8
     "hcu4": {"FLAME_HCU16": 4},
     "hcu2": {"FLAME_HCU16": 2},
@@ -43,6 +44,24 @@ VARIANTS = {
     "hb4cu4": {"FLAME_HBATCH": 4, "FLAME_HCU16": 4},
     "hb6": {"FLAME_HBATCH": 6},
     "hb4hst0": {"FLAME_HBATCH": 4, "FLAME_HST": 0},
+    "lds16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16},
+    "lds24": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 24},
+    "lds32": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32},
+    "lds16cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 8},
+    "lds32cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32, "FLAME_HLDS_CU16": 8},
+    "lds32cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32, "FLAME_HLDS_CU16": 16},
+    "lds8cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 8},
+    "lds12cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 8},
+    "lds20cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 8},
+    "lds16cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 16},
+    "lds16cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 6},
+    "lds20cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 16},
+    "lds16cu4": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 4},
+    "lds16cu5": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 5},
+    "lds16cu7": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 7},
+    "lds20cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 6},
+    "lds18cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 18, "FLAME_HLDS_CU16": 6},
+    "lds14cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 14, "FLAME_HLDS_CU16": 6},
     "hdiag1": {"FLAME_HDIAG": 1},   # diagnostic: middle weights not stored (output not checked)
     "hdiag2": {"FLAME_HDIAG": 2},   # diagnostic: middle weights neither loaded nor stored
 }
@@ -165,7 +184,7 @@ def main():
                                   ctypes.c_void_p]
         pout = torch.zeros(4, dtype=torch.int32, device=dev)
         pbytes = slab.numel() * isz // 4096 * 4096
-    ref = None
+    refs = {}       # per mode (FedBuff / sync): every variant bitwise-equal to the first one of its mode
     for nm in names:
         if nm == "probe":
             continue
@@ -180,13 +199,14 @@ def main():
         else:
             mlog = mids.clone() if not tiled_mids else mids.permute(1, 0, 2).reshape(M, tiles * T)[:, :P].clone()
         got = (mlog, gw.clone(), top.clone())
-        if nm.startswith("hdiag") or nm.endswith(":sync"):
+        if nm.startswith("hdiag"):
             continue
-        if ref is None:
-            ref = got
-        elif not all(torch.equal(x.view(torch.int16), y.view(torch.int16)) for x, y in zip(got, ref)):
-            raise SystemExit(f"variant {nm} differs from {names[0]}")
-    del ref
+        mode = "sync" if nm.endswith(":sync") else "fedbuff"
+        if mode not in refs:
+            refs[mode] = (nm, got)
+        elif not all(torch.equal(x.view(torch.int16), y.view(torch.int16)) for x, y in zip(got, refs[mode][1])):
+            raise SystemExit(f"variant {nm} differs from {refs[mode][0]}")
+    del refs
     times = {nm: [] for nm in names}
     for r in range(args.rounds):
         for nm in names:
