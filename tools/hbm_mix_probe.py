@@ -6,6 +6,7 @@ for R in {2, 3, 9, 17, 33, 65, 257, 1025} over ~16 GB of reads, both store polic
 
     python tools/hbm_mix_probe.py
     python tools/hbm_mix_probe.py --burst   # R = 65, writes gathered B per workgroup (probe_mix_burst)
+    python tools/hbm_mix_probe.py --burst --small-r   # R = 2, 3 (FedDyn), separate or in-place writes
 """
 import ctypes
 import os
@@ -57,23 +58,27 @@ def main():
 def burst(L, src, read_bytes, st):
     """Same R : 1 read:write ratio, writes issued B at a time at the end of a workgroup."""
     L.probe_mix_burst.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_void_p]
-    for R in (65, 257):
-        for B in (1, 4, 16, 24, 32, 36, 1):
+                                  ctypes.c_int, ctypes.c_void_p]
+    cases = [(R, B, 0) for R in (65, 257) for B in (1, 4, 16, 24, 32, 36, 1)]
+    if "--small-r" in sys.argv:     # FedDyn's shapes: 2 reads (w, h) : 1 write (h'), in place or not
+        cases = [(R, B, ip) for R in (2, 3) for ip in (0, 1) for B in (1, 4, 8, 16, 24, 32, 1)]
+    for R, B, inplace in cases:
+        if True:
             wgs = read_bytes // (R * B * 4096)
             dst = torch.empty(wgs * B * 1024, dtype=torch.float32, device="cuda")
             ts = []
             for _ in range(int(os.environ.get("PROBE_REPS", "6"))):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                rc = L.probe_mix_burst(src.data_ptr(), dst.data_ptr(), wgs, R, B, st)
+                rc = L.probe_mix_burst(src.data_ptr(), dst.data_ptr(), wgs, R, B, inplace, st)
                 assert rc == 0, rc
                 e1.record()
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
             t = statistics.median(ts[1:])
             rb, wb = wgs * B * R * 4096, wgs * B * 4096
-            print(f"R {R:4d} : 1, writes in bursts of {B:2d} ({wgs} workgroups, LDS {B * 4} KiB): {t:8.3f} ms  "
+            print(f"R {R:4d} : 1, writes{' in place' if inplace else ''} in bursts of {B:2d} ({wgs} workgroups, "
+                  f"LDS {B * 4} KiB): {t:8.3f} ms  "
                   f"{(rb + wb) / t / 1e6:8.1f} GB/s", flush=True)
             del dst
 

@@ -135,8 +135,9 @@ extern "C" int probe_mix_region(const void* p, void* dst, int64_t blocks, int R,
 // result in LDS, and writes its B output blocks back to back at the end (dst + (w*B + g) *
 // 4 KiB) -- the same bytes as B workgroups of mix_region_kernel, with the writes gathered
 // into one burst per workgroup instead of one write after every R reads.  Dynamic LDS: B*4 KiB.
+// inplace: each output block overwrites the first block its group read (FedDyn's h' -> h).
 __global__ __launch_bounds__(256) void mix_burst_kernel(const uint8_t* __restrict__ p, uint8_t* __restrict__ dst,
-                                                        int R, int B) {
+                                                        int R, int B, int inplace) {
     extern __shared__ u4 held[];
     const int64_t region = (int64_t)R * 4096;
     for (int g = 0; g < B; ++g) {
@@ -156,17 +157,18 @@ __global__ __launch_bounds__(256) void mix_burst_kernel(const uint8_t* __restric
         held[g * 256 + threadIdx.x] = acc;
     }
     for (int g = 0; g < B; ++g) {
-        uint8_t* o = dst + ((int64_t)blockIdx.x * B + g) * 4096 + threadIdx.x * 16;
+        uint8_t* o = inplace ? const_cast<uint8_t*>(p) + ((int64_t)blockIdx.x * B + g) * region + threadIdx.x * 16
+                             : dst + ((int64_t)blockIdx.x * B + g) * 4096 + threadIdx.x * 16;
         u4 v = held[g * 256 + threadIdx.x];
         asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(o), "v"(v) : "memory");
     }
 }
 
-extern "C" int probe_mix_burst(const void* p, void* dst, int64_t wgs, int R, int B, void* stream) {
+extern "C" int probe_mix_burst(const void* p, void* dst, int64_t wgs, int R, int B, int inplace, void* stream) {
     if (R < 1 || B < 1 || B > 36 || wgs < 1 || wgs > 0x7FFFFFFF) return 2;
     if (hipFuncSetAttribute((const void*)mix_burst_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, B * 4096) !=
         hipSuccess) return 3;
     hipLaunchKernelGGL(mix_burst_kernel, dim3((unsigned)wgs), dim3(256), (size_t)B * 4096, (hipStream_t)stream,
-                       (const uint8_t*)p, (uint8_t*)dst, R, B);
+                       (const uint8_t*)p, (uint8_t*)dst, R, B, inplace);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
