@@ -105,6 +105,10 @@ namespace {
 #ifndef FLAME_DYN_CU
 #define FLAME_DYN_CU 4    // FedDyn kernel: program steps whose loads are issued together
 #endif
+#ifndef FLAME_DYN_LDS
+#define FLAME_DYN_LDS 0   // FedDyn kernel: > 0 = hold the updated histories of that many program steps in
+                          // LDS (4 KiB each per workgroup) and store them in one burst (multiple of FLAME_DYN_CU)
+#endif
 #ifndef FLAME_DYN_ST
 #define FLAME_DYN_ST FLAME_ST_NT  // FedDyn kernel: store policy of the updated histories
 #endif
@@ -1080,7 +1084,7 @@ __global__ FLAME_HIER_ATTR void hier_fedbuff_kernel_argmeta(const ArgMeta meta, 
 // then out = avg, cld = avg + mean.  Steps [0, n_phase1) run before [n_phase1, n_steps);
 // batched loads never cross that boundary, so a phase-2 step may re-read what a phase-1
 // step stored (history order != arrival order).
-template <int DT, int CU, bool VEC>
+template <int DT, int CU, bool VEC, int G>
 __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const uint64_t* __restrict__ row,
                                              const uint32_t* __restrict__ sflags, int n_steps, int n_phase1,
                                              float ra32, float rm32, double ra64, double rm64, int64_t e0,
@@ -1119,6 +1123,19 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
     };
     using out_pol = std::integral_constant<int, FLAME_ST_NT>;
     using hist_pol = std::integral_constant<int, FLAME_DYN_ST>;
+    // G > 0: updated histories wait in LDS (lane-private slots) and go out G steps at a time
+    constexpr bool HL = VEC && G > 0;
+    static_assert(!HL || G % CU == 0, "FLAME_DYN_LDS must be a multiple of FLAME_DYN_CU");
+    __shared__ V16 held[HL ? G * kVPT * kBlock : 1];
+    auto flush = [&](int q0, int q1) {
+#pragma unroll 1
+        for (int q = q0; q < q1; ++q) {
+            if (!(sflags[q] & FLAME_DYN_HOUT)) continue;
+            T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(row[static_cast<int64_t>(q) * 3 + 2]) + hoff);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) st_pol<FLAME_DYN_ST>(p + v * VS, held[((q - q0) * kVPT + v) * kBlock + threadIdx.x]);
+        }
+    };
     A avg[kVPT][EPT], mean[kVPT][EPT];
     {
         T b[kVPT][EPT];
@@ -1131,6 +1148,7 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
 #pragma unroll 1
     for (int phase = 0; phase < 2; ++phase) {
         const int end = phase ? n_steps : n_phase1;
+        int kg = phase ? n_phase1 : 0;       // first step whose history is still held (HL)
 #pragma unroll 1
         for (int k = phase ? n_phase1 : 0; k < end; k += CU) {
             const int nb = (end - k < CU) ? end - k : CU;
@@ -1165,13 +1183,26 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
 #pragma unroll
                             for (int j = 0; j < EPT; ++j) h[u][v][j] = w[u][v][j];
                     }
-                    store(reinterpret_cast<void*>(row[static_cast<int64_t>(k + u) * 3 + 2]), hoff, h[u], hist_pol{});
+                    if constexpr (HL) {
+#pragma unroll
+                        for (int v = 0; v < kVPT; ++v)
+                            held[((k + u - kg) * kVPT + v) * kBlock + threadIdx.x] = pack<T, EPT>(h[u][v]);
+                    } else {
+                        store(reinterpret_cast<void*>(row[static_cast<int64_t>(k + u) * 3 + 2]), hoff, h[u], hist_pol{});
+                    }
                 }
                 if (f & FLAME_DYN_MEAN) {
 #pragma unroll
                     for (int v = 0; v < kVPT; ++v)
 #pragma unroll
                         for (int j = 0; j < EPT; ++j) mean[v][j] = X::add(mean[v][j], X::tmp(h[u][v][j], rm32, rm64));
+                }
+            }
+            if constexpr (HL) {     // a full group, or the phase's last steps: store the held histories
+                const int k1 = k + nb;
+                if (k1 - kg >= G || k1 >= end) {
+                    flush(kg, k1);
+                    kg = k1;
                 }
             }
         }
@@ -1207,9 +1238,10 @@ __global__ __launch_bounds__(kBlock) void feddyn_kernel(const flame_dyn_segment*
     const uint64_t* row = steps + static_cast<int64_t>(s) * n_steps * 3;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     if (vec)
-        feddyn_chunk<DT, CU, true>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+        feddyn_chunk<DT, CU, true, FLAME_DYN_LDS>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff,
+                                                  hoff);
     else
-        feddyn_chunk<DT, 1, false>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+        feddyn_chunk<DT, 1, false, 0>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
 }
 
 // ---------------------------------------------------------------- synthetic generator

@@ -52,6 +52,13 @@ VARIANTS = {
     "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
     # FedDyn round kernel (bench.py --workload feddyn with FLAME_AMD_LIB=build/variants/lib_<name>.so)
     "dyncu2": {"FLAME_DYN_CU": 2},
+    # updated histories held in LDS, stored G steps at a time (tools/feddyn_sweep.py)
+    "dynlds8": {"FLAME_DYN_LDS": 8},
+    "dynlds16": {"FLAME_DYN_LDS": 16},
+    "dynlds32": {"FLAME_DYN_LDS": 32},
+    "dynlds16cu8": {"FLAME_DYN_LDS": 16, "FLAME_DYN_CU": 8},
+    "dynlds24cu8": {"FLAME_DYN_LDS": 24, "FLAME_DYN_CU": 8},
+    "dynlds12cu6": {"FLAME_DYN_LDS": 12, "FLAME_DYN_CU": 6},
     "dyncu8": {"FLAME_DYN_CU": 8},
     "dynst0": {"FLAME_DYN_ST": 0},
     "dynst1": {"FLAME_DYN_ST": 1},
