@@ -86,6 +86,8 @@ def parse():
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--hier-wave-quantum", default="on", choices=["on", "off"],
+                    help="sharded hierarchy: size the last wave to whole rounds of resident workgroups")
     ap.add_argument("--shard-fracs", default=None,
                     help="N>1: element fractions of the waves, e.g. 0.9,0.1 (default: flame_amd.shard's)")
     ap.add_argument("--force-shard", action="store_true",
@@ -581,6 +583,8 @@ def _collective_note(plan, world, itemsize):
     recv = sum((s.g1 - s.g0) - (s.hi - s.lo) for s in plan.subs if not s.tail) * itemsize
     return {"kind": "in-place all_gather_into_tensor per wave (RCCL over xGMI)" if world > 1 else "none (world 1)",
             "waves": plan.n_waves, "bytes_received_per_rank": recv,
+            "wave_elements_per_rank": [sum(s.hi - s.lo for s in plan.subs if s.wave == w and not s.tail)
+                                       for w in range(plan.n_waves)],
             "replicated_tail_elements": sum(s.hi - s.lo for s in plan.subs if s.tail)}
 
 
@@ -666,7 +670,9 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
     if args.hier_mode not in ("fused", "sync"):
         raise SystemExit("multi-GPU hier bench: --hier-mode fused or sync (the product's ShardedHierarchy)")
     hier = shard.ShardedHierarchy({"model": torch.empty(G, dtype=dt, device="meta")}, device=dev,
-                                  fracs=_fracs(args, shard, shard.HIER_FRACS))
+                                  fracs=_fracs(args, shard, shard.HIER_FRACS),
+                                  middles=M if args.hier_wave_quantum == "on" else None,
+                                  sync=args.hier_mode == "sync")
     plan = hier.plan
     store, client_w = _local_slab(plan, M * C, dev, args.seed + 4, 1e-2)
     gw = torch.empty(G, dtype=dt, device=dev)

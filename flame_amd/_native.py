@@ -32,7 +32,7 @@ SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
     "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
-    "flame_feddyn_round", "flame_synth_fill",
+    "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
 )
 
@@ -81,6 +81,8 @@ def lib() -> ctypes.CDLL:
     L.flame_hier_fedbuff.argtypes = [ctypes.c_int, u32, vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, f32, vp]
     L.flame_hier_fedbuff_argmeta.restype = ctypes.c_int
     L.flame_hier_fedbuff_argmeta.argtypes = [ctypes.c_int, u32, vp, i64, i32, i64, i32, i32] + [i64] * 6 + [f32, vp]
+    L.flame_hier_resident_per_cu.restype = ctypes.c_int
+    L.flame_hier_resident_per_cu.argtypes = [ctypes.c_int, u32, i32]
     L.flame_feddyn_round.restype = ctypes.c_int
     L.flame_feddyn_round.argtypes = [ctypes.c_int, vp, i32, i64, vp, vp, i32, i32, ctypes.c_double,
                                      ctypes.c_double, vp]

@@ -1595,6 +1595,31 @@ int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta,
     return check_launch("flame_hier_fedbuff_argmeta");
 }
 
+int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
+    if (n_mids < 1) return -set_err(FLAME_EINVAL, "flame_hier_resident_per_cu: n_mids < 1");
+    const bool sync = (flags & FLAME_HIER_SYNC) != 0;
+    const bool lds = FLAME_HLDS && n_mids >= FLAME_HLDS_MIN_MIDS;
+    const void* f = nullptr;
+    // the instantiation FLAME_HIER_LAUNCH in flame_hier_fedbuff picks for these arguments
+#define FLAME_HIER_PICK(DT, CUV, CUL)                                                                          \
+    if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)          \
+                      : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, false, kHBL, true>);        \
+    else f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, true, kHB, false>)              \
+                  : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, false, kHB, false>);
+    switch (dtype) {
+    case FLAME_F32: FLAME_HIER_PICK(FLAME_F32, kClientUnroll, kClientUnroll) break;
+    case FLAME_BF16: FLAME_HIER_PICK(FLAME_BF16, kHierUnroll16, kHierLdsUnroll16) break;
+    case FLAME_F16: FLAME_HIER_PICK(FLAME_F16, kHierUnroll16, kHierLdsUnroll16) break;
+#undef FLAME_HIER_PICK
+    default:
+        return -set_err(FLAME_ENOTSUP, "flame_hier_resident_per_cu: dtype %d not supported (f32, bf16, f16)", dtype);
+    }
+    int blocks = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, kBlock, FLAME_OCC_LDS);
+    if (e != hipSuccess) return -set_err(FLAME_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
+    return blocks < 1 ? 1 : blocks;
+}
+
 int flame_feddyn_round(int dtype, const flame_dyn_segment* segs, int32_t n_segs, int64_t n_chunks,
                        const void* const* steps, const uint32_t* step_flags, int32_t n_steps, int32_t n_phase1,
                        double rate_avg, double rate_mean, void* stream) {

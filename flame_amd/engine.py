@@ -631,6 +631,14 @@ def hier_fedbuff_(segs: Sequence[HierSeg], code: int, mid_rates, mid_goals, top_
     keep.append(dm)
 
 
+def hier_resident_per_cu(code: int, n_mids: int, sync: bool = False) -> int:
+    """Resident workgroups per CU of the flame_hier_fedbuff launch for these arguments."""
+    r = int(N.lib().flame_hier_resident_per_cu(code, N.FLAME_HIER_SYNC if sync else 0, int(n_mids)))
+    if r < 1:
+        N.check(-r)
+    return r
+
+
 # ------------------------------------------------------------------ FedDyn server round
 def feddyn_program(arrivals: Sequence, dict_order: Sequence, had_history) -> tuple:
     """Step program of one flame_feddyn_round launch (host only, no GPU).

@@ -75,7 +75,8 @@ class ShardPlan:
     order; a rank-local dict (of views, client slices, optimizer state) uses them.
     """
 
-    def __init__(self, model, world: int, rank: int, *, align: int = ALIGN_ELEMS, fracs=DEFAULT_FRACS):
+    def __init__(self, model, world: int, rank: int, *, align: int = ALIGN_ELEMS, fracs=DEFAULT_FRACS,
+                 last_wave_quantum: int = 0):
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world {world}")
         self.world, self.rank, self.align = int(world), int(rank), int(align)
@@ -90,6 +91,12 @@ class ShardPlan:
         for f in fracs[:-1]:
             acc += f
             cuts.append(min(max(int(total * acc) // unit * unit, cuts[-1]), total))
+        q = int(last_wave_quantum)
+        if q > 0 and len(cuts) > 1 and q % self.align == 0 and total // self.world >= 2 * q:
+            # the last wave's per-rank size -> the nearest whole multiple of q (>= 1): a launch
+            # of long-lived workgroups then ends on a full round of them (ShardedHierarchy)
+            n_q = max(1, round((total - cuts[-1]) / self.world / q))
+            cuts[-1] = max(total - n_q * q * self.world, cuts[-2])
         cuts.append(total)
         subs, off = [], 0
         for k in self.keys:
@@ -587,6 +594,21 @@ class ShardedOptimizer:
 
 
 # -------------------------------------------------------------------- config 5
+def _hier_wave_quantum(model, device, middles: int, sync: bool) -> int:
+    """Per-rank elements of one full round of resident hierarchy workgroups on ``device``
+    (for the dtype of the model's largest key), a multiple of ALIGN_ELEMS; 0 if unknown."""
+    if device is None or torch.device(device).type != "cuda" or not model:
+        return 0
+    big = max(model.keys(), key=lambda k: math.prod(engine.logical_shape(model, k)))
+    code = engine.DTYPE_CODE.get(engine.weight_dtype(model, big))
+    if code not in (engine.N.FLAME_F32, engine.N.FLAME_BF16, engine.N.FLAME_F16):
+        return 0
+    per_cu = engine.hier_resident_per_cu(code, int(middles), sync)
+    cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+    q = per_cu * cus * engine.chunk_elems(code)
+    return q if q % ALIGN_ELEMS == 0 else 0
+
+
 class ShardedHierarchy:
     """A node's co-located two-level hierarchy, parameter-sharded over the node's GPUs
     (BASELINE.json config 5: hierarchical FedBuff, 4096 clients x 125M bf16 over 8 MI355X).
@@ -604,12 +626,20 @@ class ShardedHierarchy:
       ``scale_add`` + upload delta (``:221-226,246``), the top's FedBuff over the deltas
       (``asyncfl/top_aggregator.py:85-92``) and its ``scale_add`` (``:103-110``).
     * ``sync_round(middles, top_weights)``: the synchronous hierarchy.
+
+    ``middles`` (the node's fan-out, if known up front) sizes the last wave to a whole
+    round of the hierarchy kernel's resident workgroups on ``device`` (a workgroup lives
+    for all of a chunk's arrivals, so a launch ending on a partial round idles most of the
+    GPU for one workgroup lifetime); ``sync`` says which kernel mode the rounds will use.
     """
 
     def __init__(self, model, group=None, device: Optional[torch.device] = None, *, fracs=HIER_FRACS,
-                 align: int = ALIGN_ELEMS, round_fn=None, sync_round_fn=None):
+                 align: int = ALIGN_ELEMS, round_fn=None, sync_round_fn=None, middles: Optional[int] = None,
+                 sync: bool = False):
         self.comm = _Comm(group)
-        self.plan = ShardPlan(model, self.comm.world, self.comm.rank, align=align, fracs=fracs)
+        q = _hier_wave_quantum(model, device, middles, sync) if middles else 0
+        self.plan = ShardPlan(model, self.comm.world, self.comm.rank, align=align, fracs=fracs,
+                              last_wave_quantum=q)
         self.device = device
         self._round_fn, self._sync_fn = round_fn, sync_round_fn
 

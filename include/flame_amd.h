@@ -292,6 +292,16 @@ int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void *host_meta,
                                float top_goal, void *stream);
 
 /*
+ * Workgroups of the flame_hier_fedbuff launch for (dtype, n_mids, FLAME_HIER_SYNC in flags)
+ * that stay resident per CU at once (hipOccupancyMaxActiveBlocksPerMultiprocessor on the
+ * instantiation flame_hier_fedbuff would pick).  Its workgroups are long-lived (a chunk's
+ * every arrival), so a launch of chunks not a multiple of (this x CUs) ends in a partly
+ * filled last round of workgroups; flame_amd.shard sizes its waves with it.  Returns the
+ * count (>= 1) or a negative FLAME_E* status (host-side query, no launch).
+ */
+int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids);
+
+/*
  * Host buffers the kernels read zero-copy over PCIe (ingest; flame_amd/ingest.py).
  *   flame_host_register:   page-lock + map an existing host range (e.g. a received
  *                          channel payload or the LIFL shared-memory segment,

@@ -482,3 +482,50 @@ def test_sharded_many_keys_resnet_like_two_ranks_one_gpu():
     int64 num_batches_tracked) through ShardedOptimizer(FedAvg) and (FedAdam, which promotes
     the int64 buffers) with rank-local slab caches: == one process, bitwise, 3 rounds."""
     _two_ranks(_many_keys_worker)
+
+
+def test_hier_wave_quantum_world1():
+    """ShardedHierarchy(middles=M) on the GPU: the library's residency for the hierarchy
+    launch (2 workgroups per CU with LDS-held store groups, more without) sizes the last
+    wave to whole rounds of resident workgroups; the sharded round stays bitwise equal to
+    one hierarchy_round (world 1, no process group)."""
+    from flame_amd import engine, shard
+    from flame_amd.optimizer.fedbuff import FedBuff, hierarchy_round
+    from flame_amd.slab import UpdateSlab
+    big = engine.hier_resident_per_cu(engine.N.FLAME_BF16, 64)
+    small = engine.hier_resident_per_cu(engine.N.FLAME_BF16, 2)
+    assert big >= 1 and small >= big, (big, small)
+    assert engine.hier_resident_per_cu(engine.N.FLAME_BF16, 64, sync=True) >= 1
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    M, C, rnd = 16, 2, 7
+    q = engine.hier_resident_per_cu(engine.N.FLAME_BF16, M) * cus * engine.chunk_elems(engine.N.FLAME_BF16)
+    P = 2 * q + 12_345
+    g = torch.Generator().manual_seed(5)
+    tmpl = {"w": torch.randn(P, generator=g).bfloat16(), "b": torch.randn(9, generator=g).bfloat16()}
+    hier = shard.ShardedHierarchy(tmpl, device=torch.device(DEV), middles=M)
+    waves = [sum(s.hi - s.lo for s in hier.plan.subs if s.wave == w and not s.tail) for w in range(hier.plan.n_waves)]
+    assert hier.plan.n_waves == 2 and waves[-1] % q == 0, (waves, q)
+    ups = [[{k: (torch.randn(v.shape, generator=g) * 1e-2).bfloat16() for k, v in tmpl.items()} for _ in range(C)]
+           for _ in range(M)]
+    outs = []
+    for sharded in (True, False):
+        slab = UpdateSlab(tmpl, capacity=M * C, device=DEV)
+        mids = []
+        for m in range(M):
+            opt, agg = (hier.middle_optimizer() if sharded else FedBuff()), None
+            for t in range(C):
+                c = S.SortedCache()
+                c[f"m{m}t{t}"] = S.TR(slab.put({k: v.to(DEV) for k, v in ups[m][t].items()}), 1, rnd - (m + t) % 3)
+                agg = opt.do(agg, c, total=1, version=rnd)
+            mids.append(({k: v.to(DEV) for k, v in tmpl.items()}, agg, C, rnd - m % 2))
+        top = {k: v.to(DEV) for k, v in tmpl.items()}
+        if sharded:
+            hier.round(mids, None, version=rnd, top_weights=top, top_goal=M)
+        else:
+            hierarchy_round(mids, None, version=rnd, top_weights=top, top_goal=M)
+        torch.cuda.synchronize()
+        outs.append((top, [m[0] for m in mids]))
+    for k in tmpl:
+        assert _eq(outs[0][0][k], outs[1][0][k]), k
+        for a, b in zip(outs[0][1], outs[1][1]):
+            assert _eq(a[k], b[k]), k

@@ -304,3 +304,33 @@ def test_sharded_hierarchy_gloo_world2():
 
 def test_sharded_hierarchy_gloo_world3():
     _run(_hier_worker, world=3)
+
+
+def test_plan_last_wave_quantum():
+    """ShardPlan(last_wave_quantum=q): the last wave's per-rank size is the nearest whole
+    multiple of q (>= 1), the other waves absorb the rest; coverage is unchanged; a quantum
+    that does not fit (model too small, not a multiple of align) leaves the plan as is."""
+    from flame_amd import shard
+    G = 125_000_000
+    model = {"model": torch.empty(G, dtype=torch.bfloat16, device="meta")}
+    for world in (1, 2, 8):
+        q = 2 * 256 * 2048
+        p = shard.ShardPlan(model, world, 0, fracs=shard.HIER_FRACS, last_wave_quantum=q)
+        waves = [sum(s.hi - s.lo for s in p.subs if s.wave == w and not s.tail) for w in range(p.n_waves)]
+        assert p.n_waves == 2 and waves[-1] % q == 0 and waves[-1] >= q, waves
+        ref = shard.ShardPlan(model, world, 0, fracs=shard.HIER_FRACS)
+        assert abs(waves[-1] - sum(s.hi - s.lo for s in ref.subs if s.wave == 1)) <= q / 2 + 2048 * world
+        assert p.owned_elements() == ref.owned_elements()
+        for r in range(world):
+            pr = shard.ShardPlan(model, world, r, fracs=shard.HIER_FRACS, last_wave_quantum=q)
+            assert [(s.g0, s.g1) for s in pr.subs] == [(s.g0, s.g1) for s in p.subs]
+        covered = sorted((s.g0 + r * ((s.g1 - s.g0) // world), s.g0 + (r + 1) * ((s.g1 - s.g0) // world))
+                         for s in p.subs if not s.tail for r in range(world))
+        assert covered[0][0] == 0 and all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+    small = {"model": torch.empty(3 * 2048, dtype=torch.float32, device="meta")}
+    a = shard.ShardPlan(small, 1, 0, fracs=shard.HIER_FRACS, last_wave_quantum=1 << 20)
+    b = shard.ShardPlan(small, 1, 0, fracs=shard.HIER_FRACS)
+    assert [(s.g0, s.g1) for s in a.subs] == [(s.g0, s.g1) for s in b.subs]
+    odd = shard.ShardPlan(model, 2, 0, fracs=shard.HIER_FRACS, last_wave_quantum=1000)    # not a multiple of align
+    assert [(s.g0, s.g1) for s in odd.subs] == [(s.g0, s.g1) for s in
+                                                shard.ShardPlan(model, 2, 0, fracs=shard.HIER_FRACS).subs]
