@@ -835,17 +835,19 @@ def test_middle_group_flush_and_scale_add_many(dtype):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("placement", ["slab", "tensors"])
 @pytest.mark.parametrize("top_start", ["none", "existing"])
-def test_hierarchy_round_one_pass(dtype, placement, top_start):
+@pytest.mark.parametrize("M", [5, 21])
+def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
     """flame_hier_fedbuff (the co-located middles + top in ONE launch) == the separate
     launches (scale_add_agg_weights_with_delta per middle, top FedBuff.do per delta,
     top scale_add) == the oracle's op sequence, bitwise: top aggregate, top weights,
-    middle weights and deltas."""
+    middle weights and deltas.  M = 5 takes the register store groups, M = 21 the LDS-held
+    groups of 16 (>= FLAME_HLDS_MIN_MIDS) with a partial last group."""
     from flame_amd.optimizer.fedbuff import hierarchy_round, _compose_hierarchy
     from flame_amd.slab import UpdateSlab
     O = _oracle()
     g = torch.Generator().manual_seed(41)
     shapes = {"w": (3001,), "m": (17, 129), "b": (5,)}
-    M, C, rnd = 5, 4, 12
+    C, rnd = 4, 12
     ups = [[{k: (torch.randn(s, generator=g) * 1e-2).to(dtype) for k, s in shapes.items()} for _ in range(C)]
            for _ in range(M)]
     vers = [[rnd - ((m + t) % 4) for t in range(C)] for m in range(M)]
@@ -853,7 +855,7 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start):
     top_w0 = {k: torch.randn(s, generator=g).to(dtype) for k, s in shapes.items()}
     top_prev = {k: (torch.randn(s, generator=g) * 1e-3).to(dtype) for k, s in shapes.items()}
     mid_ver = [rnd - (m % 3) for m in range(M)]
-    goals = [C, C + 1, C, 3, C]
+    goals = [[C, C + 1, C, 3, C][m % 5] for m in range(M)]
     slab = UpdateSlab({k: torch.empty(s, dtype=dtype) for k, s in shapes.items()}, capacity=M * C, device=DEV) \
         if placement == "slab" else None
 
@@ -907,13 +909,14 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_hierarchy_round_readonly_middles(dtype):
+@pytest.mark.parametrize("M", [4, 18])
+def test_hierarchy_round_readonly_middles(dtype, M):
     """update_middle_weights=False (FLAME_HIER_MID_READONLY): middle weights untouched, the
     same tensor may serve every middle, and the top aggregate / top weights / deltas equal
     those of the in-place run with private copies, bitwise."""
     from flame_amd.optimizer.fedbuff import hierarchy_round
     g = torch.Generator().manual_seed(67)
-    M, C, rnd, P = 4, 3, 8, 5000
+    C, rnd, P = 3, 8, 5000
     ups = [[(torch.randn(P, generator=g) * 1e-2).to(dtype) for _ in range(C)] for _ in range(M)]
     fetched = torch.randn(P, generator=g).to(dtype)
     top0 = torch.randn(P, generator=g).to(dtype)
@@ -1104,15 +1107,17 @@ def test_sync_hierarchy_golden(golden, with_delta, slab):
     assert sum(1 for ev in launches if ev[0] == "flame_hier_fedbuff") == 3 * 2   # f32, bf16, f16 x 2 rounds
 
 
-def test_sync_hierarchy_vs_oracle_readonly_middles():
-    """8 middles x 16 trainers over ~1M params (tails, every float dtype + int64): top and
-    deltas == the oracle's FedAvg / delta / FedAvg composition; with
-    update_middle_weights=False one shared middle tensor is read, never written."""
+@pytest.mark.parametrize("M", [8, 20])
+def test_sync_hierarchy_vs_oracle_readonly_middles(M):
+    """8 / 20 middles x 16 trainers over ~1M params (tails, every float dtype + int64): top
+    and deltas == the oracle's FedAvg / delta / FedAvg composition; with
+    update_middle_weights=False one shared middle tensor is read, never written.  20
+    middles take the LDS-held store groups (a full group of 16 + 4)."""
     from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
     O = _oracle()
     g = torch.Generator().manual_seed(41)
     tmpl = _dyn_model(g, 1_000_003)
-    M, C = 8, 16
+    C = 16
     mid_cpu = {k: v.clone() for k, v in tmpl.items()}
     top_cpu = {k: (v * 0.5 if v.is_floating_point() else v) for k, v in tmpl.items()}
     ups = [[_dyn_update(g, tmpl, 5 * j + i) for i in range(C)] for j in range(M)]
@@ -1135,7 +1140,7 @@ def test_sync_hierarchy_vs_oracle_readonly_middles():
             cache[f"m{j}t{i:02d}"] = S.TR({k: v.clone() for k, v in ups[j][i].items()}, counts[j][i])
         new = O.OracleFedAvg().do({k: v.clone() for k, v in mid_cpu.items()}, cache, total=sum(counts[j]))
         exp_deltas.append({k: new[k] - mid_cpu[k] for k in new})
-        top_cache[f"mid{j}"] = S.TR(exp_deltas[-1], sum(counts[j]))
+        top_cache[f"mid{j:02d}"] = S.TR(exp_deltas[-1], sum(counts[j]))
     exp_top = O.OracleFedAvg().do({k: v.clone() for k, v in top_cpu.items()}, top_cache,
                                   total=sum(sum(c) for c in counts))
     for j in range(M):
