@@ -334,3 +334,12 @@ def test_plan_last_wave_quantum():
     odd = shard.ShardPlan(model, 2, 0, fracs=shard.HIER_FRACS, last_wave_quantum=1000)    # not a multiple of align
     assert [(s.g0, s.g1) for s in odd.subs] == [(s.g0, s.g1) for s in
                                                 shard.ShardPlan(model, 2, 0, fracs=shard.HIER_FRACS).subs]
+
+
+def test_sharded_paths_gloo_world8():
+    """The N = 8 layout the driver's 8-GPU runs use (every rank owns 1/8 of each wave, the
+    tails replicated), rehearsed with 8 gloo ranks on CPU: sharded FedAvg in waves, FedOPT +
+    FedBuff and the sharded hierarchy, each bitwise against one process / the oracle."""
+    _run(_fedavg_worker, world=8)
+    _run(_opt_worker, world=8)
+    _run(_hier_worker, world=8)
