@@ -24,6 +24,8 @@
  *   flame_feddyn_round          optimizer/feddyn.py:90-113,125-139 (FedDyn.do: add_to_hist,
  *                               FedAvg with rate 1/len(cache), mean of the histories, cld_model)
  *   flame_synth_fill            (bench/test plumbing: counter-based synthetic updates)
+ *   flame_hier_resident_per_cu  (no reference counterpart: occupancy query the parameter
+ *                               shard uses to size its waves, flame_amd/shard.py)
  *
  * Conventions
  *   - All pointers passed to the compute entry points are DEVICE pointers
