@@ -53,6 +53,9 @@ int main(void) {
     EXPECT_ERR(flame_host_unregister(NULL), FLAME_EINVAL, "");
     EXPECT_ERR(flame_host_device_pointer(NULL, NULL), FLAME_EINVAL, "");
     EXPECT_ERR(flame_feddyn_round(0, NULL, 0, 1, NULL, NULL, 0, 0, .5, .5, NULL), FLAME_EINVAL, "");
+    EXPECT(flame_hier_resident_per_cu(FLAME_BF16, 0, 0) == -FLAME_EINVAL, "resident_per_cu n_mids 0");
+    EXPECT(strstr(flame_last_error(), "n_mids") != NULL, "resident_per_cu msg");
+    EXPECT(flame_hier_resident_per_cu(FLAME_I64, 0, 64) == -FLAME_ENOTSUP, "resident_per_cu int dtype");
     EXPECT_ERR(flame_feddyn_round(0, fake, 1, 1, fake, NULL, 2, 0, .5, .5, NULL), FLAME_EINVAL, "step flag");
     EXPECT_ERR(flame_feddyn_round(0, fake, 1, 1, fake, fake, 2, 3, .5, .5, NULL), FLAME_EINVAL, "n_phase1");
     EXPECT_ERR(flame_hier_fedbuff(0, 0, fake, 1, 1, 0, 1, fake, NULL, fake, fake, fake, fake, 0.f, NULL),
