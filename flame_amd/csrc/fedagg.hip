@@ -123,6 +123,15 @@ namespace {
 #ifndef FLAME_OPT_PREFETCH
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
+#ifndef FLAME_OPT_WGC
+#define FLAME_OPT_WGC 8   // FedOPT (fp32, >= 8 x 256 x WGC chunks): chunks per workgroup; > 1 holds their
+                          // avg/m/v/cur blocks in LDS (16 KiB per chunk, 128 KiB at 8 -> one workgroup
+                          // per CU) and stores them in one burst at the end.  C4 FedAdam, tiled slab:
+                          // 15.18 -> 14.62 ms (tools/kernel_sweep.py, profiles/r02_fedopt_wgc_sweep.log)
+#endif
+#ifndef FLAME_OPT_CU
+#define FLAME_OPT_CU FLAME_CU  // FedOPT fp32 client unroll with FLAME_OPT_WGC > 1
+#endif
 
 constexpr int kBlock = FLAME_BLOCK;
 constexpr int kHB = FLAME_HBATCH;
@@ -625,20 +634,23 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
     cur_out = rnd<DT>(__fadd_rn(cur, q));
 }
 
+// One chunk of a FedOPT round.  held != nullptr: a full-vector chunk leaves its avg / m / v /
+// cur blocks in LDS (held[(o * kVPT + v) * kBlock + lane], o = avg, m, v, cur) for the caller
+// to store, and returns true; otherwise everything is stored here and it returns false.
 template <int DT, int VARIANT, int CU>
-__device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ segs, int n_segs,
-                                            const uint64_t* __restrict__ clients, int n_clients,
-                                            const float* __restrict__ r32, unsigned flags, float b1,
-                                            float omb1, float b2, float omb2, float eta, float tau) {
+__device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ segs, int n_segs, int64_t chunk,
+                                             const uint64_t* __restrict__ clients, int n_clients,
+                                             const float* __restrict__ r32, unsigned flags, float b1,
+                                             float omb1, float b2, float omb2, float eta, float tau,
+                                             V16* held) {
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
-    const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
-    if (e0 >= sg.numel) return;
+    if (e0 >= sg.numel) return false;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const int64_t coff = client_offset<DT>(sg, chunk);
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
@@ -692,11 +704,20 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
                 v_o[j] = X::st(vj);
                 c_o[j] = X::st(cj);
             }
+            if (held) {
+                V16* h = held + v * kBlock + threadIdx.x;
+                h[0 * kVPT * kBlock] = pack<T, EPT>(avg_o);
+                h[1 * kVPT * kBlock] = pack<T, EPT>(m_o);
+                h[2 * kVPT * kBlock] = pack<T, EPT>(v_o);
+                h[3 * kVPT * kBlock] = pack<T, EPT>(c_o);
+                continue;
+            }
             if (ap) st_v(ap + v * VS, pack<T, EPT>(avg_o));
             st_v(mp + v * VS, pack<T, EPT>(m_o));
             st_v(vp + v * VS, pack<T, EPT>(v_o));
             st_v(cop + v * VS, pack<T, EPT>(c_o));
         }
+        return held != nullptr;
     } else {
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
@@ -718,14 +739,62 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
                 st1(cop + o, X::st(cj));
             }
     }
+    return false;
 }
 
-template <int DT, int VARIANT, int CU>
+// G = 1: one chunk per workgroup, stored as computed.  G > 1: G consecutive chunks per
+// workgroup, their outputs held in LDS and stored together at the end (FLAME_OPT_WGC).
+template <int DT, int VARIANT, int CU, int G>
+__device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ segs, int n_segs,
+                                            const uint64_t* __restrict__ clients, int n_clients,
+                                            const float* __restrict__ r32, unsigned flags, float b1,
+                                            float omb1, float b2, float omb2, float eta, float tau,
+                                            int64_t n_chunks) {
+    if constexpr (G == 1) {
+        (void)n_chunks;
+        fedopt_chunk<DT, VARIANT, CU>(segs, n_segs, blockIdx.x, clients, n_clients, r32, flags, b1, omb1, b2,
+                                      omb2, eta, tau, nullptr);
+    } else {
+        using T = typename Tr<DT>::T;
+        constexpr int64_t VS = static_cast<int64_t>(kBlock) * Tr<DT>::EPT;
+        __shared__ V16 held[G * 4 * kVPT * kBlock];
+        unsigned pending = 0;
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+            const int64_t chunk = static_cast<int64_t>(blockIdx.x) * G + g;
+            if (chunk >= n_chunks) break;
+            if (fedopt_chunk<DT, VARIANT, CU>(segs, n_segs, chunk, clients, n_clients, r32, flags, b1, omb1, b2, omb2,
+                                              eta, tau, held + g * 4 * kVPT * kBlock))
+                pending |= 1u << g;
+        }
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+            if (!(pending >> g & 1u)) continue;
+            const int64_t chunk = static_cast<int64_t>(blockIdx.x) * G + g;
+            const flame_segment& sg = segs[find_segment(segs, n_segs, chunk)];
+            const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() +
+                               static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
+            T* outs[4] = {sg.out ? reinterpret_cast<T*>(sg.out) + e0 : nullptr, reinterpret_cast<T*>(sg.m) + e0,
+                          reinterpret_cast<T*>(sg.v) + e0, reinterpret_cast<T*>(sg.cur_out) + e0};
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (!outs[o]) continue;
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v)
+                    st_v(outs[o] + v * VS, held[((g * 4 + o) * kVPT + v) * kBlock + threadIdx.x]);
+            }
+        }
+    }
+}
+
+template <int DT, int VARIANT, int CU, int G>
 __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                         const uint64_t* __restrict__ clients, int n_clients,
                                                         const float* __restrict__ r32, unsigned flags, float b1,
-                                                        float omb1, float b2, float omb2, float eta, float tau) {
-    fedopt_body<DT, VARIANT, CU>(segs, n_segs, clients, n_clients, r32, flags, b1, omb1, b2, omb2, eta, tau);
+                                                        float omb1, float b2, float omb2, float eta, float tau,
+                                                        int64_t n_chunks) {
+    fedopt_body<DT, VARIANT, CU, G>(segs, n_segs, clients, n_clients, r32, flags, b1, omb1, b2, omb2, eta, tau,
+                                    n_chunks);
 }
 
 // The same with the metadata block as a kernel argument, read in place (flame_fedopt_reduce_adapt_argmeta;
@@ -737,9 +806,9 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta me
                                                                 float eta, float tau) {
     (void)sizeof(meta);
     const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    fedopt_body<DT, VARIANT, CU>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
-                                 off_r32 >= 0 ? reinterpret_cast<const float*>(w + off_r32) : nullptr, flags,
-                                 b1, omb1, b2, omb2, eta, tau);
+    fedopt_body<DT, VARIANT, CU, 1>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
+                                    off_r32 >= 0 ? reinterpret_cast<const float*>(w + off_r32) : nullptr, flags,
+                                    b1, omb1, b2, omb2, eta, tau, 0);
 }
 
 // ---------------------------------------------------------------- FedBuff scale-add (+delta)
@@ -1267,6 +1336,9 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 constexpr int kClientUnroll = FLAME_CU;
 constexpr int kClientUnroll16 = FLAME_CU16;
 constexpr int kHierUnroll16 = FLAME_HCU16;
+constexpr int kOptWGC = FLAME_OPT_WGC;
+constexpr int kOptUnroll = FLAME_OPT_CU;
+static_assert(kOptWGC >= 1 && kOptWGC <= 32, "FLAME_OPT_WGC: 1..32 chunks per workgroup");
 constexpr int kHierLdsUnroll16 = FLAME_HLDS_CU16;
 constexpr int kHBL = FLAME_HLDS_BATCH;
 
@@ -1404,31 +1476,37 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
     if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: unknown variant %d", variant);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    // FLAME_OPT_WGC chunks per workgroup (outputs held in LDS) for fp32 launches big enough to fill
+    // the GPU several times over; one chunk per workgroup otherwise
+    const bool multi = kOptWGC > 1 && n_chunks >= 8ll * 256 * kOptWGC;
+    const dim3 grid(static_cast<unsigned>(multi ? (n_chunks + kOptWGC - 1) / kOptWGC : n_chunks)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-#define FLAME_OPT_LAUNCH(DT, CUV)                                                                              \
+#define FLAME_OPT_LAUNCH1(DT, CUV, G)                                                                          \
     switch (variant) {                                                                                         \
     case FLAME_FEDADAM:                                                                                        \
-        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAM, CUV>), grid, block, 0, st, segs, n_segs, cl,       \
-                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAM, CUV, G>), grid, block, 0, st, segs, n_segs, cl,    \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                 \
         break;                                                                                                 \
     case FLAME_FEDYOGI:                                                                                        \
-        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDYOGI, CUV>), grid, block, 0, st, segs, n_segs, cl,       \
-                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDYOGI, CUV, G>), grid, block, 0, st, segs, n_segs, cl,    \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                 \
         break;                                                                                                 \
     default:                                                                                                   \
-        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAGRAD, CUV>), grid, block, 0, st, segs, n_segs, cl,    \
-                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau);                           \
+        hipLaunchKernelGGL((fedopt_kernel<DT, FLAME_FEDADAGRAD, CUV, G>), grid, block, 0, st, segs, n_segs, cl, \
+                           n_clients, rates32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                 \
         break;                                                                                                 \
     }
     switch (dtype) {
-    case FLAME_F32: FLAME_OPT_LAUNCH(FLAME_F32, kClientUnroll) break;
-    case FLAME_BF16: FLAME_OPT_LAUNCH(FLAME_BF16, kClientUnroll16) break;
-    case FLAME_F16: FLAME_OPT_LAUNCH(FLAME_F16, kClientUnroll16) break;
+    case FLAME_F32:
+        if (multi) { FLAME_OPT_LAUNCH1(FLAME_F32, kOptUnroll, kOptWGC) }
+        else { FLAME_OPT_LAUNCH1(FLAME_F32, kClientUnroll, 1) }
+        break;
+    case FLAME_BF16: FLAME_OPT_LAUNCH1(FLAME_BF16, kClientUnroll16, 1) break;
+    case FLAME_F16: FLAME_OPT_LAUNCH1(FLAME_F16, kClientUnroll16, 1) break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: dtype %d not supported (f32, bf16, f16)", dtype);
     }
-#undef FLAME_OPT_LAUNCH
+#undef FLAME_OPT_LAUNCH1
     return check_launch("flame_fedopt_reduce_adapt");
 }
 

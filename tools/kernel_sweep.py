@@ -51,6 +51,20 @@ VARIANTS = {
     "wgc4d": {"FLAME_WGC": 4, "FLAME_DEFER_ST": 1},
     "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
     # FedDyn round kernel (bench.py --workload feddyn with FLAME_AMD_LIB=build/variants/lib_<name>.so)
+    # FedOPT: several chunks per workgroup, outputs held in LDS and stored in one burst
+    "optwgc2": {"FLAME_OPT_WGC": 2},
+    "optwgc3": {"FLAME_OPT_WGC": 3},
+    "optwgc4": {"FLAME_OPT_WGC": 4},
+    "optwgc6": {"FLAME_OPT_WGC": 6},
+    "optwgc8": {"FLAME_OPT_WGC": 8},
+    "optwgc4cu16": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 16},
+    "optwgc6cu16": {"FLAME_OPT_WGC": 6, "FLAME_OPT_CU": 16},
+    "optwgc3cu16": {"FLAME_OPT_WGC": 3, "FLAME_OPT_CU": 16},
+    "optwgc5": {"FLAME_OPT_WGC": 5},
+    "optwgc7": {"FLAME_OPT_WGC": 7},
+    "optwgc10": {"FLAME_OPT_WGC": 10},
+    "optwgc8cu16": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 16},
+    "optwgc8cu4": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 4},
     "dyncu2": {"FLAME_DYN_CU": 2},
     # updated histories held in LDS, stored G steps at a time (tools/feddyn_sweep.py)
     "dynlds8": {"FLAME_DYN_LDS": 8},
@@ -151,9 +165,13 @@ def main():
     plans = {}
     if args.kernel != "agg":
         cur = base0.clone()
-        m = torch.zeros_like(base0)
-        v = torch.zeros_like(base0)
+        m = torch.empty_like(base0)
+        v = torch.empty_like(base0)
+        engine.synth_fill_(m, 2, 9001, 0, 1e-3)
+        engine.synth_fill_(v, 2, 9002, 0, 1e-3)
+        v.abs_()
         cur_out = torch.empty_like(base0)
+        state0 = (cur.clone(), m.clone(), v.clone())
     for nm, L in libs.items():
         if nm.endswith(":tiled"):
             T = tiled_slab.shape[2]
@@ -206,17 +224,24 @@ def main():
         plans["probe"] = None
         names = names + ["probe"]
 
-    # correctness: every variant bitwise equal to the first (agg kernel; fedopt state evolves)
-    ref = None
+    # correctness: every variant bitwise equal to the first of its layout (FedOPT: from the same
+    # cur / m / v state, all four outputs compared)
+    refs = {}
     for nm in names:
+        if args.kernel != "agg" and nm != "probe":
+            for t, t0 in zip((cur, m, v), state0):
+                t.copy_(t0)
         launch(nm)
         torch.cuda.synchronize()
-        if args.kernel != "agg" or nm == "probe" or nm.endswith(":tiled") or nm.startswith("nostore"):
+        if nm == "probe" or nm.startswith("nostore"):
             continue
-        if ref is None:
-            ref = out.clone()
-        elif not torch.equal(out.view(torch.int16), ref.view(torch.int16)):
-            raise SystemExit(f"variant {nm} differs from {names[0]}")
+        got = [out.clone()] if args.kernel == "agg" else [out.clone(), m.clone(), v.clone(), cur_out.clone()]
+        lay = "tiled" if nm.endswith(":tiled") else "rows"
+        if lay not in refs:
+            refs[lay] = (nm, got)
+        elif not all(torch.equal(a.view(torch.int16), b.view(torch.int16)) for a, b in zip(got, refs[lay][1])):
+            raise SystemExit(f"variant {nm} differs from {refs[lay][0]}")
+    print("bitwise: every variant equals the first of its layout", flush=True)
     times = {nm: [] for nm in names}
     for r in range(args.rounds):
         for nm in names:
