@@ -52,6 +52,7 @@ VARIANTS = {
     "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
     # FedDyn round kernel (bench.py --workload feddyn with FLAME_AMD_LIB=build/variants/lib_<name>.so)
     # FedOPT: several chunks per workgroup, outputs held in LDS and stored in one burst
+    "optwgc1": {"FLAME_OPT_WGC": 1},      # round 1's FedOPT kernel (one chunk per workgroup)
     "optwgc2": {"FLAME_OPT_WGC": 2},
     "optwgc3": {"FLAME_OPT_WGC": 3},
     "optwgc4": {"FLAME_OPT_WGC": 4},
