@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/optab; mkdir -p $OUT
-for i in 1 2; do
+for i in 1 2 3 4 5; do
   for lib in product optwgc1; do
     if [ $lib = product ]; then L=flame_amd/libflame_amd.so; else L=build/variants/lib_$lib.so; fi
     FLAME_AMD_LIB=$L timeout -k 10 300 python bench.py --workload fedadam --steps 10 --warmup 3 --cpu-clients 0 \
