@@ -757,6 +757,7 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
     } else {
         using T = typename Tr<DT>::T;
         constexpr int64_t VS = static_cast<int64_t>(kBlock) * Tr<DT>::EPT;
+        static_assert(G * 4 * kVPT * kBlock * sizeof(V16) <= 160 * 1024, "FLAME_OPT_WGC: outputs exceed the LDS");
         __shared__ V16 held[G * 4 * kVPT * kBlock];
         unsigned pending = 0;
 #pragma unroll 1
