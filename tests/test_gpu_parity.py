@@ -1637,3 +1637,52 @@ def test_key_subset_arrivals():
             S.assert_bitwise("fedadam subsets r0", cur, ecur)
         else:
             S.assert_close_fedopt(f"fedadam subsets r{r}", cur, ecur, elementwise=r == 1)
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi"])
+def test_fedopt_multichunk_multikey(sort):
+    """FedOPT launches large enough for the 8-chunks-per-workgroup build (>= 16,384 fp32
+    chunks): five keys (odd sizes, a 3-element and an empty key) in one launch, so a
+    workgroup's chunks straddle keys and ragged key tails; slab and tensor placements equal
+    each other bitwise (avg, m, v, cur), and the oracle within the §8(c) contract."""
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(23)
+    shapes = {"a": (4_000_037,), "b": (3001, 4099), "c": (1_000_001,), "d": (3,), "e": (0,)}
+    n, rounds = 6, 3
+    w0 = {k: torch.randn(s, generator=g) for k, s in shapes.items()}
+    data = [([{k: torch.randn(s, generator=g) * 1e-2 for k, s in shapes.items()} for _ in range(n)],
+             torch.randint(1, 1000, (n,), generator=g).tolist()) for _ in range(rounds)]
+    slab = UpdateSlab({k: torch.empty(s) for k, s in shapes.items()}, capacity=n, device=DEV)
+    runs = {}
+    for placement in ("slab", "tensors"):
+        amd = make_amd(sort)
+        wa = {k: v.to(DEV) for k, v in w0.items()}
+        outs = []
+        for cl, counts in data:
+            c = S.SortedCache()
+            for i in range(n):
+                w = {k: v.to(DEV) for k, v in cl[i].items()}
+                c[f"{i:02d}"] = S.TR(slab.put(w) if placement == "slab" else w, counts[i])
+            wa = amd.do({k: v.clone() for k, v in wa.items()}, c, total=sum(counts))
+            torch.cuda.synchronize()
+            outs.append((S.to_cpu(dict(wa)), S.to_cpu(dict(amd.m_t)) if amd.m_t else None,
+                         S.to_cpu(dict(amd.v_t)) if amd.v_t else None))
+        runs[placement] = outs
+    for r in range(rounds):
+        for j, lbl in enumerate(("cur", "m", "v")):
+            if runs["slab"][r][j] is not None:
+                S.assert_bitwise(f"slab vs tensors r{r}/{lbl}", runs["slab"][r][j], runs["tensors"][r][j])
+    ora = O.OracleFedOPT(sort)
+    wo = {k: v.clone() for k, v in w0.items()}
+    for r, (cl, counts) in enumerate(data):
+        c = S.SortedCache()
+        for i in range(n):
+            c[f"{i:02d}"] = S.TR({k: v.clone() for k, v in cl[i].items()}, counts[i])
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, c, total=sum(counts))
+        got = runs["slab"][r][0]
+        if r == 0:
+            S.assert_bitwise(f"{sort}/r0", got, wo)
+        else:
+            S.assert_close_fedopt(f"{sort}/r{r}/cur", got, wo, elementwise=r == 1)
+            S.assert_close_fedopt(f"{sort}/r{r}/m", runs["slab"][r][1], ora.m_t, elementwise=r == 1)
