@@ -68,7 +68,11 @@ class FedOPT(FedAvg):
     def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         logger.debug("calling fedopt (flame_amd)")
         if self.current_weights is not None and base_weights is not None and len(cache) > 0 and total != 0:
-            return self._do_fused(base_weights, cache, total)
+            # flame_amd.shard passes its plan's waves (one launch per wave, its all-gather started
+            # right behind it) and an allocator placing each key's new `current` straight into
+            # the full tensor the gather fills (callers from flame pass none of these)
+            return self._do_fused(base_weights, cache, total, kwargs.get("flame_amd_key_groups"),
+                                  kwargs.get("flame_amd_after_group"), kwargs.get("flame_amd_out_alloc"))
         self.agg_weights = super().do(base_weights, cache, total=total, version=version)
         if self.agg_weights is None:
             return self.current_weights
@@ -79,7 +83,7 @@ class FedOPT(FedAvg):
         return self.current_weights
 
     # ------------------------------------------------------------------ fused round
-    def _do_fused(self, base_weights, cache, total):
+    def _do_fused(self, base_weights, cache, total, key_groups=None, after_group=None, alloc=None):
         self.agg_weights = base_weights
         entries = self._pop_entries(cache, total)
         current = self.current_weights
@@ -108,35 +112,49 @@ class FedOPT(FedAvg):
         if state_zero:
             self.m_t, self.v_t = {}, {}
         new_cur = {}
-        if fused:
-            targets = [engine._Target(base_weights[k], device) for k in fused]
-            curs = [engine._as_device(current[k], device) for k in fused]
-            outs = [torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device) for k in fused]
-            ms, vs = [], []
-            for k in fused:
-                if state_zero:  # zeros_like(d_t[k]) in the reference: d's dtype
-                    self.m_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
-                    self.v_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
-                else:
-                    self.m_t[k] = engine._as_device(self.m_t[k], device)
-                    self.v_t[k] = engine._as_device(self.v_t[k], device)
-                ms.append(self.m_t[k])
-                vs.append(self.v_t[k])
-            hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
-            engine.fedopt_reduce_adapt_(self.variant, [t.dev for t in targets], [t.dev for t in targets], curs,
-                                        outs, ms, vs, [[w[k] for w, _ in entries] for k in fused],
-                                        [r for _, r in entries], hyper, state_zero)
-            for t in targets:
-                t.writeback()
-            new_cur.update(zip(fused, outs))
-        if generic:
+        if generic:       # first, so every key of a group is final when its group is handed on
             sub = {k: base_weights[k] for k in generic}
             engine.accumulate(sub, [({k: w[k] for k in generic if k in w}, r) for w, r in entries], device=device)
-            new_cur.update(self._adapt_generic(generic, base_weights, current, state_zero))
+            res = self._adapt_generic(generic, base_weights, current, state_zero)
+            if alloc is not None:
+                for k, v in res.items():
+                    res[k] = alloc(k, v.dtype, v.shape).copy_(v)
+            new_cur.update(res)
+        hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
+        in_fused = set(fused)
+        for gi, group in enumerate(key_groups if key_groups is not None else [keys]):
+            ks = [k for k in group if k in in_fused]
+            if ks:
+                self._launch_fused(ks, base_weights, current, entries, device, hyper, state_zero, alloc, new_cur)
+            if after_group is not None:
+                after_group(gi)
         self._prev_current = current
         self._d_t = None
         self.current_weights = OrderedDict((k, new_cur[k]) for k in current.keys() if k in new_cur)
         return self.current_weights
+
+    def _launch_fused(self, ks, base_weights, current, entries, device, hyper, state_zero, alloc, new_cur):
+        """One flame_fedopt_reduce_adapt launch per dtype over keys ``ks``."""
+        targets = [engine._Target(base_weights[k], device) for k in ks]
+        curs = [engine._as_device(current[k], device) for k in ks]
+        outs = [alloc(k, base_weights[k].dtype, base_weights[k].shape) if alloc is not None else
+                torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device) for k in ks]
+        ms, vs = [], []
+        for k in ks:
+            if state_zero:  # zeros_like(d_t[k]) in the reference: d's dtype
+                self.m_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
+                self.v_t[k] = torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device)
+            else:
+                self.m_t[k] = engine._as_device(self.m_t[k], device)
+                self.v_t[k] = engine._as_device(self.v_t[k], device)
+            ms.append(self.m_t[k])
+            vs.append(self.v_t[k])
+        engine.fedopt_reduce_adapt_(self.variant, [t.dev for t in targets], [t.dev for t in targets], curs,
+                                    outs, ms, vs, [[w[k] for w, _ in entries] for k in ks],
+                                    [r for _, r in entries], hyper, state_zero)
+        for t in targets:
+            t.writeback()
+        new_cur.update(zip(ks, outs))
 
     def _adapt_generic(self, keys, average, current, state_zero):
         """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""

@@ -326,6 +326,17 @@ class _Gatherer:
             t[s.lo:s.hi].copy_(r.reshape(-1))
             self.target[n] = t
 
+    def alloc(self, name, dtype, shape) -> torch.Tensor:
+        """Where a wrapped optimizer writes local result ``name``: its range of a new full
+        tensor of ``dtype`` (gathered in place when the name's wave is issued)."""
+        s = self.plan.by_name[name]
+        t = self.new.get(s.key)
+        if t is None or t.dtype != dtype:
+            t = self.new[s.key] = torch.empty(self.plan.numel[s.key], dtype=dtype,
+                                              device=self.work.flat[s.key].device)
+        self.target[name] = t
+        return t[s.lo:s.hi].view(shape)
+
     def issue(self, wave: int) -> None:
         if wave in self.issued:
             return
@@ -440,6 +451,12 @@ def _restrict(plan: ShardPlan, rec, wave: int) -> _SlicedResult:
     return _SlicedResult(plan.restrict(rec.weights, wave), getattr(rec, "count", 0), getattr(rec, "version", 0))
 
 
+def _fedopt_round(inner) -> bool:
+    """flame_amd's FedOPT with state: its next round is a fused adaptive step."""
+    from .optimizer.fedopt import FedOPT
+    return isinstance(inner, FedOPT) and inner.current_weights is not None
+
+
 def _device_of(weights, device):
     if device is not None:
         return torch.device(device)
@@ -549,6 +566,19 @@ class ShardedOptimizer:
                 return None
             gat.check_inplace(res, local)
             return gat.finish()
+        if _fedopt_round(self.inner) and self.waves is not False:
+            # flame_amd FedOPT past its passthrough round: one do(), one launch per wave writing
+            # the new `current` straight into the full tensors, each wave gathered right behind
+            res = self.inner.do(local, _Replay(records), total=total, version=version,
+                                flame_amd_key_groups=plan.wave_names, flame_amd_after_group=gat.issue,
+                                flame_amd_out_alloc=gat.alloc, **kwargs)
+            if res is None:
+                return None
+            missing = [n for n in plan.names if n in res and n not in gat.target]
+            if missing:      # not produced through the allocator: gathered after the fact
+                gat.collect(res, local, missing)
+                gat.issued.clear()
+            return self._remember(res, gat.finish())
         if self.waves:
             # any other stateless optimizer (e.g. the CPU oracle in tests): one do() per wave on
             # the records replayed, each wave gathered as soon as it is done
