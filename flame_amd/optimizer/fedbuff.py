@@ -173,9 +173,12 @@ class FedBuff(AbstractOptimizer):
         else:
             engine.accumulate(self.agg_goal_weights, entries)
 
-    def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal: int):
-        """base[k] += agg[k] / agg_goal in place; returns base_weights (fedbuff.py:101-127)."""
-        return self._scale_add(base_weights, agg_goal_weights, agg_goal, None)
+    def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal: int, **kwargs):
+        """base[k] += agg[k] / agg_goal in place; returns base_weights (fedbuff.py:101-127).
+        flame_amd.shard passes its waves (``flame_amd_key_groups`` / ``flame_amd_after_group``:
+        one launch per wave, its all-gather started behind it); flame passes none."""
+        return self._scale_add(base_weights, agg_goal_weights, agg_goal, None,
+                               kwargs.get("flame_amd_key_groups"), kwargs.get("flame_amd_after_group"))
 
     def scale_add_agg_weights_with_delta(self, base_weights, agg_goal_weights, agg_goal: int):
         """scale_add fused with the middle aggregator's upload delta (new - old).
@@ -189,22 +192,25 @@ class FedBuff(AbstractOptimizer):
                  for k in base_weights.keys()}
         return self._scale_add(base_weights, agg_goal_weights, agg_goal, delta), delta
 
-    def _scale_add(self, base_weights, agg_goal_weights, agg_goal, delta):
+    def _scale_add(self, base_weights, agg_goal_weights, agg_goal, delta, key_groups=None, after_group=None):
         if isinstance(agg_goal_weights, DeferredAggregate):
-            if self.fuse_scale_add and _fused_scale_add(base_weights, agg_goal_weights, agg_goal, delta):
+            if self.fuse_scale_add and _fused_scale_add(base_weights, agg_goal_weights, agg_goal, delta, key_groups,
+                                                        after_group):
                 return base_weights
             agg_goal_weights.flush()
-        keys = list(base_weights.keys())
         device = engine.pick_device(base_weights, agg_goal_weights)
-        targets = [engine._Target(base_weights[k], device) for k in keys]
-        engine.scale_add_([t.dev for t in targets], [agg_goal_weights[k] for k in keys], agg_goal,
-                          [delta[k] for k in keys] if delta is not None else None)
-        for t in targets:
-            t.writeback()
+        for gi, keys in enumerate(key_groups if key_groups is not None else [list(base_weights.keys())]):
+            targets = [engine._Target(base_weights[k], device) for k in keys]
+            engine.scale_add_([t.dev for t in targets], [agg_goal_weights[k] for k in keys], agg_goal,
+                              [delta[k] for k in keys] if delta is not None else None)
+            for t in targets:
+                t.writeback()
+            if after_group is not None:
+                after_group(gi)
         return base_weights
 
 
-def _fused_scale_add(base_weights, agg, agg_goal, delta) -> bool:
+def _fused_scale_add(base_weights, agg, agg_goal, delta, key_groups=None, after_group=None) -> bool:
     """``base += agg / agg_goal`` (+ the delta) straight from a None-start aggregate whose
     arrivals are still queued: the arrivals are reduced in registers and applied in ONE
     ``flame_hier_fedbuff`` launch per dtype (one middle, no top) -- the aggregate is never
@@ -232,15 +238,18 @@ def _fused_scale_add(base_weights, agg, agg_goal, delta) -> bool:
     if rows is None:
         return False
     rates = [[r for _, r in agg._pending]]
-    groups = collections.OrderedDict()
-    for k in keys:
-        groups.setdefault(codes[k], []).append(k)
-    for code, ks in groups.items():
-        segs = [engine.HierSeg(numel=base_weights[k].numel(), mid_w=[base_weights[k].data_ptr()], clients=rows[k][0],
-                               mid_delta=[delta[k].data_ptr()] if delta is not None else None,
-                               tile_stride=rows[k][1]) for k in ks]
-        engine.hier_fedbuff_(segs, code, rates, [agg_goal], [1.0], top_accum=False, top_goal=None, device=device,
-                             keep=keep)
+    for gi, gkeys in enumerate(key_groups if key_groups is not None else [keys]):
+        groups = collections.OrderedDict()
+        for k in gkeys:
+            groups.setdefault(codes[k], []).append(k)
+        for code, ks in groups.items():
+            segs = [engine.HierSeg(numel=base_weights[k].numel(), mid_w=[base_weights[k].data_ptr()],
+                                   clients=rows[k][0], mid_delta=[delta[k].data_ptr()] if delta is not None else None,
+                                   tile_stride=rows[k][1]) for k in ks]
+            engine.hier_fedbuff_(segs, code, rates, [agg_goal], [1.0], top_accum=False, top_goal=None, device=device,
+                                 keep=keep)
+        if after_group is not None:
+            after_group(gi)
     engine._keepalive(keep, device)
     return True
 

@@ -613,8 +613,18 @@ class ShardedOptimizer:
         plan = self._ensure_plan(base_weights)
         work = _Work(base_weights, plan.keys, _device_of(base_weights, self.device))
         local = plan.views(work.flat)
+        gat = _Gatherer(self.comm, plan, base_weights, work)
+        from .optimizer.fedbuff import FedBuff
+        if isinstance(self.inner, FedBuff):
+            # flame_amd FedBuff: one launch per wave in place, each wave's gather right behind it
+            gat.expect_inplace()
+            res = self.inner.scale_add_agg_weights(local, agg_goal_weights, agg_goal,
+                                                   flame_amd_key_groups=plan.wave_names,
+                                                   flame_amd_after_group=gat.issue)
+            gat.check_inplace(res, local)
+            return gat.finish()
         res = self.inner.scale_add_agg_weights(local, agg_goal_weights, agg_goal)
-        return self._gather_all(res, local, _Gatherer(self.comm, plan, base_weights, work))
+        return self._gather_all(res, local, gat)
 
     def __getattr__(self, name):              # regularizer, m_t, v_t, ... of the wrapped optimizer
         inner = self.__dict__.get("inner")

@@ -529,3 +529,37 @@ def test_hier_wave_quantum_world1():
         assert _eq(outs[0][0][k], outs[1][0][k]), k
         for a, b in zip(outs[0][1], outs[1][1]):
             assert _eq(a[k], b[k]), k
+
+
+def test_sharded_fedbuff_scale_add_waves_world1():
+    """The async top sharded (ShardedOptimizer(FedBuff, accumulate_only=True)): arrivals one
+    per do() on this rank's slices, then scale_add_agg_weights -- one fused launch per wave
+    in place (the waves' gathers behind them) -- bitwise equal to the unsharded FedBuff, for
+    fused and unfused scale_add and a multi-key, mixed-dtype model."""
+    from flame_amd import shard
+    from flame_amd.optimizer.fedbuff import FedBuff
+    g = torch.Generator().manual_seed(31)
+    tmpl = {"w": torch.randn(700_001, generator=g), "h": torch.randn(3001, 17, generator=g).bfloat16(),
+            "b": torch.randn(5, generator=g)}
+    K, rnd = 7, 9
+    ups = [{k: (torch.randn(v.shape, generator=g) * 1e-2).to(v.dtype) for k, v in tmpl.items()} for _ in range(K)]
+    for fuse in (True, False):
+        outs = []
+        for sharded in (True, False):
+            inner = FedBuff(fuse_scale_add=fuse)
+            opt = shard.ShardedOptimizer(inner, device=torch.device(DEV), accumulate_only=True) if sharded else inner
+            model = {k: v.to(DEV) for k, v in tmpl.items()}
+            if sharded:
+                opt.set_layout(model)
+                assert opt.plan.n_waves == 3
+            agg = None
+            for i in range(K):
+                c = S.SortedCache()
+                c[f"{i:02d}"] = S.TR({k: v.to(DEV) for k, v in ups[i].items()}, 1, rnd - i % 3)
+                agg = opt.do(agg, c, total=1, version=rnd)
+            out = opt.scale_add_agg_weights(model, agg, K)
+            torch.cuda.synchronize()
+            assert out is model
+            outs.append(model)
+        for k in tmpl:
+            assert _eq(outs[0][k], outs[1][k]), (fuse, k)
