@@ -16,8 +16,10 @@ FLAME_OK, FLAME_EINVAL, FLAME_EHIP, FLAME_ENOTSUP = 0, 1, 2, 3
 FLAME_F32, FLAME_BF16, FLAME_F16, FLAME_F64, FLAME_I64, FLAME_I32 = range(6)
 FLAME_AGG_INIT_FIRST = 1
 FLAME_AGG_SEG_RATES = 2
+FLAME_AGG_XCD_MAP = 4
 FLAME_FEDADAM, FLAME_FEDYOGI, FLAME_FEDADAGRAD = 0, 1, 2
 FLAME_OPT_STATE_ZERO = 1
+FLAME_OPT_XCD_MAP = 2
 FLAME_SEG_UNALIGNED = 1
 FLAME_HIER_TOP_ACCUM = 1
 FLAME_HIER_TOP_APPLY = 2

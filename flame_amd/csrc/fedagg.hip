@@ -525,6 +525,13 @@ __device__ __forceinline__ void store_chunk(T* op, const V16 (&ov)[kVPT]) {
     }
 }
 
+// Workgroup slot of block b when the 8 XCDs (dispatched round-robin) each take one
+// contiguous eighth of the slots (FLAME_AGG_XCD_MAP / FLAME_OPT_XCD_MAP): a bijection.
+__device__ __forceinline__ int64_t xcd_slot(int64_t b, int64_t n) {
+    const int64_t q = n / 8, r = n % 8, x = b % 8;
+    return x * q + (x < r ? x : r) + b / 8;
+}
+
 // Workgroup w reduces chunks [w*kWGC, (w+1)*kWGC).  With FLAME_DEFER_ST the full
 // chunks' output vectors stay in registers and are stored together at the end.
 template <int DT, int CU>
@@ -547,13 +554,8 @@ __device__ __forceinline__ void agg_reduce_body(const flame_segment* __restrict_
     for (int k = 0; k < kWGC; ++k)
         if (full[k]) store_chunk(op[k], ov[k]);
 #else
-#if FLAME_XCD_SWIZZLE
-    // bijection: XCD x (= blockIdx % 8) owns q + (x < r) consecutive workgroup slots
-    const int64_t q = gridDim.x / 8, r = gridDim.x % 8, x = blockIdx.x % 8;
-    const int64_t wg = x * q + (x < r ? x : r) + blockIdx.x / 8;
-#else
-    const int64_t wg = blockIdx.x;
-#endif
+    const int64_t wg = (FLAME_XCD_SWIZZLE || (flags & FLAME_AGG_XCD_MAP)) ? xcd_slot(blockIdx.x, gridDim.x)
+                                                                           : blockIdx.x;
 #pragma unroll 1
     for (int k = 0; k < kWGC; ++k) {
         const int64_t chunk = wg * kWGC + k;
@@ -750,9 +752,10 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
                                             const float* __restrict__ r32, unsigned flags, float b1,
                                             float omb1, float b2, float omb2, float eta, float tau,
                                             int64_t n_chunks) {
+    const int64_t wg = (flags & FLAME_OPT_XCD_MAP) ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
     if constexpr (G == 1) {
         (void)n_chunks;
-        fedopt_chunk<DT, VARIANT, CU>(segs, n_segs, blockIdx.x, clients, n_clients, r32, flags, b1, omb1, b2,
+        fedopt_chunk<DT, VARIANT, CU>(segs, n_segs, wg, clients, n_clients, r32, flags, b1, omb1, b2,
                                       omb2, eta, tau, nullptr);
     } else {
         using T = typename Tr<DT>::T;
@@ -762,7 +765,7 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
         unsigned pending = 0;
 #pragma unroll 1
         for (int g = 0; g < G; ++g) {
-            const int64_t chunk = static_cast<int64_t>(blockIdx.x) * G + g;
+            const int64_t chunk = wg * G + g;
             if (chunk >= n_chunks) break;
             if (fedopt_chunk<DT, VARIANT, CU>(segs, n_segs, chunk, clients, n_clients, r32, flags, b1, omb1, b2, omb2,
                                               eta, tau, held + g * 4 * kVPT * kBlock))
@@ -771,7 +774,7 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
 #pragma unroll 1
         for (int g = 0; g < G; ++g) {
             if (!(pending >> g & 1u)) continue;
-            const int64_t chunk = static_cast<int64_t>(blockIdx.x) * G + g;
+            const int64_t chunk = wg * G + g;
             const flame_segment& sg = segs[find_segment(segs, n_segs, chunk)];
             const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() +
                                static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
@@ -1389,7 +1392,7 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     if (rc) return rc;
     if ((flags & FLAME_AGG_INIT_FIRST) && n_clients < 1)
         return set_err(FLAME_EINVAL, "FLAME_AGG_INIT_FIRST needs at least one client");
-    if (flags & ~(FLAME_AGG_INIT_FIRST | FLAME_AGG_SEG_RATES))
+    if (flags & ~(FLAME_AGG_INIT_FIRST | FLAME_AGG_SEG_RATES | FLAME_AGG_XCD_MAP))
         return set_err(FLAME_EINVAL, "flame_agg_reduce: unknown flags 0x%x", flags);
     if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
         return set_err(FLAME_EINVAL, "rate array is NULL");
@@ -1431,7 +1434,7 @@ int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void* host_meta, i
     if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
     if ((flags & FLAME_AGG_INIT_FIRST) && n_clients < 1)
         return set_err(FLAME_EINVAL, "FLAME_AGG_INIT_FIRST needs at least one client");
-    if (flags & ~(FLAME_AGG_INIT_FIRST | FLAME_AGG_SEG_RATES))
+    if (flags & ~(FLAME_AGG_INIT_FIRST | FLAME_AGG_SEG_RATES | FLAME_AGG_XCD_MAP))
         return set_err(FLAME_EINVAL, "flame_agg_reduce_argmeta: unknown flags 0x%x", flags);
     const int64_t rows = (flags & FLAME_AGG_SEG_RATES) ? n_segs : 1;
     auto inside = [&](int64_t off, int64_t bytes) { return off >= 0 && off % 8 == 0 && off + bytes <= meta_bytes; };
@@ -1476,6 +1479,8 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
     if (n_clients > 0 && !rates32) return set_err(FLAME_EINVAL, "rate array is NULL");
     if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: unknown variant %d", variant);
+    if (flags & ~(FLAME_OPT_STATE_ZERO | FLAME_OPT_XCD_MAP))
+        return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt: unknown flags 0x%x", flags);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // FLAME_OPT_WGC chunks per workgroup (outputs held in LDS) for fp32 launches big enough to fill
     // the GPU several times over; one chunk per workgroup otherwise
@@ -1521,7 +1526,7 @@ int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, co
     if (n_segs <= 0 || n_clients < 0)
         return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: n_segs <= 0 or n_clients < 0");
     if (n_chunks <= 0 || n_chunks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "n_chunks out of range: %lld", (long long)n_chunks);
-    if (flags & ~FLAME_OPT_STATE_ZERO)
+    if (flags & ~(FLAME_OPT_STATE_ZERO | FLAME_OPT_XCD_MAP))
         return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt_argmeta: unknown flags 0x%x", flags);
     if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt_argmeta: unknown variant %d", variant);

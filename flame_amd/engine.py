@@ -385,6 +385,10 @@ def _launch_reduce(code, segs, rates, device, keep, *, init_first=False, seg_rat
                                                _stream_ptr(device)))
         return
     p = plan(code, segs, rates, seg_rates=seg_rates)
+    if p.n_chunks >= XCD_MAP_MIN_CHUNKS and all(s.tile_stride == 0 for s in segs):
+        # clients as separate tensors: each XCD streams a contiguous eighth of the chunks
+        # (C3 rows 16.25 -> 15.89 ms; a tiled slab loses with it)
+        flags |= N.FLAME_AGG_XCD_MAP
     dm = _staging.upload(p.meta, device)
     segp, clp, r32p, r64p = _device_ptrs(dm, p)
     with _timed("flame_agg_reduce", device, nbytes):
@@ -392,6 +396,9 @@ def _launch_reduce(code, segs, rates, device, keep, *, init_first=False, seg_rat
                                    _stream_ptr(device)))
     keep.append(dm)
 
+
+# Row-layout launches of at least this many chunks take the XCD-contiguous chunk map.
+XCD_MAP_MIN_CHUNKS = int(os.environ.get("FLAME_AMD_XCD_MAP_MIN_CHUNKS", "4096"))
 
 # Kernel-argument metadata for small launches (FLAME_AMD_ARGMETA=0 disables).
 ARGMETA = os.environ.get("FLAME_AMD_ARGMETA", "1") != "0"
@@ -460,11 +467,12 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
             _keepalive(keep, device)
             continue
         p = plan(code, segs, rates)
+        if p.n_chunks >= XCD_MAP_MIN_CHUNKS and all(s.tile_stride == 0 for s in segs):
+            opt_flags |= N.FLAME_OPT_XCD_MAP        # clients as separate tensors (see _launch_reduce)
         dm = _staging.upload(p.meta, device)
         segp, clp, r32p, _ = _device_ptrs(dm, p)
         with _timed("flame_fedopt_reduce_adapt", device, nbytes):
-            N.check(L.flame_fedopt_reduce_adapt(code, FEDOPT_VARIANT[variant],
-                                                N.FLAME_OPT_STATE_ZERO if state_zero else 0,
+            N.check(L.flame_fedopt_reduce_adapt(code, FEDOPT_VARIANT[variant], opt_flags,
                                                 segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
                                                 *[float(x) for x in h], _stream_ptr(device)))
         keep.append(dm)

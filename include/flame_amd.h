@@ -70,12 +70,17 @@ extern "C" {
 #define FLAME_AGG_SEG_RATES 2u   /* rates are [n_segs][n_clients]: one rate row per segment
                                     (independent reductions -- e.g. the middle aggregators of
                                     a node, asyncfl/middle_aggregator.py:164-256 -- in one launch) */
+#define FLAME_AGG_XCD_MAP 4u     /* workgroups take chunks XCD by XCD (each of the 8 XCDs, which get
+                                    workgroups round-robin, streams one contiguous eighth of the
+                                    chunks): faster when every client is its own tensor (rows),
+                                    slower for a tiled UpdateSlab; results are identical */
 
 /* flame_fedopt_reduce_adapt variants and flags */
 #define FLAME_FEDADAM 0
 #define FLAME_FEDYOGI 1
 #define FLAME_FEDADAGRAD 2
 #define FLAME_OPT_STATE_ZERO 1u  /* m_t, v_t were None: treat as zeros, do not read (fedopt.py:108-122) */
+#define FLAME_OPT_XCD_MAP 2u     /* as FLAME_AGG_XCD_MAP, for flame_fedopt_reduce_adapt */
 
 /* per-segment flag (flame_segment.flags) */
 #define FLAME_SEG_UNALIGNED 1    /* some pointer of this segment is not 16-byte aligned */

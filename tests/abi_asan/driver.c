@@ -41,7 +41,7 @@ int main(void) {
 
     void *fake = (void *)(uintptr_t)4096;     /* never dereferenced: checks run first */
     EXPECT_ERR(flame_agg_reduce(0, 0, NULL, 0, 1, NULL, 0, NULL, NULL, NULL), FLAME_EINVAL, "segment");
-    EXPECT_ERR(flame_agg_reduce(0, 4, fake, 1, 1, NULL, 0, NULL, NULL, NULL), FLAME_EINVAL, "unknown flags");
+    EXPECT_ERR(flame_agg_reduce(0, 8, fake, 1, 1, NULL, 0, NULL, NULL, NULL), FLAME_EINVAL, "unknown flags");
     EXPECT_ERR(flame_agg_reduce(77, 0, fake, 1, 1, fake, 1, fake, NULL, NULL), FLAME_ENOTSUP, "");
     EXPECT_ERR(flame_fedbuff_scale_add(0, fake, 1, 1, 0, NULL), FLAME_EINVAL, "goal");
     EXPECT_ERR(flame_synth_fill(0, NULL, 5, 0, 0, 0, 1.f, NULL), FLAME_EINVAL, "");
@@ -81,7 +81,7 @@ int main(void) {
                                                  .001f, NULL), FLAME_EINVAL, "outside");
     EXPECT_ERR(flame_fedopt_reduce_adapt_argmeta(0, 0, 0, blk, 4096, 1, 1, 2, 80, 96, .9f, .1f, .99f, .01f, .01f,
                                                  .001f, NULL), FLAME_EINVAL, "");
-    EXPECT_ERR(flame_fedopt_reduce_adapt_argmeta(0, 0, 2, blk, 512, 1, 1, 2, 504, 96, .9f, .1f, .99f, .01f, .01f,
+    EXPECT_ERR(flame_fedopt_reduce_adapt_argmeta(0, 0, 4, blk, 512, 1, 1, 2, 504, 96, .9f, .1f, .99f, .01f, .01f,
                                                  .001f, NULL), FLAME_EINVAL, "unknown flags");
 
     /* randomized: a table offset or count that puts a table outside the block must be refused

@@ -84,7 +84,7 @@ def test_agg_reduce_rejects_unknown_flags_without_gpu():
     from flame_amd import _native
     L = _native.lib()
     fake = ctypes.c_void_p(4096)   # never dereferenced: flags are checked on the host first
-    assert L.flame_agg_reduce(0, 4, fake, 1, 1, None, 0, None, None, None) == _native.FLAME_EINVAL
+    assert L.flame_agg_reduce(0, 8, fake, 1, 1, None, 0, None, None, None) == _native.FLAME_EINVAL
     assert b"unknown flags" in L.flame_last_error()
 
 
@@ -140,6 +140,6 @@ def test_fedopt_argmeta_validates_without_gpu():
     assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 0, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
     assert b"outside" in L.flame_last_error()
     assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 0, blk, 4096, 1, 1, 2, 80, 96, *hyper, None) == _native.FLAME_EINVAL
-    assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 2, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
+    assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 4, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
     assert b"unknown flags" in L.flame_last_error()
     assert L.flame_fedopt_reduce_adapt_argmeta(0, 7, 0, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_ENOTSUP
