@@ -467,8 +467,6 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
             _keepalive(keep, device)
             continue
         p = plan(code, segs, rates)
-        if p.n_chunks >= XCD_MAP_MIN_CHUNKS and all(s.tile_stride == 0 for s in segs):
-            opt_flags |= N.FLAME_OPT_XCD_MAP        # clients as separate tensors (see _launch_reduce)
         dm = _staging.upload(p.meta, device)
         segp, clp, r32p, _ = _device_ptrs(dm, p)
         with _timed("flame_fedopt_reduce_adapt", device, nbytes):
