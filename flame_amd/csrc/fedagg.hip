@@ -109,6 +109,11 @@ namespace {
 #define FLAME_DYN_LDS 0   // FedDyn kernel: > 0 = hold the updated histories of that many program steps in
                           // LDS (4 KiB each per workgroup) and store them in one burst (multiple of FLAME_DYN_CU)
 #endif
+#ifndef FLAME_DYN_XCD
+#define FLAME_DYN_XCD 1   // FedDyn kernel: XCD-contiguous chunk map (see FLAME_AGG_XCD_MAP); histories are
+                          // per-end rows by default: 512 x 12M fp32 -0.7 % (cache order) / -1.4 %
+                          // (other order), tools/feddyn_sweep.py, profiles/r02_feddyn_xcd_sweep.log
+#endif
 #ifndef FLAME_DYN_ST
 #define FLAME_DYN_ST FLAME_ST_NT  // FedDyn kernel: store policy of the updated histories
 #endif
@@ -1298,7 +1303,7 @@ __global__ __launch_bounds__(kBlock) void feddyn_kernel(const flame_dyn_segment*
     using X = Tr<DT>;
     constexpr int EPT = X::EPT;
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
-    const int64_t chunk = blockIdx.x;
+    const int64_t chunk = FLAME_DYN_XCD ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_dyn_segment sg = segs[s];
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;

@@ -66,6 +66,7 @@ VARIANTS = {
     "optwgc10": {"FLAME_OPT_WGC": 10},
     "optwgc8cu16": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 16},
     "optwgc8cu4": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 4},
+    "dynxcd0": {"FLAME_DYN_XCD": 0},       # round-robin chunk order (before)
     "dyncu2": {"FLAME_DYN_CU": 2},
     # updated histories held in LDS, stored G steps at a time (tools/feddyn_sweep.py)
     "dynlds8": {"FLAME_DYN_LDS": 8},
