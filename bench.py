@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--e2e-mode", default="zerocopy",
                     choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference", "eager",
-                             "shm", "shm_reference"],
+                             "shm", "shm_reference", "shard"],
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
                          "stream overlapped with the reduction; pageable: reference weights_to_model_device")
     ap.add_argument("--e2e-placement", default="slab", choices=["slab", "hbm"],
@@ -989,6 +989,10 @@ def bench_e2e(args, n, P, dev):
               with the reduction of the previous batch;
     pageable: the reference convention (weights_to_model_device: per-tensor .to(device)
               from pageable memory), then one FedAvg;
+    shard:    the parameter-sharded ingest + round: every arrival goes into
+              DeviceUpdateCache(shard=plan) (this rank's ranges, strided H2D on its side
+              stream, into the rank-local slab), then ShardedOptimizer(FedAvg).do (waves +
+              in-place gathers; at world 1 the gathers are no-ops);
     eager:    the eager top aggregator (eager_syncfl/top_aggregator.py:36-90): every arrival
               goes into a DeviceUpdateCache (H2D on its side stream) and FedAvg.do runs
               per arrival with the running total, so the reduction trails the transfers;
@@ -1006,7 +1010,7 @@ def bench_e2e(args, n, P, dev):
     n = min(n, 64)
     batch = 8
     mode = args.e2e_mode
-    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode in ("zerocopy", "copy", "eager")))
+    host = torch.empty((n, P), dtype=torch.float32, pin_memory=(mode in ("zerocopy", "copy", "eager", "shard")))
     tmp = torch.empty(P, dtype=torch.float32, device=dev)
     for i in range(n):
         engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
@@ -1054,6 +1058,12 @@ def bench_e2e(args, n, P, dev):
     if mode == "eager":
         from flame_amd.ingest import DeviceUpdateCache
         ecache = DeviceUpdateCache(device=dev, placement=args.e2e_placement, capacity=n)
+    if mode == "shard":
+        from flame_amd import shard
+        from flame_amd.ingest import DeviceUpdateCache
+        sopt = shard.ShardedOptimizer(opt, device=dev)
+        sopt.set_layout({"model": torch.empty(P, dtype=torch.float32, device="meta")})
+        scache = DeviceUpdateCache(device=dev, placement="slab", capacity=n, shard=sopt.plan)
     torch.cuda.synchronize()
 
     def step():
@@ -1090,6 +1100,10 @@ def bench_e2e(args, n, P, dev):
                 del msg
             opt.do({"model": base}, cache, total=total)
             del cache, w
+        elif mode == "shard":
+            for i in range(n):   # arrival i: this rank's ranges -> the rank-local slab (side stream)
+                scache[f"{i:05d}"] = TR({"model": host[i]}, int(counts[i]))
+            sopt.do({"model": base}, scache, total=total)
         elif mode == "eager":
             base_w = {"model": base}
             running = 0
