@@ -546,7 +546,68 @@ def fedopt_eager():
         print(f"wrote {sort}_eager.npz")
 
 
-CASES = {"fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def subset_cases():
+    """Updates carrying a SUBSET of the model's keys: FedAvg adds each client's keys only
+    (fedavg.py:93 ``for k, v in tres.weights.items()``); FedBuff's None-start aggregate takes
+    the first arrival's keys and later arrivals add theirs (fedbuff.py:143-157)."""
+    shapes = {"w": ((300, 7), torch.float32), "b": ((7,), torch.bfloat16), "h": ((129,), torch.float16),
+              "nbt": ((), torch.int64)}
+    subsets = [("w", "b", "h", "nbt"), ("w", "nbt"), ("b",), ("w", "b", "h"), ("h",), ("w",), ("nbt", "b")]
+    gen = torch.Generator().manual_seed(77)
+    rng = np.random.default_rng(77)
+    base = small_weights(gen, shapes, 1.0)
+    clients = []
+    for ks in subsets:
+        c = small_weights(gen, {k: shapes[k] for k in ks}, 1e-2)
+        if "nbt" in c:
+            c["nbt"] = torch.randint(-50, 50, (), generator=gen, dtype=torch.int64)
+        clients.append(c)
+    n = len(clients)
+    ids = end_ids(rng, n)
+    counts = [int(x) for x in rng.integers(1, 1001, n)]
+    cache = Cache()
+    for e, w, c in zip(ids, clients, counts):
+        cache[e] = TrainResult(w, c)
+    order = list(cache.iterkeys())
+    out = optimizer_provider.get("fedavg").do(deepcopy(base), cache, total=sum(counts), num_trainers=n)
+    fw = FixtureWriter()
+    fw.meta.update({"kind": "fedavg", "n": n, "end_ids": ids, "counts": counts, "order": order,
+                    "total": sum(counts), "subsets": [list(k) for k in subsets]})
+    fw.put_weights("base", base)
+    for i, w in enumerate(clients):
+        fw.put_weights(f"client{i}", w)
+    fw.put_weights("out", out)
+    fw.save(os.path.join(HERE, "fedavg_subsets.npz"))
+    print("wrote fedavg_subsets.npz")
+
+    # FedBuff: one arrival per do(), the first carrying every key (it fixes the aggregate's
+    # keys), later ones subsets; then scale_add into the float weights
+    fshapes = {k: v for k, v in shapes.items() if k != "nbt"}
+    fsub = [("w", "b", "h"), ("w",), ("b", "h"), ("h",), ("w", "b")]
+    ups = [small_weights(gen, {k: fshapes[k] for k in ks}, 1e-2) for ks in fsub]
+    stale = [1, 0, 3, 2, 1]
+    rnd, goal = 6, len(fsub)
+    opt = optimizer_provider.get("fedbuff")
+    agg = None
+    for i, u in enumerate(ups):
+        c = Cache()
+        c[f"t{i}"] = TrainResult(u, 1, rnd - stale[i])
+        agg = opt.do(agg, c, total=1, version=rnd)
+    weights0 = small_weights(gen, fshapes, 1.0)
+    new = opt.scale_add_agg_weights(deepcopy(weights0), agg, goal)
+    fw = FixtureWriter()
+    fw.meta.update({"kind": "fedbuff_subsets", "round": rnd, "stale": stale, "goal": goal,
+                    "subsets": [list(k) for k in fsub]})
+    for i, u in enumerate(ups):
+        fw.put_weights(f"update{i}", u)
+    fw.put_weights("agg", agg)
+    fw.put_weights("weights0", weights0)
+    fw.put_weights("out", new)
+    fw.save(os.path.join(HERE, "fedbuff_subsets.npz"))
+    print("wrote fedbuff_subsets.npz")
+
+
+CASES = {"subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -572,6 +633,7 @@ def main():
     hier_fedbuff_small()
     fedopt_mixed_rounds()
     fedopt_eager()
+    subset_cases()
 
 
 if __name__ == "__main__":

@@ -173,6 +173,27 @@ def run_fedbuff_seq(fx, make_opt, device):
     return res
 
 
+def run_fedbuff_subsets(fx, make_opt, device):
+    """Arrivals with key subsets, one per do(); twice: the aggregate read only at the end
+    (every arrival still queued in a deferred aggregate), then read after every arrival."""
+    m = fx.meta
+    res = []
+    for read_each in (False, True):
+        opt = make_opt("fedbuff")
+        agg = None
+        for i in range(m["goal"]):
+            cache = SortedCache()
+            cache[f"t{i}"] = TR(to_dev(fx.weights(f"update{i}"), device), 1, m["round"] - m["stale"][i])
+            agg = opt.do(agg, cache, total=1, version=m["round"])
+            if read_each:
+                to_cpu(agg)
+        res.append((f"agg/read_each={read_each}", to_cpu(agg), fx.weights("agg")))
+        weights = to_dev(fx.weights("weights0"), device)
+        new = opt.scale_add_agg_weights(weights, agg, m["goal"])
+        res.append((f"out/read_each={read_each}", new, fx.weights("out")))
+    return res
+
+
 def run_fedbuff_none_multi(fx, make_opt, device):
     m = fx.meta
     cache = SortedCache()
@@ -419,6 +440,8 @@ BITWISE_FIXTURES = [
     ("fedbuff_seq_fp32.npz", run_fedbuff_seq),
     ("fedbuff_seq_bf16.npz", run_fedbuff_seq),
     ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
+    ("fedavg_subsets.npz", run_fedavg),
+    ("fedbuff_subsets.npz", run_fedbuff_subsets),
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
