@@ -607,7 +607,41 @@ def subset_cases():
     print("wrote fedbuff_subsets.npz")
 
 
-CASES = {"subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def fedbuff_dtypes():
+    """FedBuff over every dtype a state_dict carries: f32 / bf16 / f16 / f64 keys and an int64
+    buffer (tmp = (v * rate).to(int64), fedbuff.py:149-157), arrivals one per do(); the
+    scale_add covers the float keys (an int base raises in the reference)."""
+    gen = torch.Generator().manual_seed(88)
+    shapes = {"f32": ((257,), torch.float32), "bf16": ((300,), torch.bfloat16), "f16": ((129,), torch.float16),
+              "f64": ((65,), torch.float64), "i64": ((9,), torch.int64)}
+    goal, rnd = 6, 9
+    stale = [0, 2, 1, 3, 0, 1]
+    ups = []
+    for _ in range(goal):
+        u = small_weights(gen, shapes, 1e-2)
+        u["i64"] = torch.randint(-500, 500, (9,), generator=gen, dtype=torch.int64)
+        ups.append(u)
+    opt = optimizer_provider.get("fedbuff")
+    agg = None
+    fw = FixtureWriter()
+    for i, u in enumerate(ups):
+        c = Cache()
+        c[f"t{i}"] = TrainResult(u, 1, rnd - stale[i])
+        agg = opt.do(agg, c, total=1, version=rnd)
+        fw.put_weights(f"agg{i}", deepcopy(agg))
+    fshapes = {k: v for k, v in shapes.items() if k != "i64"}
+    weights0 = small_weights(gen, fshapes, 1.0)
+    new = opt.scale_add_agg_weights(deepcopy(weights0), agg, goal)
+    fw.meta.update({"kind": "fedbuff_dtypes", "goal": goal, "round": rnd, "stale": stale})
+    for i, u in enumerate(ups):
+        fw.put_weights(f"update{i}", u)
+    fw.put_weights("weights0", weights0)
+    fw.put_weights("out", new)
+    fw.save(os.path.join(HERE, "fedbuff_dtypes.npz"))
+    print("wrote fedbuff_dtypes.npz")
+
+
+CASES = {"fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -634,6 +668,7 @@ def main():
     fedopt_mixed_rounds()
     fedopt_eager()
     subset_cases()
+    fedbuff_dtypes()
 
 
 if __name__ == "__main__":

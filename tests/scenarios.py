@@ -194,6 +194,24 @@ def run_fedbuff_subsets(fx, make_opt, device):
     return res
 
 
+def run_fedbuff_dtypes(fx, make_opt, device):
+    """Every-dtype FedBuff sequence: the aggregate after each arrival, then scale_add of the
+    float keys."""
+    m = fx.meta
+    opt = make_opt("fedbuff")
+    agg = None
+    res = []
+    for i in range(m["goal"]):
+        cache = SortedCache()
+        cache[f"t{i}"] = TR(to_dev(fx.weights(f"update{i}"), device), 1, m["round"] - m["stale"][i])
+        agg = opt.do(agg, cache, total=1, version=m["round"])
+        res.append((f"agg{i}", to_cpu(agg), fx.weights(f"agg{i}")))
+    weights = to_dev(fx.weights("weights0"), device)
+    new = opt.scale_add_agg_weights(weights, agg, m["goal"])
+    res.append(("out", new, fx.weights("out")))
+    return res
+
+
 def run_fedbuff_none_multi(fx, make_opt, device):
     m = fx.meta
     cache = SortedCache()
@@ -442,6 +460,7 @@ BITWISE_FIXTURES = [
     ("fedbuff_none_multi.npz", run_fedbuff_none_multi),
     ("fedavg_subsets.npz", run_fedavg),
     ("fedbuff_subsets.npz", run_fedbuff_subsets),
+    ("fedbuff_dtypes.npz", run_fedbuff_dtypes),
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
