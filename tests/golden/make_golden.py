@@ -641,7 +641,53 @@ def fedbuff_dtypes():
     print("wrote fedbuff_dtypes.npz")
 
 
-CASES = {"fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def nonfinite():
+    """A diverged trainer's updates (NaN, +-inf, values whose weighted sums overflow) through
+    the reference's FedAvg and FedBuff (+ scale_add), every float dtype."""
+    fw = FixtureWriter()
+    n, P = 5, 4099
+    counts = [100 + 7 * i for i in range(n)]
+    stale = [i % 3 for i in range(n)]
+    rnd = 9
+    tags = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.float64: "f64"}
+    for dt, tag in tags.items():
+        g = torch.Generator().manual_seed(61)
+        big = {torch.float32: 3.0e38, torch.bfloat16: 3.0e38, torch.float16: 6.0e4, torch.float64: 1.7e308}[dt]
+        base = torch.randn(P, generator=g, dtype=torch.float64).to(dt)
+        cl = []
+        for i in range(n):
+            c = (torch.randn(P, generator=g, dtype=torch.float64) * 1e-2).to(dt)
+            c[i::97] = float("nan")
+            c[(i + 11)::89] = float("inf")
+            c[(i + 23)::83] = -float("inf")
+            c[(i + 37)::79] = big
+            c[(i + 41)::73] = -big
+            cl.append(c)
+        base[::101] = float("nan")
+        base[7::103] = float("inf")
+        cache = Cache()
+        for i, c in enumerate(cl):
+            cache[f"e{i}"] = TrainResult({"w": c}, counts[i])
+        avg = optimizer_provider.get("fedavg").do({"w": base.clone()}, cache, total=sum(counts))
+        fb, agg = optimizer_provider.get("fedbuff"), None
+        for i, c in enumerate(cl):
+            one = Cache()
+            one["a"] = TrainResult({"w": c}, 1, rnd - stale[i])
+            agg = fb.do(agg, one, total=1, version=rnd)
+        w = fb.scale_add_agg_weights({"w": base.clone()}, agg, n)
+        fw.put_weights(f"{tag}/base", {"w": base})
+        for i, c in enumerate(cl):
+            fw.put_weights(f"{tag}/client{i}", {"w": c})
+        fw.put_weights(f"{tag}/fedavg", avg)
+        fw.put_weights(f"{tag}/fedbuff_agg", agg)
+        fw.put_weights(f"{tag}/fedbuff_out", w)
+    fw.meta.update({"kind": "nonfinite", "n": n, "counts": counts, "stale": stale, "round": rnd,
+                    "float_dtypes": list(tags.values())})
+    fw.save(os.path.join(HERE, "nonfinite.npz"))
+    print("wrote nonfinite.npz")
+
+
+CASES = {"nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -669,6 +715,7 @@ def main():
     fedopt_eager()
     subset_cases()
     fedbuff_dtypes()
+    nonfinite()
 
 
 if __name__ == "__main__":

@@ -572,3 +572,26 @@ def oracle_sync_hierarchy_round(middles, top_weights, *, with_delta=False, updat
     for gi in range(len(key_groups or ())):
         after_group(gi)
     return top_weights, (deltas if with_delta else None)
+
+
+def run_nonfinite(fx, make_opt, device):
+    """nonfinite.npz: per float dtype, FedAvg and FedBuff (+ scale_add) over a diverged
+    trainer's updates; yields (label, got, expected) compared with assert_same_nonfinite."""
+    m = fx.meta
+    for tag in m["float_dtypes"]:
+        base = fx.weights(f"{tag}/base")["w"]
+        cl = [fx.weights(f"{tag}/client{i}")["w"] for i in range(m["n"])]
+        cache = SortedCache()
+        for i, c in enumerate(cl):
+            cache[f"e{i}"] = TR({"w": c.to(device)}, m["counts"][i])
+        got = make_opt("fedavg").do({"w": base.clone().to(device)}, cache, total=sum(m["counts"]))
+        yield f"{tag}/fedavg", got["w"], fx.weights(f"{tag}/fedavg")["w"]
+        fb, agg = make_opt("fedbuff"), None
+        for i, c in enumerate(cl):
+            one = SortedCache()
+            one["a"] = TR({"w": c.to(device)}, 1, m["round"] - m["stale"][i])
+            agg = fb.do(agg, one, total=1, version=m["round"])
+        yield f"{tag}/fedbuff_agg", to_cpu(agg)["w"], fx.weights(f"{tag}/fedbuff_agg")["w"]
+        w = {"w": base.clone().to(device)}
+        fb.scale_add_agg_weights(w, agg, m["n"])
+        yield f"{tag}/fedbuff_out", w["w"], fx.weights(f"{tag}/fedbuff_out")["w"]

@@ -1058,6 +1058,17 @@ def test_shm_receiver_registered_segment_to_fedavg(where):
             seg.unlink()
 
 
+def test_golden_nonfinite(golden):
+    """nonfinite.npz, generated by the reference: the HIP path puts NaN and +-inf where the
+    reference's torch-CPU ops do (FedAvg, FedBuff aggregate, FedBuff scale_add; f32 / bf16 /
+    f16 / f64), every other element bitwise."""
+    n = 0
+    for label, got, exp in S.run_nonfinite(golden("nonfinite.npz"), make_amd, DEV):
+        S.assert_same_nonfinite(f"nonfinite:{label}", got, exp)
+        n += 1
+    assert n == 12
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 def test_nonfinite_updates_match_oracle(dtype):
     """A diverged trainer (NaN, +-inf, overflowing sums): FedAvg and FedBuff + scale_add put

@@ -29,6 +29,16 @@ def test_oracle_bitwise(golden, name, driver):
         S.assert_bitwise(f"{name}:{label}", got, exp)
 
 
+def test_oracle_nonfinite(golden):
+    """nonfinite.npz (the reference's FedAvg / FedBuff over a diverged trainer's updates):
+    NaN and +-inf where the reference puts them, every other element bitwise."""
+    labels = []
+    for label, got, exp in S.run_nonfinite(golden("nonfinite.npz"), make_oracle, "cpu"):
+        S.assert_same_nonfinite(f"nonfinite:{label}", got, exp)
+        labels.append(label)
+    assert len(labels) == 12
+
+
 @pytest.mark.parametrize("name", S.FEDOPT_FIXTURES)
 def test_oracle_fedopt(golden, name):
     for label, got, exp in S.run_fedopt(golden(name), make_oracle, "cpu"):
