@@ -190,7 +190,10 @@ class OracleFedOPT(OracleFedAvg):
             self.m_t, self.v_t = {}, {}
         new = OrderedDict()
         for k in cur.keys():
-            if avg[k].dtype == torch.float32 and cur[k].dtype == torch.float32:
+            # the C kernel takes all-fp32 state; anything else (e.g. FedAdaGrad's v of an int64
+            # buffer stays int64: `v + d**2` on int64) keeps the reference's torch op sequence
+            if (avg[k].dtype == torch.float32 and cur[k].dtype == torch.float32
+                    and (first or (self.m_t[k].dtype == torch.float32 and self.v_t[k].dtype == torch.float32))):
                 if first:
                     self.m_t[k] = torch.zeros_like(avg[k])
                     self.v_t[k] = torch.zeros_like(avg[k])

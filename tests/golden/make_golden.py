@@ -255,14 +255,16 @@ def fedopt_rounds(sort):
     print("wrote", sort)
 
 
-def fedopt_mixed_rounds():
+def fedopt_mixed_rounds(sort="fedadam", name="fedadam_mixed_rounds.npz", seed=71, f16=False):
     """FedAdam over a BatchNorm-like model: fp32 weights, a bf16 tensor and an int64
     num_batches_tracked buffer (which the reference silently promotes to fp32 in the
-    adaptive step, fedopt.py:125-129)."""
-    gen = torch.Generator().manual_seed(71)
+    adaptive step, fedopt.py:125-129).  ``f16``: an fp16 tensor too (FedYogi / FedAdaGrad)."""
+    gen = torch.Generator().manual_seed(seed)
     shapes = {"w": ((40, 30), torch.float32), "bf": ((70,), torch.bfloat16), "nbt": ((), torch.int64)}
+    if f16:
+        shapes["hf"] = ((53,), torch.float16)
     weights = small_weights(gen, shapes, 1.0)
-    opt = optimizer_provider.get("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    opt = optimizer_provider.get(sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
     n, rounds = 5, 4
     fw = FixtureWriter()
     fw.put_weights("weights0", weights)
@@ -284,10 +286,15 @@ def fedopt_mixed_rounds():
         if opt.m_t is not None:
             fw.put_weights(f"r{r}/m", opt.m_t)
             fw.put_weights(f"r{r}/v", opt.v_t)
-    fw.meta.update({"kind": "fedopt_rounds", "sort": "fedadam", "n": n, "rounds": rounds,
+    fw.meta.update({"kind": "fedopt_rounds", "sort": sort, "n": n, "rounds": rounds,
                     "counts": all_counts, "beta_1": 0.9, "beta_2": 0.99, "eta": 1e-2, "tau": 1e-3})
-    fw.save(os.path.join(HERE, "fedadam_mixed_rounds.npz"))
-    print("wrote fedadam_mixed_rounds.npz")
+    fw.save(os.path.join(HERE, name))
+    print("wrote", name)
+
+
+def fedopt_mixed_more():
+    fedopt_mixed_rounds("fedyogi", "fedyogi_mixed_rounds.npz", 72, f16=True)
+    fedopt_mixed_rounds("fedadagrad", "fedadagrad_mixed_rounds.npz", 73, f16=True)
 
 
 def hier_fedbuff_small():
@@ -687,7 +694,7 @@ def nonfinite():
     print("wrote nonfinite.npz")
 
 
-CASES = {"nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+CASES = {"fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -716,6 +723,7 @@ def main():
     subset_cases()
     fedbuff_dtypes()
     nonfinite()
+    fedopt_mixed_more()
 
 
 if __name__ == "__main__":

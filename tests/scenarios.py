@@ -466,7 +466,8 @@ BITWISE_FIXTURES = [
     ("fedgft_rounds.npz", run_fedgft),
     ("hier_fedavg_small.npz", run_hier_fedavg),
 ]
-FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz"]
+FEDOPT_FIXTURES = ["fedadam_rounds.npz", "fedyogi_rounds.npz", "fedadagrad_rounds.npz", "fedadam_mixed_rounds.npz",
+                   "fedyogi_mixed_rounds.npz", "fedadagrad_mixed_rounds.npz"]
 
 
 def delta_torch(a, b):
