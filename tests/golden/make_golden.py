@@ -297,27 +297,30 @@ def fedopt_mixed_more():
     fedopt_mixed_rounds("fedadagrad", "fedadagrad_mixed_rounds.npz", 73, f16=True)
 
 
-def hier_fedbuff_small():
-    """2 middle aggregators x 3 trainers -> top FedBuff (config 5 in miniature)."""
-    gen = torch.Generator().manual_seed(61)
-    shapes = {"w": ((20, 7), torch.bfloat16), "b": ((7,), torch.bfloat16)}
+def hier_fedbuff_small(name="hier_fedbuff_small.npz", shapes=None, mids_n=2, arrivals=3, seed=61,
+                       mid_versions=None):
+    """``mids_n`` middle aggregators x ``arrivals`` trainers -> top FedBuff (config 5 in
+    miniature; the default is the original 2 x 3 bf16 fixture)."""
+    gen = torch.Generator().manual_seed(seed)
+    shapes = shapes or {"w": ((20, 7), torch.bfloat16), "b": ((7,), torch.bfloat16)}
     top_w0 = small_weights(gen, shapes, 1.0)
     rnd = 3
+    mid_versions = mid_versions or [rnd - m for m in range(mids_n)]
     fw = FixtureWriter()
     fw.put_weights("top_w0", top_w0)
     mids = []
-    for m in range(2):
+    for m in range(mids_n):
         opt = optimizer_provider.get("fedbuff")
         mid_w = deepcopy(top_w0)  # middle starts from the distributed global model
         agg = None
-        for t in range(3):
+        for t in range(arrivals):
             u = small_weights(gen, shapes, 1e-2)
             fw.put_weights(f"m{m}/update{t}", u)
             cache = Cache()
             cache[f"m{m}t{t}"] = TrainResult(u, 10 + t, rnd - t % 2)
             agg = opt.do(agg, cache, total=10 + t, version=rnd)
         prev = deepcopy(mid_w)
-        mid_w = opt.scale_add_agg_weights(mid_w, agg, 3)
+        mid_w = opt.scale_add_agg_weights(mid_w, agg, arrivals)
         delta = {k: mid_w[k] - prev[k] for k in mid_w}   # common/util.py:152-159
         fw.put_weights(f"m{m}/delta", delta)
         mids.append(delta)
@@ -325,13 +328,22 @@ def hier_fedbuff_small():
     agg = None
     for m, d in enumerate(mids):
         cache = Cache()
-        cache[f"mid{m}"] = TrainResult(d, 30, rnd - m)
+        cache[f"mid{m:02d}"] = TrainResult(d, 30, mid_versions[m])
         agg = opt.do(agg, cache, total=30, version=rnd)
-    top = opt.scale_add_agg_weights(deepcopy(top_w0), agg, 2)
+    top = opt.scale_add_agg_weights(deepcopy(top_w0), agg, mids_n)
     fw.put_weights("top_out", top)
-    fw.meta.update({"kind": "hier_fedbuff", "round": rnd})
-    fw.save(os.path.join(HERE, "hier_fedbuff_small.npz"))
-    print("wrote hier_fedbuff_small.npz")
+    fw.meta.update({"kind": "hier_fedbuff", "round": rnd, "mids": mids_n, "arrivals": arrivals,
+                    "mid_versions": mid_versions})
+    fw.save(os.path.join(HERE, name))
+    print("wrote", name)
+
+
+def hier_fedbuff_wide():
+    """18 middles x 2 arrivals over f32 / f16 / bf16 keys: the one-pass hierarchy's launch
+    takes the LDS-held store groups (>= 16 middles) with a partial second group."""
+    hier_fedbuff_small("hier_fedbuff_wide.npz",
+                       {"w": ((20, 7), torch.float32), "h": ((33,), torch.float16), "b": ((7,), torch.bfloat16)},
+                       mids_n=18, arrivals=2, seed=62, mid_versions=[3 - m % 3 for m in range(18)])
 
 
 FEDDYN_SHAPES = {"w": ((40, 30), torch.float32), "b": ((30,), torch.float32),
@@ -694,7 +706,7 @@ def nonfinite():
     print("wrote nonfinite.npz")
 
 
-CASES = {"fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -724,6 +736,7 @@ def main():
     fedbuff_dtypes()
     nonfinite()
     fedopt_mixed_more()
+    hier_fedbuff_wide()
 
 
 if __name__ == "__main__":

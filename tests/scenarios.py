@@ -274,22 +274,29 @@ def check_fedopt_eager(res):
         assert_close_fedopt(label, got, exp, elementwise=(r == 0))
 
 
+def hier_shape(m):
+    """(middles, arrivals per middle, the top's version of each middle) of a hier fixture."""
+    mids, arr = m.get("mids", 2), m.get("arrivals", 3)
+    return mids, arr, m.get("mid_versions", [m["round"] - i for i in range(mids)])
+
+
 def run_hier(fx, make_opt, device, delta_fn):
     m = fx.meta
     rnd = m["round"]
+    mids, arr, mver = hier_shape(m)
     top_w0 = fx.weights("top_w0")
     res = []
     deltas = []
-    for mid in range(2):
+    for mid in range(mids):
         opt = make_opt("fedbuff")
         mid_w = to_dev(top_w0, device)
         agg = None
-        for t in range(3):
+        for t in range(arr):
             cache = SortedCache()
             cache[f"m{mid}t{t}"] = TR(to_dev(fx.weights(f"m{mid}/update{t}"), device), 10 + t, rnd - t % 2)
             agg = opt.do(agg, cache, total=10 + t, version=rnd)
         prev = deepcopy(mid_w)
-        mid_w = opt.scale_add_agg_weights(mid_w, agg, 3)
+        mid_w = opt.scale_add_agg_weights(mid_w, agg, arr)
         delta = delta_fn(mid_w, prev)
         res.append((f"m{mid}/delta", to_cpu(delta), fx.weights(f"m{mid}/delta")))
         deltas.append(delta)
@@ -297,11 +304,14 @@ def run_hier(fx, make_opt, device, delta_fn):
     agg = None
     for mid, d in enumerate(deltas):
         cache = SortedCache()
-        cache[f"mid{mid}"] = TR(d, 30, rnd - mid)
+        cache[f"mid{mid:02d}"] = TR(d, 30, mver[mid])
         agg = opt.do(agg, cache, total=30, version=rnd)
-    top = opt.scale_add_agg_weights(to_dev(top_w0, device), agg, 2)
+    top = opt.scale_add_agg_weights(to_dev(top_w0, device), agg, mids)
     res.append(("top_out", to_cpu(top), fx.weights("top_out")))
     return res
+
+
+HIER_FIXTURES = ["hier_fedbuff_small.npz", "hier_fedbuff_wide.npz"]
 
 
 def run_hier_fedavg(fx, make_opt, device):

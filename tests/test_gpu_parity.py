@@ -82,58 +82,64 @@ def test_golden_feddyn_pingpong(golden):
         S.assert_bitwise(f"feddyn_pingpong:{label}", got, exp)
 
 
-def test_golden_hier_torch_delta(golden):
-    for label, got, exp in S.run_hier(golden("hier_fedbuff_small.npz"), make_amd, DEV, S.delta_torch):
-        S.assert_bitwise(label, got, exp)
+@pytest.mark.parametrize("name", S.HIER_FIXTURES)
+def test_golden_hier_torch_delta(golden, name):
+    for label, got, exp in S.run_hier(golden(name), make_amd, DEV, S.delta_torch):
+        S.assert_bitwise(f"{name}:{label}", got, exp)
 
 
-def test_golden_hier_fused_delta(golden):
+@pytest.mark.parametrize("name", S.HIER_FIXTURES)
+def test_golden_hier_fused_delta(golden, name):
     """Middle aggregator using the fused scale_add+delta kernel."""
-    fx = golden("hier_fedbuff_small.npz")
+    fx = golden(name)
     m = fx.meta
     rnd = m["round"]
+    mids, arr, _ = S.hier_shape(m)
     top_w0 = fx.weights("top_w0")
-    for mid in range(2):
+    for mid in range(mids):
         opt = make_amd("fedbuff")
         mid_w = S.to_dev(top_w0, DEV)
         agg = None
-        for t in range(3):
+        for t in range(arr):
             c = S.SortedCache()
             c[f"m{mid}t{t}"] = S.TR(S.to_dev(fx.weights(f"m{mid}/update{t}"), DEV), 10 + t, rnd - t % 2)
             agg = opt.do(agg, c, total=10 + t, version=rnd)
-        new, delta = opt.scale_add_agg_weights_with_delta(mid_w, agg, 3)
+        new, delta = opt.scale_add_agg_weights_with_delta(mid_w, agg, arr)
         assert new is mid_w
         S.assert_bitwise(f"m{mid}/delta", delta, fx.weights(f"m{mid}/delta"))
 
 
+@pytest.mark.parametrize("name", S.HIER_FIXTURES)
 @pytest.mark.parametrize("update_middle_weights", [True, False])
-def test_golden_hier_one_pass(golden, update_middle_weights):
-    """The whole 2-middle x 3-arrival hierarchy of the reference-generated fixture in ONE
-    flame_hier_fedbuff launch (hierarchy_round): middle deltas and the top model bitwise
-    equal the reference's (make_golden.py drove flame's own FedBuff + delta_weights)."""
+def test_golden_hier_one_pass(golden, name, update_middle_weights):
+    """A reference-generated hierarchy (2 middles x 3 arrivals, bf16; 18 x 2 over f32 / f16 /
+    bf16 -- LDS-held store groups) in ONE flame_hier_fedbuff launch per dtype
+    (hierarchy_round): middle deltas and the top model bitwise equal the reference's
+    (make_golden.py drove flame's own FedBuff + delta_weights)."""
     from flame_amd import engine
     from flame_amd.optimizer.fedbuff import hierarchy_round
-    fx = golden("hier_fedbuff_small.npz")
+    fx = golden(name)
     rnd = fx.meta["round"]
+    mids, arr, mver = S.hier_shape(fx.meta)
     top_w0 = fx.weights("top_w0")
     middles = []
     shared = S.to_dev(top_w0, DEV)
-    for mid in range(2):
+    for mid in range(mids):
         opt, agg = make_amd("fedbuff"), None
-        for t in range(3):
+        for t in range(arr):
             c = S.SortedCache()
             c[f"m{mid}t{t}"] = S.TR(S.to_dev(fx.weights(f"m{mid}/update{t}"), DEV), 10 + t, rnd - t % 2)
             agg = opt.do(agg, c, total=10 + t, version=rnd)
-        middles.append((S.to_dev(top_w0, DEV) if update_middle_weights else shared, agg, 3, rnd - mid))
+        middles.append((S.to_dev(top_w0, DEV) if update_middle_weights else shared, agg, arr, mver[mid]))
     top = S.to_dev(top_w0, DEV)
     engine.kernel_events = []
     try:
-        _, deltas = hierarchy_round(middles, None, version=rnd, top_weights=top, top_goal=2, with_delta=True,
+        _, deltas = hierarchy_round(middles, None, version=rnd, top_weights=top, top_goal=mids, with_delta=True,
                                     update_middle_weights=update_middle_weights)
         assert [e[0] for e in engine.kernel_events] == ["flame_hier_fedbuff"] * len({v.dtype for v in top.values()})
     finally:
         engine.kernel_events = None
-    for mid in range(2):
+    for mid in range(mids):
         S.assert_bitwise(f"m{mid}/delta", S.to_cpu(deltas[mid]), fx.weights(f"m{mid}/delta"))
     S.assert_bitwise("top_out", S.to_cpu(top), fx.weights("top_out"))
 

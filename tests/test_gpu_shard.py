@@ -164,33 +164,37 @@ def _hier_fixture_worker(rank, world, port, q):
         from fixture_io import Fixture
         from flame_amd import engine, shard
         from flame_amd.ingest import DeviceUpdateCache
-        fx = Fixture(os.path.join(GOLD, "hier_fedbuff_small.npz"))
-        rnd = fx.meta["round"]
-        top_w0 = S.to_dev(fx.weights("top_w0"), DEV)
-        hier = shard.ShardedHierarchy(top_w0, align=8)
-        ok = hier.plan.n_waves == 2
-        dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=hier.plan)
-        middles = []
-        for mid in range(2):
-            opt, agg = hier.middle_optimizer(), None
-            for t in range(3):
-                key = f"m{mid}t{t}"
-                dc[key] = S.TR(fx.weights(f"m{mid}/update{t}"), 10 + t, rnd - t % 2)
-                c = S.SortedCache()
-                c[key] = dc.pop(key)
-                agg = opt.do(agg, c, total=10 + t, version=rnd)
-            middles.append(({k: v.clone() for k, v in top_w0.items()}, agg, 3, rnd - mid))
-        top = {k: v.clone() for k, v in top_w0.items()}
-        engine.kernel_events = []
-        _, deltas = hier.round(middles, None, version=rnd, top_weights=top, top_goal=2, with_delta=True)
-        names = [e[0] for e in engine.kernel_events]
-        engine.kernel_events = None
-        ok = ok and names == ["flame_hier_fedbuff"] * hier.plan.n_waves      # one pass per wave
-        torch.cuda.synchronize()
-        ok = ok and all(_eq(top[k], fx.weights("top_out")[k]) for k in top)
-        for mid in range(2):
-            exp = hier.plan.slice_update(fx.weights(f"m{mid}/delta"))
-            ok = ok and all(_eq(deltas[mid][n], exp[n]) for n in exp)
+        ok = True
+        for name in S.HIER_FIXTURES:        # 2 x 3 bf16; 18 x 2 over f32 / f16 / bf16 (LDS groups)
+            fx = Fixture(os.path.join(GOLD, name))
+            rnd = fx.meta["round"]
+            mids, arr, mver = S.hier_shape(fx.meta)
+            top_w0 = S.to_dev(fx.weights("top_w0"), DEV)
+            hier = shard.ShardedHierarchy(top_w0, align=8)
+            ok = ok and hier.plan.n_waves == 2
+            dc = DeviceUpdateCache(device=DEV, placement="slab", capacity=mids * arr, shard=hier.plan)
+            middles = []
+            for mid in range(mids):
+                opt, agg = hier.middle_optimizer(), None
+                for t in range(arr):
+                    key = f"m{mid}t{t}"
+                    dc[key] = S.TR(fx.weights(f"m{mid}/update{t}"), 10 + t, rnd - t % 2)
+                    c = S.SortedCache()
+                    c[key] = dc.pop(key)
+                    agg = opt.do(agg, c, total=10 + t, version=rnd)
+                middles.append(({k: v.clone() for k, v in top_w0.items()}, agg, arr, mver[mid]))
+            top = {k: v.clone() for k, v in top_w0.items()}
+            engine.kernel_events = []
+            _, deltas = hier.round(middles, None, version=rnd, top_weights=top, top_goal=mids, with_delta=True)
+            names = [e[0] for e in engine.kernel_events]
+            engine.kernel_events = None
+            # one pass per wave and dtype, no separate launches
+            ok = ok and set(names) == {"flame_hier_fedbuff"} and len(names) >= hier.plan.n_waves
+            torch.cuda.synchronize()
+            ok = ok and all(_eq(top[k], fx.weights("top_out")[k]) for k in top)
+            for mid in range(mids):
+                exp = hier.plan.slice_update(fx.weights(f"m{mid}/delta"))
+                ok = ok and all(_eq(deltas[mid][n], exp[n]) for n in exp)
         q.put((rank, bool(ok)))
     except Exception:  # noqa: BLE001
         import traceback

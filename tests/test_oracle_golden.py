@@ -69,9 +69,10 @@ def test_oracle_fedopt_single_round_elementwise(golden, name):
             S.assert_close_fedopt(f"{name}:r{r}/{key}", got, exp[key])
 
 
-def test_oracle_hier(golden):
-    for label, got, exp in S.run_hier(golden("hier_fedbuff_small.npz"), make_oracle, "cpu", S.delta_torch):
-        S.assert_bitwise(label, got, exp)
+@pytest.mark.parametrize("name", S.HIER_FIXTURES)
+def test_oracle_hier(golden, name):
+    for label, got, exp in S.run_hier(golden(name), make_oracle, "cpu", S.delta_torch):
+        S.assert_bitwise(f"{name}:{label}", got, exp)
 
 
 def test_oracle_synth_matches_numpy():
