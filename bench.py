@@ -73,7 +73,10 @@ def parse():
                          "one tiled UpdateSlab (a chunk's middles are one contiguous block) or one tensor each")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "hier_fedbuff", "feddyn",
-                             "scaffold"])
+                             "scaffold", "fedavg_eager"])
+    ap.add_argument("--eager-defer", default="on", choices=["on", "off"],
+                    help="fedavg_eager / --e2e-mode eager: FedAvg(defer=True) queues the one-arrival do() "
+                         "calls and reduces them in one launch (on) or launches per arrival (off)")
     ap.add_argument("--fedbuff-fuse", default="on", choices=["on", "off"],
                     help="fedbuff: scale_add straight from the queued arrivals (on) or flush + scale_add (off)")
     ap.add_argument("--feddyn-order", default="sorted", choices=["sorted", "shuffled"],
@@ -428,6 +431,48 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
         }), flush=True)
 
 
+def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
+    """The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) on
+    device-resident updates: base = deepcopy(weights), then one do() per arrival with the
+    running total; the role keeps the returned object (read once, at the round's end).
+    --eager-defer on: FedAvg(defer=True), one launch per round; off: one per arrival."""
+    from flame_amd.optimizers import optimizer_provider
+    if world > 1:
+        raise SystemExit("--workload fedavg_eager is a one-GPU bench")
+    defer = args.eager_defer == "on"
+    opt = optimizer_provider.get("fedavg", defer=defer)
+    keys = [f"{i:05d}" for i in range(n)]
+    state = {"weights": {"model": base}}
+
+    def step():
+        bw = {"model": state["weights"]["model"].clone()}      # deepcopy(self.weights)
+        running, out = 0, None
+        for i, k in enumerate(keys):
+            running += int(counts[i])
+            cache = Cache()
+            cache[k] = TR(client_w[i], int(counts[i]))
+            out = opt.do(bw, cache, total=running, num_trainers=n)
+        state["weights"] = {"model": out["model"]}              # self.weights = global_weights; read
+
+    elapsed, events = timed(world, args.steps, args.warmup, step)
+    ks = kernel_stats(events, "flame_agg_reduce")
+    if rank == 0:
+        k_time = ks["avg_s"] * ks["launches"] / args.steps
+        k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
+        print(json.dumps({
+            "metric": "aggregated params/sec (device-resident), eager FedAvg round",
+            "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32",
+            "config": {"workload": f"fedavg_eager: {n} arrivals (one do() each, running total) x {P} fp32 "
+                                   f"params, {args.layout} layout, defer {args.eager_defer}"},
+            "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": "flame_agg_reduce",
+                         "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
+                         "algorithmic_bytes_per_step": k_bytes,
+                         "bytes_per_client_param": k_bytes / (n * P * 4)},
+        }), flush=True)
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args.force_shard)
@@ -441,7 +486,7 @@ def main():
     if args.workload == "fedbuff":
         return bench_fedbuff(args, world, rank, dev)
 
-    n = args.clients or (512 if args.workload in ("feddyn", "scaffold") else 1024)
+    n = args.clients or {"feddyn": 512, "scaffold": 512, "fedavg_eager": 64}.get(args.workload, 1024)
     P = args.params or 25_000_000
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
@@ -454,6 +499,8 @@ def main():
     counts = synth.counts(args.seed, n)
     if args.workload in ("feddyn", "scaffold"):
         return bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts)
+    if args.workload == "fedavg_eager":
+        return bench_eager(args, world, rank, dev, n, P, client_w, base, counts)
     base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
     total = int(counts.sum())
     keys = [f"{i:05d}" for i in range(n)]
@@ -1021,6 +1068,8 @@ def bench_e2e(args, n, P, dev):
     counts = synth.counts(args.seed, n)
     total = int(counts.sum())
     opt = optimizer_provider.get("fedavg")
+    if mode == "eager" and args.eager_defer == "on":
+        opt = optimizer_provider.get("fedavg", defer=True)
     out_h = torch.empty(P, dtype=torch.float32).pin_memory()
     if mode.startswith("wire"):
         import cloudpickle
@@ -1110,7 +1159,8 @@ def bench_e2e(args, n, P, dev):
             for i in range(n):   # arrival i: receive -> cache (H2D on the side stream) -> do()
                 running += int(counts[i])
                 ecache[f"{i:05d}"] = TR({"model": host[i]}, int(counts[i]))
-                opt.do(base_w, ecache, total=running, num_trainers=n)
+                res = opt.do(base_w, ecache, total=running, num_trainers=n)
+            base = res["model"]       # the role reads the returned object (a deferred round flushes)
         elif mode == "pageable":
             cache = Cache()
             for i in range(n):  # weights_to_model_device (common/util.py:198-208)

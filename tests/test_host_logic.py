@@ -371,3 +371,42 @@ def test_compact_block_size_prediction():
         rates = [[0.5] * n for _ in range(S_)] if seg_rates else [0.5] * n
         p = engine.plan(code, segs, rates, seg_rates=seg_rates, compact=True)
         assert p.meta.nbytes == engine.compact_meta_bytes(code, S_, n, seg_rates), (code, S_, n, seg_rates)
+
+
+# ------------------------------------------------------------------ eager FedAvg deferral
+def test_eager_fedavg_defer_queues_one_launch(golden, monkeypatch):
+    """FedAvg(defer=True) under the eager caller (eager_syncfl/top_aggregator.py:36-90): the
+    arrivals queue with their own count/total and reach the engine as ONE accumulate call on
+    the first read; the oracle as that call's arithmetic reproduces the reference fixture's
+    final state bitwise.  An empty do() flushes first (None, base already written)."""
+    from oracle import oracle as O
+    import scenarios as S
+    from flame_amd.optimizer import fedavg as F
+
+    calls = []
+
+    def accumulate(base, entries, key_groups=None, after_group=None):
+        calls.append(len(entries))
+        for k in base:
+            O.reduce_tensor(base[k], [w[k] for w, _ in entries], [r for _, r in entries])
+
+    monkeypatch.setattr(F.engine, "accumulate", accumulate)
+    fx = golden("fedavg_eager.npz")
+    m = fx.meta
+    opt = F.FedAvg(defer=True)
+    base = {k: v.clone() for k, v in fx.weights("base").items()}
+    cache = S.SortedCache()
+    total, out = 0, None
+    for step, (e, c) in enumerate(zip(m["end_ids"], m["counts"])):
+        total += c
+        cache[e] = S.TR(fx.weights(f"client{step}"), c)
+        out = opt.do(base, cache, total=total, num_trainers=m["n"])
+        assert isinstance(out, F.DeferredWeights) and out.pending == step + 1
+    assert calls == []
+    last = len(m["end_ids"]) - 1
+    S.assert_bitwise("final", dict(out.items()), fx.weights(f"after{last}"))
+    assert calls == [len(m["end_ids"])]
+    assert opt.do(base, S.SortedCache(), total=total) is None and out.pending == 0
+    # the non-deferred default keeps the reference's return (the base dict itself)
+    cache["z"] = S.TR(fx.weights("client0"), 1)
+    assert F.FedAvg().do(base, cache, total=1) is base and calls[-1] == 1
