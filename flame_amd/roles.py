@@ -15,6 +15,11 @@ the read ceiling.  :func:`install_cache` swaps a role's caches for
 so flame's own role code is unchanged.  An unpatched role still works with the
 drop-in optimizers -- its updates are unpickled into one tensor each (row layout,
 16.7 ms instead of 14.8 ms for config 3) after the disk round trip.
+
+The eager top aggregator (``eager_syncfl/top_aggregator.py:36-90``) calls ``do()`` once per
+arrival and reads only the object the last call returns; :func:`patch_eager_role_class`
+(``install_device_cache(eager_batching=True)``) turns on ``FedAvg(defer=True)`` for it, so
+a round's arrivals are reduced in one launch (flame_amd/optimizer/fedavg.py).
 """
 from __future__ import annotations
 
@@ -77,16 +82,60 @@ def patch_role_class(cls, **kwargs):
     return cls
 
 
-def install_device_cache(**kwargs):
+# the eager top aggregator (inherits syncfl TopAggregator.internal_init)
+EAGER_ROLE_CLASS = ("flame.mode.horizontal.eager_syncfl.top_aggregator", "TopAggregator")
+
+
+def enable_eager_batching(role):
+    """Turn on eager batching (``defer=True``) for ``role.optimizer`` when it is the
+    flame_amd FedAvg itself (subclasses -- FedOPT, FedProx, ... -- keep their own ``do``).
+    Returns whether it was enabled."""
+    from .optimizer.fedavg import FedAvg
+    opt = getattr(role, "optimizer", None)
+    if type(opt) is FedAvg:
+        opt.defer = True
+        return True
+    return False
+
+
+def patch_eager_role_class(cls):
+    """Wrap ``cls.internal_init`` -- its own, or the one it inherits, looked up at call time
+    so a cache patch of the parent still runs -- to call :func:`enable_eager_batching` after
+    it (idempotent)."""
+    own = cls.__dict__.get("internal_init")
+    if getattr(own, "_flame_amd_eager", False):
+        return cls
+
+    def internal_init(self, *a, **kw):
+        out = own(self, *a, **kw) if own is not None else super(cls, self).internal_init(*a, **kw)
+        enable_eager_batching(self)
+        return out
+    internal_init._flame_amd_eager = True
+    internal_init.__doc__ = getattr(own, "__doc__", None)
+    cls.internal_init = internal_init
+    return cls
+
+
+def _import_class(mod, name):
+    try:
+        return getattr(importlib.import_module(mod), name)
+    except Exception as e:  # noqa: BLE001  (flame's role layer needs paho, aiostream, ...)
+        logger.info("flame_amd.roles: %s.%s not patched (%s)", mod, name, e)
+        return None
+
+
+def install_device_cache(eager_batching: bool = False, **kwargs):
     """Patch flame's aggregator role classes (ROLE_CLASSES) in place; call once before roles
-    are composed, next to ``flame_amd.optimizers.install()``.  Returns the patched classes;
-    classes whose module does not import here are skipped (logged)."""
+    are composed, next to ``flame_amd.optimizers.install()``.  ``eager_batching``: also
+    patch the eager top aggregator (:func:`patch_eager_role_class`).  Returns the patched
+    classes; classes whose module does not import here are skipped (logged)."""
     done = []
     for mod, name in ROLE_CLASSES:
-        try:
-            cls = getattr(importlib.import_module(mod), name)
-        except Exception as e:  # noqa: BLE001  (flame's role layer needs paho, aiostream, ...)
-            logger.info("flame_amd.roles: %s.%s not patched (%s)", mod, name, e)
-            continue
-        done.append(patch_role_class(cls, **kwargs))
+        cls = _import_class(mod, name)
+        if cls is not None:
+            done.append(patch_role_class(cls, **kwargs))
+    if eager_batching:
+        cls = _import_class(*EAGER_ROLE_CLASS)
+        if cls is not None:
+            done.append(patch_eager_role_class(cls))
     return done

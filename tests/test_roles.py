@@ -81,3 +81,38 @@ def test_install_device_cache_skips_unimportable_roles():
     from flame_amd import roles
     # flame's role layer does not import in this image (paho, aiostream, ... are absent)
     assert isinstance(roles.install_device_cache(placement="host"), list)
+
+
+def test_eager_role_patch_enables_batching_after_cache_patch():
+    """patch_eager_role_class on a class that inherits internal_init: the parent's cache
+    patch (applied before or after) still runs, and the role's flame_amd FedAvg defers;
+    FedAvg subclasses (FedOPT) are left alone."""
+    from flame_amd import roles
+    from flame_amd.ingest import DeviceUpdateCache
+    from flame_amd.optimizer import FedAdam, FedAvg
+    Cache = _disk_cache_cls()
+
+    class Top:                                  # syncfl TopAggregator.internal_init
+        sort = "fedavg"
+
+        def internal_init(self):
+            self.cache = Cache()
+            self.optimizer = FedAvg() if self.sort == "fedavg" else FedAdam()
+
+    class EagerTop(Top):                        # eager_syncfl/top_aggregator.py: no internal_init
+        pass
+
+    roles.patch_eager_role_class(EagerTop)
+    roles.patch_eager_role_class(EagerTop)       # idempotent
+    roles.patch_role_class(Top, placement="host")
+    e = EagerTop()
+    e.internal_init()
+    assert isinstance(e.cache, DeviceUpdateCache) and e.optimizer.defer is True
+    t = Top()
+    t.internal_init()
+    assert t.optimizer.defer is False            # only the eager role
+    EagerTop.sort = "fedadam"
+    e2 = EagerTop()
+    e2.internal_init()
+    assert e2.optimizer.defer is False
+    assert isinstance(roles.install_device_cache(eager_batching=True, placement="host"), list)
