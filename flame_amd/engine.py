@@ -504,11 +504,16 @@ def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
         for s in idx:
             b = bases[s]
             a = _as_device(aggs[s], device)
-            if a.dtype != b.dtype or a.numel() != b.numel():
-                raise NotImplementedError("flame_amd: scale_add needs matching dtype/numel")
+            if a.numel() != b.numel():
+                raise RuntimeError(f"flame_amd: scale_add of {a.numel()} elements into {b.numel()}")
+            if a.dtype != b.dtype:
+                _scale_add_promoted(b, a, goal, deltas[s] if deltas is not None else None, device)
+                continue
             keep.append(a)
             d = deltas[s].data_ptr() if deltas is not None else 0
             segs.append(Seg(b.numel(), out=b.data_ptr(), inp=a.data_ptr(), cur_out=d))
+        if not segs:
+            continue
         p = plan(code, segs, [], chunk=chunk_elems(code, scale_add=True))
         dm = _staging.upload(p.meta, device)
         nbytes = sum(s.numel for s in segs) * ITEMSIZE[code] * (3 + (1 if deltas is not None else 0))
@@ -517,6 +522,23 @@ def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
                                               _stream_ptr(device)))
         keep.append(dm)
     _keepalive(keep, device)
+
+
+def _scale_add_promoted(b: torch.Tensor, a: torch.Tensor, goal: int, delta, device) -> None:
+    """``b += a / goal`` (fedbuff.py:126) when the aggregate's dtype is not the model's:
+    ``q = a / goal`` is true division in a's dtype (int64 / int -> float32, torch's default
+    dtype), formed by the scale_add kernel into a -0.0-filled buffer (x + -0 == x for every
+    x, so the buffer holds exactly ``fl(a / goal)``); then the promoted in-place add
+    (:func:`_add_promoted`); ``delta = new - old`` in b's dtype (common/util.py:152-159)."""
+    af = a.reshape(-1)
+    if not af.is_floating_point():
+        af = af.to(torch.get_default_dtype())
+    q = torch.full(af.shape, -0.0, dtype=af.dtype, device=device)
+    scale_add_([q], [af], goal)
+    old = b.clone() if delta is not None else None
+    _add_promoted(b.view(-1), q)
+    if delta is not None:
+        torch.sub(b.view(-1), old.view(-1), out=delta.view(-1))
 
 
 # ------------------------------------------------------------------ co-located FedBuff hierarchy
@@ -917,26 +939,66 @@ def _accumulate_slab(agg: dict, entries, device, key_groups=None, after_group=No
 def _accumulate_promoted(agg: dict, k, entries, device) -> None:
     """agg[k] += tmp_i where tmp_i = (v_i * rate_i).to(v_i.dtype) has another dtype.
 
-    torch computes ``acc + tmp`` in promote_types(acc, tmp); in place that is only
-    legal when the promotion is acc's own dtype (e.g. an fp32 aggregate receiving
-    int64 ``num_batches_tracked`` after FedOPT promoted it).  Then
-    ``fl(acc + T(tmp))`` == ``fl(acc + fl(T(tmp) * 1.0))``: each tmp_i is formed in
-    its own dtype by the kernel, cast to acc's dtype, and summed in order with rate 1.
+    Each tmp_i is formed in its own dtype by the kernel (fedavg.py:93-102), then added with
+    torch's in-place semantics (:104): the sum in promote_types(acc, tmp), rounded back to
+    acc's dtype -- :func:`_add_promoted`.  Runs of tmps whose promotion is acc's own float
+    dtype (e.g. an fp32 aggregate receiving int64 ``num_batches_tracked``) are summed in one
+    launch: ``fl(acc + T(tmp))`` == ``fl(acc + fl(T(tmp) * 1.0))``.
     """
     acc = agg[k]
     tmps = []
     for w, r in entries:
         v = w[k]
-        if torch.promote_types(acc.dtype, v.dtype) != acc.dtype:
-            raise RuntimeError(f"result type {torch.promote_types(acc.dtype, v.dtype)} can't be cast to the "
-                               f"desired output type {acc.dtype}")
-        t = v if v.dtype == acc.dtype else None
+        _check_cast(acc.dtype, v.dtype)
+        if v.dtype == acc.dtype:
+            tmps.append(v)           # the kernel below forms round(v * r) itself
+            continue
         tmp = torch.empty(acc.shape, dtype=v.dtype, device=device)
         reduce_([tmp], None, [[v]], [r], init_first=True)
-        tmps.append(tmp.to(acc.dtype) if t is None else tmp)
+        tmps.append(tmp)
+    rates = [r if v.dtype == acc.dtype else 1.0 for (v, (_, r)) in zip(tmps, entries)]
     target = _Target(acc, device)
-    reduce_([target.dev], [target.dev], [tmps], [1.0] * len(tmps))
+    run, run_r = [], []
+
+    def flush_run():
+        if run:
+            reduce_([target.dev], [target.dev], [list(run)], list(run_r))
+            run.clear()
+            run_r.clear()
+    for t, r in zip(tmps, rates):
+        p = torch.promote_types(acc.dtype, t.dtype)
+        if t.dtype == acc.dtype or (p == acc.dtype and p.is_floating_point):
+            run.append(t if t.dtype == acc.dtype else t.to(acc.dtype))
+            run_r.append(r)
+        else:
+            flush_run()
+            _add_promoted(target.dev, t)
+    flush_run()
     target.writeback()
+
+
+def _check_cast(acc_dt, v_dt) -> None:
+    p = torch.promote_types(acc_dt, v_dt)
+    if not torch.can_cast(p, acc_dt):
+        raise RuntimeError(f"result type {str(p).replace('torch.', '').capitalize()} can't be cast to the "
+                           f"desired output type {str(acc_dt).replace('torch.', '').capitalize()}")
+
+
+def _add_promoted(acc: torch.Tensor, tmp: torch.Tensor) -> None:
+    """``acc += tmp`` in place with torch's semantics when the dtypes differ: computed in
+    promote_types(acc, tmp) and rounded back to acc's dtype (bf16 += f32, f16 += bf16,
+    f32 += f64, ...: the add runs in the kernel in the promoted dtype with rate 1, the
+    up/down casts are device copies); integer promotions (int32 += int64) are an exact
+    integer add, wrapping like torch's."""
+    p = torch.promote_types(acc.dtype, tmp.dtype)
+    _check_cast(acc.dtype, tmp.dtype)
+    if p.is_floating_point:
+        accp = acc if p == acc.dtype else acc.to(p)
+        reduce_([accp], [accp], [[tmp if tmp.dtype == p else tmp.to(p)]], [1.0])
+        if accp is not acc:
+            acc.copy_(accp)
+    else:
+        acc.copy_(acc.to(p) + tmp.to(p))
 
 
 def logical_shape(weights, k):

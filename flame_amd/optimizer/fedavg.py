@@ -50,7 +50,17 @@ class DeferredWeights(collections.abc.Mapping):
         self._arrival_bytes = sum(v.numel() * v.element_size() for v in base.values()
                                   if isinstance(v, torch.Tensor))
 
+    def _check(self, w):
+        # the reference raises from the do() that brought a bad arrival (fedavg.py:93-104):
+        # unknown keys, and `agg += tmp` whose promoted dtype cannot be cast back to the aggregate's
+        for k in w.keys():
+            if k not in self._base:
+                raise KeyError(k)
+            engine._check_cast(self._base[k].dtype, engine.weight_dtype(w, k))
+
     def _queue(self, entries):
+        for w, _ in entries:
+            self._check(w)
         # a view into a sender's shared-memory segment is copied to HBM before do() returns
         entries = [(_own_shm_views(w), r) for w, r in entries]
         self._pending.extend(entries)

@@ -66,14 +66,19 @@ def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
     assert acc.is_contiguous() and acc.device.type == "cpu"
     if any(c.dtype != acc.dtype for c in clients):
         # fedavg.py:93-104 with v.dtype != agg.dtype: tmp = (v*rate).to(v.dtype), then
-        # agg += tmp in promote_types(agg, tmp) (legal in place only if that is agg's dtype)
+        # `agg += tmp`: torch adds in promote_types(agg, tmp) and rounds back to agg's dtype
+        # (legal in place when that promotion can be cast back: bf16 += f32 is, int += f32 is not)
         for c, r in zip(clients, rates):
             c = _cpu(c)
-            if torch.promote_types(acc.dtype, c.dtype) != acc.dtype:
+            if c.dtype == acc.dtype:
+                reduce_tensor(acc, [c], [r])
+                continue
+            p = torch.promote_types(acc.dtype, c.dtype)
+            if not torch.can_cast(p, acc.dtype):
                 raise RuntimeError("result type can't be cast to the desired output type")
             tmp = torch.empty(acc.shape, dtype=c.dtype)
             reduce_tensor(tmp, [c], [r], init_first=True)
-            reduce_tensor(acc, [tmp.to(acc.dtype)], [1.0])
+            add_promoted(acc, tmp)
         return
     n = len(clients)
     cl = [_cpu(c) for c in clients]
@@ -84,6 +89,20 @@ def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
                               r32.ctypes.data, r64.ctypes.data, n, int(bool(init_first)))
 
 
+def add_promoted(acc: torch.Tensor, tmp: torch.Tensor) -> None:
+    """acc += tmp (CPU, in place) for tmp of another dtype, as torch does it: the sum in
+    promote_types(acc, tmp) -- one correctly rounded add, here the C restatement with rate
+    1 -- then the cast back to acc's dtype; integer promotions are an exact integer add."""
+    p = torch.promote_types(acc.dtype, tmp.dtype)
+    if p.is_floating_point:
+        accp = acc if p == acc.dtype else acc.to(p)
+        reduce_tensor(accp, [tmp.to(p)], [1.0])
+        if accp is not acc:
+            acc.copy_(accp)
+    else:
+        acc.copy_(acc.to(p) + tmp.to(p))
+
+
 def scale_add_tensor(base: torch.Tensor, agg: torch.Tensor, goal: int, want_delta=False):
     assert base.is_contiguous() and base.device.type == "cpu"
     if base.dtype in (torch.int64, torch.int32):
@@ -91,6 +110,15 @@ def scale_add_tensor(base: torch.Tensor, agg: torch.Tensor, goal: int, want_delt
         raise RuntimeError("result type Float can't be cast to the desired output type "
                            + str(base.dtype).replace("torch.", "").capitalize())
     a = _cpu(agg)
+    if a.dtype != base.dtype:
+        # fedbuff.py:126 across dtypes: q = agg / goal in agg's dtype (int -> float32), then
+        # `base += q` promoted; the scale_add restatement on a -0.0 buffer gives fl(agg / goal)
+        af = a if a.is_floating_point() else a.to(torch.float32)
+        q = torch.full(af.shape, -0.0, dtype=af.dtype)
+        scale_add_tensor(q, af, goal)
+        old = base.clone()
+        add_promoted(base, q)
+        return base - old if want_delta else None
     delta = torch.empty_like(base) if want_delta else None
     lib().flame_oracle_scale_add(DT[base.dtype], base.data_ptr(), a.data_ptr(), base.numel(), int(goal),
                                  delta.data_ptr() if delta is not None else None)

@@ -706,7 +706,70 @@ def nonfinite():
     print("wrote nonfinite.npz")
 
 
-CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def downcast_cases():
+    """Updates whose dtype differs from the aggregate's, where torch's in-place add computes
+    in the promoted dtype and rounds back (bf16 += f32, f16 += bf16, f32 += f64, int32 +=
+    int64, ...; fedavg.py:93-104, fedbuff.py:149-157), and FedBuff's scale_add into a model
+    of another dtype (fedbuff.py:122-127)."""
+    gen = torch.Generator().manual_seed(97)
+    rng = np.random.default_rng(97)
+    fw = FixtureWriter()
+    # FedAvg, sync caller: base dtypes vs client dtypes, key by key
+    base_t = {"bf_f32": ((3001,), torch.bfloat16), "h_f32": ((2003,), torch.float16),
+              "f_f64": ((1501,), torch.float32), "h_bf": ((1003,), torch.float16),
+              "bf_h": ((999,), torch.bfloat16), "bf_f64": ((517,), torch.bfloat16),
+              "f_bf": ((77,), torch.float32), "i32_i64": ((11,), torch.int32), "f_i64": ((13,), torch.float32)}
+    cl_t = {"bf_f32": torch.float32, "h_f32": torch.float32, "f_f64": torch.float64, "h_bf": torch.bfloat16,
+            "bf_h": torch.float16, "bf_f64": torch.float64, "f_bf": torch.bfloat16, "i32_i64": torch.int64,
+            "f_i64": torch.int64}
+    n = 7
+    base = small_weights(gen, base_t, 1.0)
+    clients = [small_weights(gen, {k: (s, cl_t[k]) for k, (s, _) in base_t.items()}, 1e-2) for _ in range(n)]
+    for c in clients:
+        c["i32_i64"] = torch.randint(-(1 << 40), 1 << 40, (11,), generator=gen, dtype=torch.int64)
+        c["f_i64"] = torch.randint(-(1 << 30), 1 << 30, (13,), generator=gen, dtype=torch.int64)
+    ids = end_ids(rng, n)
+    counts = [int(x) for x in rng.integers(1, 1001, n)]
+    cache = Cache()
+    for e, w, c in zip(ids, clients, counts):
+        cache[e] = TrainResult(w, c)
+    order = list(cache.iterkeys())
+    out = optimizer_provider.get("fedavg").do(deepcopy(base), cache, total=sum(counts), num_trainers=n)
+    fw.meta.update({"kind": "downcast", "n": n, "end_ids": ids, "counts": counts, "order": order,
+                    "total": sum(counts)})
+    fw.put_weights("fedavg/base", base)
+    for i, w in enumerate(clients):
+        fw.put_weights(f"fedavg/client{i}", w)
+    fw.put_weights("fedavg/out", out)
+    # FedBuff: the first arrival fixes the aggregate's dtypes (None start), later arrivals
+    # bring other dtypes; then scale_add into a model of yet other dtypes
+    first_t = {"a": ((2049,), torch.bfloat16), "b": ((1025,), torch.float32), "c": ((515,), torch.float16),
+               "d": ((300,), torch.float32)}
+    later_t = {"a": torch.float32, "b": torch.float64, "c": torch.bfloat16, "d": torch.bfloat16}
+    model_t = {"a": torch.float32, "b": torch.bfloat16, "c": torch.float16, "d": torch.float16}
+    goal, rnd = 5, 8
+    stale = [0, 1, 3, 2, 0]
+    ups = [small_weights(gen, first_t, 1e-2)]
+    ups += [small_weights(gen, {k: (s, later_t[k]) for k, (s, _) in first_t.items()}, 1e-2) for _ in range(goal - 1)]
+    opt = optimizer_provider.get("fedbuff")
+    agg = None
+    for i, u in enumerate(ups):
+        c = Cache()
+        c[f"t{i}"] = TrainResult(u, 1, rnd - stale[i])
+        agg = opt.do(agg, c, total=1, version=rnd)
+        fw.put_weights(f"fedbuff/agg{i}", deepcopy(agg))
+    weights0 = small_weights(gen, {k: (s, model_t[k]) for k, (s, _) in first_t.items()}, 1.0)
+    new = opt.scale_add_agg_weights(deepcopy(weights0), agg, goal)
+    for i, u in enumerate(ups):
+        fw.put_weights(f"fedbuff/update{i}", u)
+    fw.put_weights("fedbuff/weights0", weights0)
+    fw.put_weights("fedbuff/out", new)
+    fw.meta.update({"goal": goal, "round": rnd, "stale": stale})
+    fw.save(os.path.join(HERE, "downcast.npz"))
+    print("wrote downcast.npz")
+
+
+CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -737,6 +800,7 @@ def main():
     nonfinite()
     fedopt_mixed_more()
     hier_fedbuff_wide()
+    downcast_cases()
 
 
 if __name__ == "__main__":

@@ -212,6 +212,33 @@ def run_fedbuff_dtypes(fx, make_opt, device):
     return res
 
 
+def run_downcast(fx, make_opt, device):
+    """Updates of another dtype than the aggregate (torch adds in the promoted dtype and rounds
+    back): FedAvg; FedBuff read after every arrival and read once at the end (all queued),
+    each followed by a scale_add into a model of other dtypes."""
+    m = fx.meta
+    base = to_dev(fx.weights("fedavg/base"), device)
+    cache = SortedCache()
+    for i, (e, c) in enumerate(zip(m["end_ids"], m["counts"])):
+        cache[e] = TR(to_dev(fx.weights(f"fedavg/client{i}"), device), c)
+    assert list(cache.iterkeys()) == m["order"]
+    out = make_opt("fedavg").do(base, cache, total=m["total"], num_trainers=m["n"])
+    res = [("fedavg", out, fx.weights("fedavg/out"))]
+    for read_each in (True, False):
+        opt = make_opt("fedbuff")
+        agg = None
+        for i in range(m["goal"]):
+            c = SortedCache()
+            c[f"t{i}"] = TR(to_dev(fx.weights(f"fedbuff/update{i}"), device), 1, m["round"] - m["stale"][i])
+            agg = opt.do(agg, c, total=1, version=m["round"])
+            if read_each:
+                res.append((f"fedbuff/agg{i}", to_cpu(agg), fx.weights(f"fedbuff/agg{i}")))
+        w = to_dev(fx.weights("fedbuff/weights0"), device)
+        new = opt.scale_add_agg_weights(w, agg, m["goal"])
+        res.append(("fedbuff/out" + ("" if read_each else " (deferred)"), new, fx.weights("fedbuff/out")))
+    return res
+
+
 def run_fedbuff_none_multi(fx, make_opt, device):
     m = fx.meta
     cache = SortedCache()
@@ -471,6 +498,7 @@ BITWISE_FIXTURES = [
     ("fedavg_subsets.npz", run_fedavg),
     ("fedbuff_subsets.npz", run_fedbuff_subsets),
     ("fedbuff_dtypes.npz", run_fedbuff_dtypes),
+    ("downcast.npz", run_downcast),
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),

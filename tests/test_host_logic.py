@@ -410,3 +410,25 @@ def test_eager_fedavg_defer_queues_one_launch(golden, monkeypatch):
     # the non-deferred default keeps the reference's return (the base dict itself)
     cache["z"] = S.TR(fx.weights("client0"), 1)
     assert F.FedAvg().do(base, cache, total=1) is base and calls[-1] == 1
+
+
+def test_eager_fedavg_defer_raises_at_the_bad_arrival(monkeypatch):
+    """A queued arrival with an unknown key or an illegal in-place promotion raises from the
+    do() that brings it, as the reference's per-arrival add would (fedavg.py:93-104)."""
+    import pytest
+    import scenarios as S
+    from flame_amd.optimizer import fedavg as F
+    monkeypatch.setattr(F.engine, "accumulate", lambda *a, **k: None)
+    opt = F.FedAvg(defer=True)
+    base = {"w": torch.zeros(4, dtype=torch.bfloat16), "n": torch.tensor(1)}
+    c = S.SortedCache()
+    c["a"] = S.TR({"w": torch.ones(4, dtype=torch.bfloat16), "n": torch.tensor(2)}, 1)
+    out = opt.do(base, c, total=1)
+    c["b"] = S.TR({"w": torch.ones(4), "n": torch.tensor(1.5)}, 1)   # int64 += f32: raises
+    with pytest.raises(RuntimeError, match="can't be cast"):
+        opt.do(base, c, total=2)
+    c = S.SortedCache()
+    c["c"] = S.TR({"zz": torch.ones(4)}, 1)
+    with pytest.raises(KeyError):
+        opt.do(base, c, total=3)
+    assert out.pending == 1
