@@ -29,6 +29,9 @@ DTYPE_CODE = {
     torch.float64: N.FLAME_F64, torch.int64: N.FLAME_I64, torch.int32: N.FLAME_I32,
 }
 FLOAT_CODES = (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16, N.FLAME_F64)
+# state_dict dtypes the kernels do not carry (bool masks, uint8 / int8 / int16 buffers): their
+# tmp is formed in fp32 by the kernel and cast, their adds are torch's (see tmp_of)
+NARROW = (torch.bool, torch.uint8, torch.int8, torch.int16)
 VEC_BYTES = 16
 ITEMSIZE = {N.FLAME_F32: 4, N.FLAME_BF16: 2, N.FLAME_F16: 2, N.FLAME_F64: 8, N.FLAME_I64: 8, N.FLAME_I32: 4}
 
@@ -492,7 +495,7 @@ def scale_add_(bases: List[torch.Tensor], aggs: List[torch.Tensor], goal: int,
     L = N.lib()
     groups = collections.OrderedDict()
     for s, b in enumerate(bases):
-        code = dtype_code(b.dtype)
+        code = dtype_code(b.dtype) if b.is_floating_point() else None
         if code not in FLOAT_CODES:
             # torch: int_tensor / int -> float; in-place add into an int tensor raises
             raise RuntimeError(f"result type Float can't be cast to the desired output type "
@@ -825,7 +828,8 @@ def accumulate(agg: dict, entries, *, device=None, key_groups=None, after_group=
         if k in per_key:
             groups.setdefault(tuple(per_key[k]), []).append(k)
     for cis, ks in groups.items():
-        same = [k for k in ks if all(entries[ci][0][k].dtype == agg[k].dtype for ci in cis)]
+        same = [k for k in ks if agg[k].dtype in DTYPE_CODE
+                and all(entries[ci][0][k].dtype == agg[k].dtype for ci in cis)]
         mixed = [k for k in ks if k not in same]
         if same:
             targets = [_Target(agg[k], device) for k in same]
@@ -937,26 +941,28 @@ def _accumulate_slab(agg: dict, entries, device, key_groups=None, after_group=No
 
 
 def _accumulate_promoted(agg: dict, k, entries, device) -> None:
-    """agg[k] += tmp_i where tmp_i = (v_i * rate_i).to(v_i.dtype) has another dtype.
+    """agg[k] += tmp_i where tmp_i = (v_i * rate_i).to(v_i.dtype) has another dtype than
+    agg[k], or either is a dtype the kernels do not carry (:data:`NARROW`).
 
-    Each tmp_i is formed in its own dtype by the kernel (fedavg.py:93-102), then added with
-    torch's in-place semantics (:104): the sum in promote_types(acc, tmp), rounded back to
-    acc's dtype -- :func:`_add_promoted`.  Runs of tmps whose promotion is acc's own float
-    dtype (e.g. an fp32 aggregate receiving int64 ``num_batches_tracked``) are summed in one
-    launch: ``fl(acc + T(tmp))`` == ``fl(acc + fl(T(tmp) * 1.0))``.
+    Each tmp_i is formed in its own dtype (fedavg.py:93-102, :func:`tmp_of`), then added
+    with torch's in-place semantics (:104): the sum in promote_types(acc, tmp), rounded back
+    to acc's dtype -- :func:`_add_promoted` (integer aggregates: exact integer adds).  Runs
+    of tmps whose promotion is acc's own float dtype (e.g. an fp32 aggregate receiving int64
+    ``num_batches_tracked``) are summed in one launch: ``fl(acc + T(tmp))`` ==
+    ``fl(acc + fl(T(tmp) * 1.0))``.
     """
     acc = agg[k]
-    tmps = []
+    direct = acc.dtype in DTYPE_CODE
+    terms = []                   # (tensor, rate, summable by the kernel into acc)
     for w, r in entries:
         v = w[k]
         _check_cast(acc.dtype, v.dtype)
-        if v.dtype == acc.dtype:
-            tmps.append(v)           # the kernel below forms round(v * r) itself
-            continue
-        tmp = torch.empty(acc.shape, dtype=v.dtype, device=device)
-        reduce_([tmp], None, [[v]], [r], init_first=True)
-        tmps.append(tmp)
-    rates = [r if v.dtype == acc.dtype else 1.0 for (v, (_, r)) in zip(tmps, entries)]
+        tmp = tmp_of(v, r, device, acc.shape)
+        p = torch.promote_types(acc.dtype, tmp.dtype)
+        if direct and p == acc.dtype and p.is_floating_point:    # integers: exact adds below
+            terms.append((tmp if tmp.dtype == acc.dtype else tmp.to(acc.dtype), 1.0, True))
+        else:
+            terms.append((tmp, None, False))
     target = _Target(acc, device)
     run, run_r = [], []
 
@@ -965,16 +971,35 @@ def _accumulate_promoted(agg: dict, k, entries, device) -> None:
             reduce_([target.dev], [target.dev], [list(run)], list(run_r))
             run.clear()
             run_r.clear()
-    for t, r in zip(tmps, rates):
-        p = torch.promote_types(acc.dtype, t.dtype)
-        if t.dtype == acc.dtype or (p == acc.dtype and p.is_floating_point):
-            run.append(t if t.dtype == acc.dtype else t.to(acc.dtype))
+    for t, r, summable in terms:
+        if summable:
+            run.append(t)
             run_r.append(r)
         else:
             flush_run()
             _add_promoted(target.dev, t)
     flush_run()
     target.writeback()
+
+
+def tmp_of(v: torch.Tensor, rate: float, device, shape=None) -> torch.Tensor:
+    """``(v * rate).to(v.dtype)`` (fedavg.py:93-102) as a new device tensor.  Kernel dtypes:
+    one init-first launch.  bool / uint8 / int8 / int16: ``v * rate`` is fp32 in torch
+    (the integral tensor and the rate both cast to fp32), formed by the fp32 kernel, then
+    cast to v's dtype on the device (bool: != 0; integers: truncation -- in range, as
+    ``|v * rate| <= |v|`` for the callers' rates <= 1).  ``shape``: the key's model shape
+    (``v`` may be a tiled slab view)."""
+    shape = v.shape if shape is None else shape
+    if v.dtype in DTYPE_CODE:
+        tmp = torch.empty(shape, dtype=v.dtype, device=device)
+        reduce_([tmp], None, [[v]], [rate], init_first=True)
+        return tmp
+    if v.dtype not in NARROW:
+        dtype_code(v.dtype)          # raises: unsupported (complex, fp8, ...)
+    vf = v.to(device).to(torch.float32)
+    tf = torch.empty(shape, dtype=torch.float32, device=device)
+    reduce_([tf], None, [[vf]], [rate], init_first=True)
+    return tf.to(v.dtype)
 
 
 def _check_cast(acc_dt, v_dt) -> None:
@@ -1026,8 +1051,12 @@ def first_tmp(weights: dict, rate: float, *, device=None) -> dict:
     device = device or pick_device(weights)
     out = collections.OrderedDict()
     ks = list(weights.keys())
+    kern = [k for k in ks if weight_dtype(weights, k) in DTYPE_CODE]
     for k in ks:
-        v = weights[k]
-        out[k] = torch.empty(logical_shape(weights, k), dtype=v.dtype, device=device)
-    reduce_([out[k] for k in ks], None, [[weights[k]] for k in ks], [rate], init_first=True)
+        if k in kern:
+            out[k] = torch.empty(logical_shape(weights, k), dtype=weight_dtype(weights, k), device=device)
+        else:
+            out[k] = tmp_of(weights[k], rate, device, logical_shape(weights, k))
+    if kern:
+        reduce_([out[k] for k in kern], None, [[weights[k]] for k in kern], [rate], init_first=True)
     return out

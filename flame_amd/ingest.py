@@ -567,6 +567,9 @@ class DeviceUpdateCache:
         return self._stream
 
     def _fits_slab(self, w):
+        from . import engine
+        if any(isinstance(v, torch.Tensor) and v.dtype not in engine.DTYPE_CODE for v in w.values()):
+            return False       # bool / uint8 / int8 / int16 buffers: one allocation per tensor
         if self.slab is None:
             from .slab import UpdateSlab
             self.slab = UpdateSlab(self.shard.local_template() if self.shard is not None else w, self.capacity,

@@ -256,8 +256,9 @@ def _fused_scale_add(base_weights, agg, agg_goal, delta, key_groups=None, after_
 
 # ---------------------------------------------------------------- co-located middle aggregators
 def _uniform(agg: DeferredAggregate) -> bool:
-    """Every queued arrival carries every key in the aggregate's dtype (the one-launch case)."""
-    return all(k in w and engine.weight_dtype(w, k) == agg._meta[k][1]
+    """Every queued arrival carries every key in the aggregate's dtype, a dtype the kernels
+    carry (the one-launch case)."""
+    return all(agg._meta[k][1] in engine.DTYPE_CODE for k in agg._keys) and all(k in w and engine.weight_dtype(w, k) == agg._meta[k][1]
                for w in engine.representatives([w for w, _ in agg._pending]) for k in agg._keys)
 
 

@@ -64,21 +64,20 @@ def _cpu(t):
 def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
     """acc (CPU, contiguous) += Σ_i round(v_i * rate_i), sequential in list order (in place)."""
     assert acc.is_contiguous() and acc.device.type == "cpu"
-    if any(c.dtype != acc.dtype for c in clients):
+    if any(c.dtype != acc.dtype for c in clients) or acc.dtype in NARROW:
+        assert not init_first, "init_first needs the aggregate's own kernel dtype (use tmp_tensor)"
         # fedavg.py:93-104 with v.dtype != agg.dtype: tmp = (v*rate).to(v.dtype), then
         # `agg += tmp`: torch adds in promote_types(agg, tmp) and rounds back to agg's dtype
         # (legal in place when that promotion can be cast back: bf16 += f32 is, int += f32 is not)
         for c, r in zip(clients, rates):
             c = _cpu(c)
-            if c.dtype == acc.dtype:
+            if c.dtype == acc.dtype and acc.dtype not in NARROW:
                 reduce_tensor(acc, [c], [r])
                 continue
             p = torch.promote_types(acc.dtype, c.dtype)
             if not torch.can_cast(p, acc.dtype):
                 raise RuntimeError("result type can't be cast to the desired output type")
-            tmp = torch.empty(acc.shape, dtype=c.dtype)
-            reduce_tensor(tmp, [c], [r], init_first=True)
-            add_promoted(acc, tmp)
+            add_promoted(acc, tmp_tensor(c, r))
         return
     n = len(clients)
     cl = [_cpu(c) for c in clients]
@@ -87,6 +86,23 @@ def reduce_tensor(acc: torch.Tensor, clients, rates, init_first=False) -> None:
     r64 = np.asarray([float(r) for r in rates] or [0], dtype=np.float64)
     lib().flame_oracle_reduce(DT[acc.dtype], acc.data_ptr(), acc.numel(), ptrs,
                               r32.ctypes.data, r64.ctypes.data, n, int(bool(init_first)))
+
+
+NARROW = (torch.bool, torch.uint8, torch.int8, torch.int16)
+
+
+def tmp_tensor(v: torch.Tensor, rate) -> torch.Tensor:
+    """``(v * rate).to(v.dtype)`` on the CPU (fedavg.py:93-102, fedbuff.py:143-153).  bool /
+    uint8 / int8 / int16: ``v * rate`` is fp32 (both operands cast to fp32), then the cast
+    back: bool = (x != 0), integers truncate."""
+    v = _cpu(v)
+    if v.dtype in NARROW:
+        tf = torch.empty(v.shape, dtype=torch.float32)
+        reduce_tensor(tf, [v.to(torch.float32)], [rate], init_first=True)
+        return tf.to(v.dtype)
+    tmp = torch.empty(v.shape, dtype=v.dtype)
+    reduce_tensor(tmp, [v], [rate], init_first=True)
+    return tmp
 
 
 def add_promoted(acc: torch.Tensor, tmp: torch.Tensor) -> None:
@@ -105,7 +121,7 @@ def add_promoted(acc: torch.Tensor, tmp: torch.Tensor) -> None:
 
 def scale_add_tensor(base: torch.Tensor, agg: torch.Tensor, goal: int, want_delta=False):
     assert base.is_contiguous() and base.device.type == "cpu"
-    if base.dtype in (torch.int64, torch.int32):
+    if not base.is_floating_point():
         # torch: int_tensor / int -> float32; `base += float` on an int tensor raises
         raise RuntimeError("result type Float can't be cast to the desired output type "
                            + str(base.dtype).replace("torch.", "").capitalize())
@@ -267,9 +283,7 @@ class OracleFedBuff:
                 self.agg_goal_weights = {}
             for key, v in tres.weights.items():
                 if none_start:
-                    acc = torch.empty_like(_cpu(v))
-                    reduce_tensor(acc, [v], [rate], init_first=True)
-                    self.agg_goal_weights[key] = acc
+                    self.agg_goal_weights[key] = tmp_tensor(v, rate)
                 else:
                     reduce_tensor(self.agg_goal_weights[key], [v], [rate])
         return self.agg_goal_weights

@@ -17,7 +17,7 @@ except Exception:  # pragma: no cover
 
 _TORCH_NAME = {
     "float32": "f32", "bfloat16": "bf16", "float16": "f16", "float64": "f64",
-    "int64": "i64", "int32": "i32", "int16": "i16", "int8": "i8", "uint8": "u8",
+    "int64": "i64", "int32": "i32", "int16": "i16", "int8": "i8", "uint8": "u8", "bool": "b1",
 }
 
 
@@ -83,7 +83,7 @@ class Fixture:
     def get(self, name):
         tag = self.meta["dtypes"][name]
         a = self.arrays[name]
-        if torch is not None and tag in ("f32", "bf16", "f16", "f64", "i64", "i32", "i16", "i8", "u8"):
+        if torch is not None and tag in ("f32", "bf16", "f16", "f64", "i64", "i32", "i16", "i8", "u8", "b1"):
             return np_to_tensor(a, tag)
         return a
 

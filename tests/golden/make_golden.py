@@ -769,7 +769,73 @@ def downcast_cases():
     print("wrote downcast.npz")
 
 
-CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def narrow_cases():
+    """state_dict buffers of dtypes the kernels do not carry -- bool masks, uint8 / int8 /
+    int16 -- next to float keys: FedAvg ((v * rate).to(v.dtype) in fp32, then bool `+=` is a
+    logical or and the integers wrap, fedavg.py:93-104) and FedBuff (None start, then `+=`)
+    with a scale_add over the float keys only (an integral base raises, fedbuff.py:126)."""
+    gen = torch.Generator().manual_seed(131)
+    rng = np.random.default_rng(131)
+    fw = FixtureWriter()
+    shapes = {"w": (4099,), "mask": (300,), "u8": (257,), "i8": (129,), "i16": (65,), "h": (1000,)}
+    dts = {"w": torch.float32, "mask": torch.bool, "u8": torch.uint8, "i8": torch.int8, "i16": torch.int16,
+           "h": torch.bfloat16}
+
+    def one(scale, lo, hi):
+        out = {}
+        for k, shp in shapes.items():
+            dt = dts[k]
+            if dt == torch.bool:
+                out[k] = torch.rand(shp, generator=gen) < 0.3
+            elif dt.is_floating_point:
+                out[k] = (torch.randn(shp, generator=gen, dtype=torch.float64) * scale).to(dt)
+            else:
+                out[k] = torch.randint(lo, hi, shp, generator=gen).to(dt)
+        return out
+    n = 6
+    base = one(1.0, 0, 100)
+    clients = [one(1e-2, 0, 127) for _ in range(n)]
+    ids = end_ids(rng, n)
+    counts = [int(x) for x in rng.integers(1, 1001, n)]
+    cache = Cache()
+    for e, w, c in zip(ids, clients, counts):
+        cache[e] = TrainResult(w, c)
+    order = list(cache.iterkeys())
+    out = optimizer_provider.get("fedavg").do(deepcopy(base), cache, total=sum(counts), num_trainers=n)
+    fw.meta.update({"kind": "narrow", "n": n, "end_ids": ids, "counts": counts, "order": order,
+                    "total": sum(counts)})
+    fw.put_weights("fedavg/base", base)
+    for i, w in enumerate(clients):
+        fw.put_weights(f"fedavg/client{i}", w)
+    fw.put_weights("fedavg/out", out)
+    goal, rnd = 4, 6
+    stale = [0, 2, 1, 3]
+    ups = [one(1e-2, 0, 127) for _ in range(goal)]
+    opt = optimizer_provider.get("fedbuff")
+    agg = None
+    for i, u in enumerate(ups):
+        c = Cache()
+        c[f"t{i}"] = TrainResult(u, 1, rnd - stale[i])
+        agg = opt.do(agg, c, total=1, version=rnd)
+        fw.put_weights(f"fedbuff/agg{i}", deepcopy(agg))
+    fkeys = [k for k in shapes if dts[k].is_floating_point]
+    weights0 = {k: (torch.randn(shapes[k], generator=gen, dtype=torch.float64)).to(dts[k]) for k in fkeys}
+    new = opt.scale_add_agg_weights(deepcopy(weights0), agg, goal)
+    try:
+        opt.scale_add_agg_weights({"mask": base["mask"].clone()}, agg, goal)
+        raises = False
+    except RuntimeError:
+        raises = True
+    for i, u in enumerate(ups):
+        fw.put_weights(f"fedbuff/update{i}", u)
+    fw.put_weights("fedbuff/weights0", weights0)
+    fw.put_weights("fedbuff/out", new)
+    fw.meta.update({"goal": goal, "round": rnd, "stale": stale, "scale_add_bool_raises": raises})
+    fw.save(os.path.join(HERE, "narrow.npz"))
+    print("wrote narrow.npz")
+
+
+CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "narrow_cases": narrow_cases, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -801,6 +867,7 @@ def main():
     fedopt_mixed_more()
     hier_fedbuff_wide()
     downcast_cases()
+    narrow_cases()
 
 
 if __name__ == "__main__":

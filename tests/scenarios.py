@@ -239,6 +239,26 @@ def run_downcast(fx, make_opt, device):
     return res
 
 
+def run_narrow(fx, make_opt, device):
+    """bool / uint8 / int8 / int16 buffers next to float keys: the downcast driver's FedAvg and
+    FedBuff passes; a scale_add into a bool model raises as in the reference."""
+    res = run_downcast(fx, make_opt, device)
+    opt = make_opt("fedbuff")
+    m = fx.meta
+    agg = None
+    for i in range(m["goal"]):
+        c = SortedCache()
+        c[f"t{i}"] = TR(to_dev(fx.weights(f"fedbuff/update{i}"), device), 1, m["round"] - m["stale"][i])
+        agg = opt.do(agg, c, total=1, version=m["round"])
+    try:
+        opt.scale_add_agg_weights({"mask": to_dev(fx.weights("fedavg/base"), device)["mask"]}, agg, m["goal"])
+        raised = False
+    except RuntimeError:
+        raised = True
+    assert raised == m["scale_add_bool_raises"]
+    return res
+
+
 def run_fedbuff_none_multi(fx, make_opt, device):
     m = fx.meta
     cache = SortedCache()
@@ -499,6 +519,7 @@ BITWISE_FIXTURES = [
     ("fedbuff_subsets.npz", run_fedbuff_subsets),
     ("fedbuff_dtypes.npz", run_fedbuff_dtypes),
     ("downcast.npz", run_downcast),
+    ("narrow.npz", run_narrow),
     ("feddyn_rounds.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
