@@ -1,0 +1,82 @@
+"""GPU: the FedAvg / FedBuff drop-ins against torch CPU itself (the reference's arithmetic,
+fedavg.py:93-104, fedbuff.py:122-157) for every pair of (aggregate dtype, update dtype) a
+state_dict can carry -- bitwise, errors included -- with several arrivals per key (the
+kernel's in-order sum) and a FedBuff scale_add into a model of each float dtype."""
+import math
+
+import pytest
+import torch
+
+import scenarios as S
+from test_oracle_dtype_matrix import DTYPES, _rand, _reference
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native_loaded():
+    from flame_amd import _native
+    _native.lib()
+    assert torch.cuda.is_available()
+
+
+def _drop_in(sort):
+    from flame_amd.optimizers import optimizer_provider
+    return optimizer_provider.get(sort)
+
+
+@pytest.mark.parametrize("acc_dt", DTYPES, ids=[str(d)[6:] for d in DTYPES])
+def test_fedavg_every_dtype_pair_vs_torch(acc_dt):
+    g = torch.Generator().manual_seed(7 + DTYPES.index(acc_dt))
+    for v_dt in DTYPES:
+        acc = _rand(g, acc_dt, 4099, 1.0)
+        vs = [_rand(g, v_dt, 4099, 1e-1) for _ in range(3)]
+        counts = [5, 11, 17]
+        exp = acc.clone()
+        try:
+            for v, c in zip(vs, counts):
+                _reference(exp, v, c / sum(counts))
+            err = None
+        except RuntimeError as e:
+            err = e
+        cache = S.SortedCache()
+        for i, (v, c) in enumerate(zip(vs, counts)):
+            cache[f"e{i}"] = S.TR({"k": v.to(DEV)}, c)
+        base = {"k": acc.to(DEV)}
+        if err is not None:
+            with pytest.raises(RuntimeError):
+                _drop_in("fedavg").do(base, cache, total=sum(counts))
+            continue
+        out = _drop_in("fedavg").do(base, cache, total=sum(counts))
+        S.assert_bitwise(f"{acc_dt}+={v_dt}", {"k": out["k"]}, {"k": exp})
+
+
+@pytest.mark.parametrize("agg_dt", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64,
+                                    torch.uint8])
+def test_fedbuff_scale_add_every_model_dtype_vs_torch(agg_dt):
+    """FedBuff None start in agg_dt, then scale_add into a model of every float dtype
+    (``base += agg / goal``: the quotient in agg's dtype -- float32 for integers -- then
+    the promoted add)."""
+    g = torch.Generator().manual_seed(40 + int(agg_dt.itemsize))
+    ups = [_rand(g, agg_dt, 2051, 1e-1) for _ in range(3)]
+    for model_dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+        ref_agg = None
+        for i, u in enumerate(ups):
+            tmp = u * (1 / math.sqrt(1 + 10 - (10 - i)))      # fedbuff.py:96
+            tmp = tmp.to(u.dtype) if tmp.dtype != u.dtype else tmp
+            if ref_agg is None:
+                ref_agg = tmp
+            else:
+                ref_agg += tmp
+        w0 = _rand(g, model_dt, 2051, 1.0)
+        exp = w0.clone()
+        exp += ref_agg / 3
+        opt, agg = _drop_in("fedbuff"), None
+        for i, u in enumerate(ups):
+            c = S.SortedCache()
+            c["t"] = S.TR({"k": u.to(DEV)}, 1, 10 - i)
+            agg = opt.do(agg, c, total=1, version=10)
+        new = opt.scale_add_agg_weights({"k": w0.to(DEV)}, agg, 3)
+        S.assert_bitwise(f"{model_dt}+={agg_dt}/3", {"k": new["k"]}, {"k": exp})
