@@ -176,6 +176,7 @@ class ShardPlan:
         * a slot of a slab that already holds only this rank's slices: unchanged;
         * a slot of a full-model slab: a :class:`~flame_amd.slab.SlabRef` (no views made;
           the engine computes pointer rows from slot numbers);
+        * a dict already keyed by this plan's local names: unchanged;
         * a dict of tensors (device, pinned or pageable host): views / slices.
         """
         slab = getattr(weights, "slab", None)
@@ -190,6 +191,9 @@ class ShardPlan:
                    and s.lo % slab.storage[self.dtypes[s.key]].shape[2] == 0 for s in self.subs):
                 from .slab import SlabRef
                 return SlabRef(slab, weights.slot, self.full_ranges, self.local_shapes, owner=weights)
+        if slab is None and weights and all(k in self.by_name and k not in self.numel for k in weights.keys()):
+            return weights     # already this rank's slices, one tensor per range (DeviceUpdateCache(shard=plan)
+                               # keeps a model it cannot slab -- bool / uint8 buffers -- that way)
         return self.slice_update(weights)
 
     def restrict(self, weights, wave: int):

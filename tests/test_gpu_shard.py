@@ -69,8 +69,13 @@ def _model(g, P):
 
 
 def _update(g, tmpl, i, scale=1e-2):
-    return {k: (torch.randn(v.shape, generator=g) * scale).to(v.dtype) if v.is_floating_point()
-            else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
+    def one(v):
+        if v.is_floating_point():
+            return (torch.randn(v.shape, generator=g) * scale).to(v.dtype)
+        if v.dim() == 0:
+            return torch.tensor(i, dtype=v.dtype)
+        return torch.randint(0, 2 if v.dtype == torch.bool else 120, v.shape, generator=g).to(v.dtype)
+    return {k: one(v) for k, v in tmpl.items()}
 
 
 # ---------------------------------------------------------------- single process
@@ -111,7 +116,11 @@ def test_slabref_rows_equal_full_reduce():
 
 
 # ---------------------------------------------------------------- FedAvg waves, two ranks
-def _fedavg_worker(rank, world, port, q):
+def _fedavg_narrow_worker(rank, world, port, q):
+    _fedavg_worker(rank, world, port, q, narrow=True)
+
+
+def _fedavg_worker(rank, world, port, q, narrow=False):
     dist = _init(rank, world, port)
     try:
         from flame_amd import engine, shard
@@ -119,6 +128,9 @@ def _fedavg_worker(rank, world, port, q):
         from flame_amd.optimizers import optimizer_provider
         g = torch.Generator().manual_seed(51)
         tmpl = _model(g, 300_007)
+        if narrow:   # a bool mask and a uint8 buffer, split across the ranks like any key
+            tmpl["mask"] = torch.rand(40_961, generator=g) < 0.3
+            tmpl["u8"] = torch.randint(0, 120, (8195,), generator=g).to(torch.uint8)
         opt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=torch.device(DEV))
         opt.set_layout(tmpl)
         cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=16, shard=opt.plan)
@@ -155,6 +167,12 @@ def test_sharded_fedavg_waves_two_ranks_one_gpu():
     """ShardedOptimizer(FedAvg) with rank-local slab caches: three waves, in-place gathers,
     bitwise == one process over 3 rounds (f32 / bf16 / f16 / f64 / int64 keys)."""
     _two_ranks(_fedavg_worker)
+
+
+def test_sharded_fedavg_narrow_dtypes_two_ranks_one_gpu():
+    """The same with a bool mask and a uint8 buffer in the model (their ranges stay one
+    allocation per tensor in the rank's cache; torch's or / wrapping adds): == one process."""
+    _two_ranks(_fedavg_narrow_worker)
 
 
 # ---------------------------------------------------------------- config 5, two ranks

@@ -53,8 +53,13 @@ def _eq(a, b):
 
 
 def _model(g, shapes, scale):
-    return {k: (torch.randn(s, generator=g) * scale).to(dt) if dt.is_floating_point else torch.tensor(5, dtype=dt)
-            for k, (s, dt) in shapes.items()}
+    def one(s, dt):
+        if dt.is_floating_point:
+            return (torch.randn(s, generator=g) * scale).to(dt)
+        if s == ():
+            return torch.tensor(5, dtype=dt)
+        return torch.randint(0, 2 if dt == torch.bool else 120, s, generator=g).to(dt)
+    return {k: one(s, dt) for k, (s, dt) in shapes.items()}
 
 
 # ---------------------------------------------------------------- the plan (no process group)
@@ -128,6 +133,8 @@ def test_shard_plan_slices_and_restrict():
 # ---------------------------------------------------------------- FedAvg (waves) / FedOPT / FedBuff
 SHAPES = {"a": ((600, 37), torch.float32), "bf": ((5001,), torch.bfloat16), "b": ((37,), torch.float32),
           "nbt": ((), torch.int64), "h": ((3001,), torch.float16)}
+# FedAvg also carries a bool mask and a uint8 buffer (split across ranks like any key)
+FEDAVG_SHAPES = {**SHAPES, "mask": ((4099,), torch.bool), "u8": ((2500,), torch.uint8)}
 
 
 def _fedavg_worker(rank, world, port, q):
@@ -136,12 +143,12 @@ def _fedavg_worker(rank, world, port, q):
         from oracle import oracle as O
         import scenarios as S
         g = torch.Generator().manual_seed(7)
-        base = _model(g, SHAPES, 1.0)
+        base = _model(g, FEDAVG_SHAPES, 1.0)
         ok = True
         opt = shard.ShardedOptimizer(O.OracleFedAvg(), device=torch.device("cpu"), align=8, waves=True)
         for r in range(2):
             n = 11
-            clients = [_model(g, SHAPES, 1e-2) for _ in range(n)]
+            clients = [_model(g, FEDAVG_SHAPES, 1e-2) for _ in range(n)]
             for i, c in enumerate(clients):
                 c["nbt"] = torch.tensor(r + i)
             counts = torch.randint(1, 1000, (n,), generator=g).tolist()
