@@ -120,7 +120,11 @@ def _fedavg_narrow_worker(rank, world, port, q):
     _fedavg_worker(rank, world, port, q, narrow=True)
 
 
-def _fedavg_worker(rank, world, port, q, narrow=False):
+def _fedavg_overflow_worker(rank, world, port, q):
+    _fedavg_worker(rank, world, port, q, capacity=4)
+
+
+def _fedavg_worker(rank, world, port, q, narrow=False, capacity=16):
     dist = _init(rank, world, port)
     try:
         from flame_amd import engine, shard
@@ -133,7 +137,7 @@ def _fedavg_worker(rank, world, port, q, narrow=False):
             tmpl["u8"] = torch.randint(0, 120, (8195,), generator=g).to(torch.uint8)
         opt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=torch.device(DEV))
         opt.set_layout(tmpl)
-        cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=16, shard=opt.plan)
+        cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=capacity, shard=opt.plan)
         single = optimizer_provider.get("fedavg")
         ws = {k: v.to(DEV) for k, v in tmpl.items()}
         wr = {k: v.clone() for k, v in ws.items()}
@@ -167,6 +171,12 @@ def test_sharded_fedavg_waves_two_ranks_one_gpu():
     """ShardedOptimizer(FedAvg) with rank-local slab caches: three waves, in-place gathers,
     bitwise == one process over 3 rounds (f32 / bf16 / f16 / f64 / int64 keys)."""
     _two_ranks(_fedavg_worker)
+
+
+def test_sharded_fedavg_slab_overflow_two_ranks_one_gpu():
+    """7 updates per round into a rank-local slab of 4 slots: the overflow stays one tensor
+    per owned range (HBM) and the round mixes both layouts: == one process, bitwise."""
+    _two_ranks(_fedavg_overflow_worker)
 
 
 def test_sharded_fedavg_narrow_dtypes_two_ranks_one_gpu():
