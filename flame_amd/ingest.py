@@ -569,11 +569,15 @@ class DeviceUpdateCache:
     def _fits_slab(self, w):
         from . import engine
         if any(isinstance(v, torch.Tensor) and v.dtype not in engine.DTYPE_CODE for v in w.values()):
-            return False       # bool / uint8 / int8 / int16 buffers: one allocation per tensor
+            return False       # bool / uint8 / int8 / int16 buffers: see _put_mixed
         if self.slab is None:
             from .slab import UpdateSlab
-            self.slab = UpdateSlab(self.shard.local_template() if self.shard is not None else w, self.capacity,
-                                   self._dev())
+            tmpl = self.shard.local_template() if self.shard is not None else w
+            tmpl = collections.OrderedDict((k, v) for k, v in tmpl.items()
+                                           if isinstance(v, torch.Tensor) and v.dtype in engine.DTYPE_CODE)
+            if not tmpl:
+                return False
+            self.slab = UpdateSlab(tmpl, self.capacity, self._dev())
         sl = self.slab
         return (bool(sl._free) and list(w.keys()) == sl.keys
                 and all(isinstance(w[k], torch.Tensor) and w[k].dtype == sl.meta[k][0]
@@ -596,8 +600,11 @@ class DeviceUpdateCache:
             # stream, so back-to-back arrivals keep the copy engine busy while the
             # reductions of earlier arrivals run on the caller's stream
             st = self._side_stream(any(isinstance(v, torch.Tensor) and v.is_cuda for v in w.values()))
+            mixed = self._split_narrow(w) if self.placement == "slab" else None
             if self.placement == "slab" and self._fits_slab(w):
                 tres.weights = self.slab.put(w, stream=st)
+            elif mixed is not None and self._fits_slab(mixed[0]):
+                tres.weights = self._put_mixed(w, *mixed, st)
             else:
                 with torch.cuda.stream(st):
                     tres.weights = w.__class__(
@@ -618,6 +625,25 @@ class DeviceUpdateCache:
         if key in self._d:
             self._d.pop(key)
         self._d[key] = (tres, ev)
+
+    @staticmethod
+    def _split_narrow(w):
+        """(kernel-dtype keys, bool / uint8 / int8 / int16 keys) of an update that has both."""
+        from . import engine
+        main = collections.OrderedDict((k, v) for k, v in w.items()
+                                       if isinstance(v, torch.Tensor) and v.dtype in engine.DTYPE_CODE)
+        if not main or len(main) == len(w):
+            return None
+        return main, collections.OrderedDict((k, v) for k, v in w.items() if k not in main)
+
+    def _put_mixed(self, w, main, extra, st):
+        """The kernel-dtype keys into a slab slot, the others beside it as device tensors."""
+        from .slab import MixedSlotWeights
+        sw = self.slab.put(main, stream=st)
+        with torch.cuda.stream(st):
+            ext = {k: (v.to(self._dev(), non_blocking=True) if isinstance(v, torch.Tensor) else v)
+                   for k, v in extra.items()}
+        return MixedSlotWeights.of(sw, ext, list(w.keys()))
 
     def __getitem__(self, key):
         tres, ev = self._d[key]

@@ -50,6 +50,23 @@ class SlotWeights(dict):
                 pass
 
 
+class MixedSlotWeights(dict):
+    """An update whose kernel-dtype keys sit in a slab slot (tiled views) and whose bool /
+    uint8 / int8 / int16 buffers are plain device tensors beside it, in the update's key
+    order.  No ``slab`` attribute: the engine takes the generic path, reading the tiled
+    views tiled (``client_tile_stride``); ``shapes`` gives every key's model shape; holds
+    the slot's :class:`SlotWeights` so the slot is not recycled while this is alive."""
+
+    __slots__ = ("__weakref__", "shapes", "_owner")
+
+    @classmethod
+    def of(cls, slot: "SlotWeights", extra, order) -> "MixedSlotWeights":
+        w = cls((k, slot[k] if k in slot else extra[k]) for k in order)
+        w.shapes = {k: (slot.shapes[k] if k in slot else tuple(extra[k].shape)) for k in order}
+        w._owner = slot
+        return w
+
+
 class SlabRef(collections.abc.Mapping):
     """Named element ranges of ONE slab slot: ``{name: (slab_key, lo, hi)}`` -- e.g. this
     rank's slices of a client update (flame_amd.shard).  Tiled views are made only when a

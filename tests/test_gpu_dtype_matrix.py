@@ -80,3 +80,61 @@ def test_fedbuff_scale_add_every_model_dtype_vs_torch(agg_dt):
             agg = opt.do(agg, c, total=1, version=10)
         new = opt.scale_add_agg_weights({"k": w0.to(DEV)}, agg, 3)
         S.assert_bitwise(f"{model_dt}+={agg_dt}/3", {"k": new["k"]}, {"k": exp})
+
+
+def test_slab_holds_kernel_keys_beside_narrow_buffers():
+    """A model with a bool mask and a uint8 buffer: DeviceUpdateCache(slab) keeps the
+    kernel-dtype keys in the tiled slab (MixedSlotWeights) and the buffers beside them;
+    FedAvg and FedBuff (+ scale_add) over those entries == torch CPU's own ops, bitwise."""
+    from flame_amd import engine
+    from flame_amd.ingest import DeviceUpdateCache
+    from flame_amd.slab import MixedSlotWeights
+    g = torch.Generator().manual_seed(77)
+    T = engine.chunk_elems(0)
+    shapes = {"w": ((3 * T + 17,), torch.float32), "mask": ((300,), torch.bool), "bf": ((4099,), torch.bfloat16),
+              "u8": ((77,), torch.uint8), "nbt": ((), torch.int64), "m": ((33, 65), torch.float32)}
+
+    def model(scale):
+        return {k: (_rand(g, dt, 1, scale).reshape(()) if s == () else _rand(g, dt, int(torch.tensor(s).prod()),
+                                                                            scale).reshape(s))
+                for k, (s, dt) in shapes.items()}
+    base = model(1.0)
+    ups = [model(1e-1) for _ in range(6)]
+    counts = [3 + 4 * i for i in range(6)]
+    total = sum(counts)
+    # FedAvg: torch CPU reference vs the drop-in over slab-backed entries
+    exp = {k: v.clone() for k, v in base.items()}
+    for u, c in zip(ups, counts):
+        for k in exp:
+            _reference(exp[k], u[k], c / total)
+    cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=8)
+    for i, (u, c) in enumerate(zip(ups, counts)):
+        cache[f"e{i}"] = S.TR({k: v.clone() for k, v in u.items()}, c)
+    w0 = cache["e0"].weights
+    assert isinstance(w0, MixedSlotWeights) and engine.tiled_stride(w0["w"], shapes["w"][0][0])
+    assert cache.slab is not None and cache.slab.keys == ["w", "bf", "nbt", "m"]
+    del w0
+    out = _drop_in("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache, total=total)
+    S.assert_bitwise("fedavg", {k: out[k] for k in out}, exp)
+    # FedBuff one arrival per do(), the aggregate read once at the end, then scale_add
+    ref = None
+    for i, u in enumerate(ups):
+        r = 1 / math.sqrt(1 + 10 - (10 - i % 3))
+        tmps = {k: (v * r).to(v.dtype) for k, v in u.items()}
+        if ref is None:
+            ref = tmps
+        else:
+            for k in ref:
+                ref[k] += tmps[k]
+    opt, agg = _drop_in("fedbuff"), None
+    for i, u in enumerate(ups):
+        c = DeviceUpdateCache(device=DEV, placement="slab", capacity=2) if i == 0 else cache
+        c[f"t{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 1, 10 - i % 3)
+        agg = opt.do(agg, c, total=1, version=10)
+    S.assert_bitwise("fedbuff agg", {k: agg[k] for k in agg}, ref)
+    fl = [k for k, (_, dt) in shapes.items() if dt.is_floating_point]
+    w = {k: base[k].clone() for k in fl}
+    for k in fl:
+        w[k] += ref[k] / 6
+    new = opt.scale_add_agg_weights({k: base[k].to(DEV) for k in fl}, agg, 6)
+    S.assert_bitwise("scale_add", {k: new[k] for k in fl}, w)
