@@ -19,6 +19,7 @@ them complete (or at :func:`flush`), never by synchronising inside ``do()``:
 from __future__ import annotations
 
 import collections
+import contextlib
 from typing import Dict, Iterable, List
 
 from . import engine
@@ -85,6 +86,24 @@ def flush() -> None:
         mc, alias, rec = _pending.pop(0)
         rec[-1][2].synchronize()
         _save(mc, alias, rec)
+
+
+@contextlib.contextmanager
+def recording(owner):
+    """Report the launches made inside the block to ``owner.metric_collector`` -- for work an
+    optimizer queued in ``do()`` and launches later (a deferred aggregate reduced when it is
+    first read), under the owner's alias like its own calls."""
+    mc = getattr(owner, "metric_collector", None)
+    if mc is None or getattr(owner, "_flame_amd_recording", False):
+        yield
+        return
+    owner._flame_amd_recording = True
+    try:
+        with KernelRecorder() as rec:
+            yield
+    finally:
+        owner._flame_amd_recording = False
+    submit(mc, getattr(owner, "metric_alias", None) or type(owner).__name__.lower(), rec)
 
 
 def instrument(fn):

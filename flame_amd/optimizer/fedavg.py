@@ -30,7 +30,7 @@ import logging
 
 import torch
 
-from .. import engine
+from .. import engine, metrics
 from .abstract import AbstractOptimizer
 from .fedbuff import _own_shm_views
 from .regularizer import Regularizer
@@ -41,8 +41,9 @@ logger = logging.getLogger(__name__)
 class DeferredWeights(collections.abc.Mapping):
     """``base_weights`` plus queued eager arrivals, reduced into it on first read."""
 
-    def __init__(self, base, max_pending, max_pending_bytes=None):
+    def __init__(self, base, max_pending, max_pending_bytes=None, owner=None):
         self._base = base
+        self._owner = owner        # the optimizer: its metric_collector sees the flush's launch
         self._pending = []         # [(weights, rate)] in arrival order
         self._max_pending = max_pending
         self._max_bytes = max_pending_bytes
@@ -77,7 +78,8 @@ class DeferredWeights(collections.abc.Mapping):
         if not self._pending:
             return
         entries, self._pending, self._held = self._pending, [], 0
-        engine.accumulate(self._base, entries)
+        with metrics.recording(self._owner):
+            engine.accumulate(self._base, entries)
 
     def __getitem__(self, k):
         self.flush()
@@ -136,7 +138,8 @@ class FedAvg(AbstractOptimizer):
         entries = self._pop_entries(cache, total)
         if self.defer and "flame_amd_key_groups" not in kwargs:
             if pend is None:
-                self._deferred = pend = DeferredWeights(base_weights, self.max_pending, self.max_pending_bytes)
+                self._deferred = pend = DeferredWeights(base_weights, self.max_pending, self.max_pending_bytes,
+                                                        owner=self)
             pend._queue(entries)
             return pend
         # flame_amd.shard passes its plan's waves: one launch per wave, its all-gather started

@@ -28,7 +28,7 @@ import math
 import numpy as np
 import torch
 
-from .. import engine, shm_lease
+from .. import engine, metrics, shm_lease
 from .abstract import AbstractOptimizer
 from .regularizer import Regularizer
 
@@ -38,7 +38,8 @@ logger = logging.getLogger(__name__)
 class DeferredAggregate(collections.abc.Mapping):
     """FedBuff aggregate whose queued arrivals are reduced on first read."""
 
-    def __init__(self, weights, max_pending, max_pending_bytes=None):
+    def __init__(self, weights, max_pending, max_pending_bytes=None, owner=None):
+        self._owner = owner        # the optimizer: its metric_collector sees the flush's launches
         self._keys = list(weights.keys())
         self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
@@ -70,6 +71,10 @@ class DeferredAggregate(collections.abc.Mapping):
         """Reduce every queued arrival (one launch per dtype)."""
         if not self._pending:
             return
+        with metrics.recording(self._owner):
+            self._flush()
+
+    def _flush(self):
         if self._data is None and not _uniform(self):
             # later arrivals carry a subset of the first one's keys, or other dtypes: the
             # reference adds them key by key (fedbuff.py:143-157), so does accumulate()
@@ -165,7 +170,7 @@ class FedBuff(AbstractOptimizer):
             # each cached entry re-creates the aggregate: only the last one survives (fedbuff.py:139-140)
             weights, rate = entries[-1]
             if self.defer:
-                agg = DeferredAggregate(weights, self.max_pending, self.max_pending_bytes)
+                agg = DeferredAggregate(weights, self.max_pending, self.max_pending_bytes, owner=self)
                 agg._queue([(weights, rate)])
                 self.agg_goal_weights = agg
             else:

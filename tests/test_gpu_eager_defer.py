@@ -141,3 +141,43 @@ def test_eager_deferred_new_base_flushes_old():
     b.do(b2b, cb, total=4)
     assert r3.materialize() is b2a
     S.assert_bitwise("new base", S.to_cpu(dict(r3.items())), S.to_cpu(b2b))
+
+
+def test_deferred_flush_reports_to_metric_collector():
+    """The launch a deferred eager FedAvg (and a deferred FedBuff aggregate) makes when it is
+    read, outside any do(), still reaches the optimizer's metric_collector."""
+    from flame_amd import metrics
+
+    class MC:
+        def __init__(self):
+            self.state_dict = {}
+
+        def save(self, mtype, alias, value):
+            self.state_dict[f"{alias}.{mtype}"] = value
+
+    g = torch.Generator().manual_seed(9)
+    opt = _fedavg(defer=True)
+    opt.metric_collector = MC()
+    base = {"x": torch.randn(50_001, generator=g).to(DEV)}
+    total, out = 0, None
+    for i in range(5):
+        total += 3 + i
+        c = S.SortedCache()
+        c[f"e{i}"] = S.TR({"x": (torch.randn(50_001, generator=g) * 1e-2).to(DEV)}, 3 + i)
+        out = opt.do(base, c, total=total)
+    assert out.pending == 5
+    _ = out["x"]
+    metrics.flush()
+    sd = opt.metric_collector.state_dict
+    assert sd["fedavg.flame_agg_reduce.launches"] == 1, sd
+    from flame_amd.optimizers import optimizer_provider
+    fb = optimizer_provider.get("fedbuff")
+    fb.metric_collector = MC()
+    agg = None
+    for i in range(4):
+        c = S.SortedCache()
+        c["t"] = S.TR({"x": (torch.randn(50_001, generator=g) * 1e-2).to(DEV)}, 1, 7)
+        agg = fb.do(agg, c, total=1, version=7)
+    _ = agg["x"]
+    metrics.flush()
+    assert fb.metric_collector.state_dict.get("fedbuff.flame_agg_reduce.launches") == 1, fb.metric_collector.state_dict
