@@ -126,6 +126,13 @@ def setup_dist(force_group=False):
     torch.cuda.set_device(local)
     if world > 1 or force_group:
         import torch.distributed as dist
+        if "RANK" not in os.environ:      # --force-shard without torchrun: a world-1 group
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(sk.getsockname()[1]))
+            sk.close()
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
