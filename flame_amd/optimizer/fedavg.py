@@ -27,6 +27,7 @@ anything reads the result (``w[k]``, ``items()``, ``load_state_dict``, ``deepcop
 import collections.abc
 import copy
 import logging
+import weakref
 
 import torch
 
@@ -43,7 +44,9 @@ class DeferredWeights(collections.abc.Mapping):
 
     def __init__(self, base, max_pending, max_pending_bytes=None, owner=None):
         self._base = base
-        self._owner = owner        # the optimizer: its metric_collector sees the flush's launch
+        # the optimizer (weakly: it holds this object; a cycle would keep queued slab slots
+        # alive until the cyclic GC): its metric_collector sees the flush's launch
+        self._owner = weakref.ref(owner) if owner is not None else None
         self._pending = []         # [(weights, rate)] in arrival order
         self._max_pending = max_pending
         self._max_bytes = max_pending_bytes
@@ -78,7 +81,7 @@ class DeferredWeights(collections.abc.Mapping):
         if not self._pending:
             return
         entries, self._pending, self._held = self._pending, [], 0
-        with metrics.recording(self._owner):
+        with metrics.recording(self._owner() if self._owner is not None else None):
             engine.accumulate(self._base, entries)
 
     def __getitem__(self, k):

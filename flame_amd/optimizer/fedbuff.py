@@ -24,6 +24,7 @@ import collections.abc
 import copy
 import logging
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -39,7 +40,9 @@ class DeferredAggregate(collections.abc.Mapping):
     """FedBuff aggregate whose queued arrivals are reduced on first read."""
 
     def __init__(self, weights, max_pending, max_pending_bytes=None, owner=None):
-        self._owner = owner        # the optimizer: its metric_collector sees the flush's launches
+        # the optimizer (weakly: it holds this object; a cycle would keep queued slab slots
+        # alive until the cyclic GC): its metric_collector sees the flush's launches
+        self._owner = weakref.ref(owner) if owner is not None else None
         self._keys = list(weights.keys())
         self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
@@ -71,7 +74,7 @@ class DeferredAggregate(collections.abc.Mapping):
         """Reduce every queued arrival (one launch per dtype)."""
         if not self._pending:
             return
-        with metrics.recording(self._owner):
+        with metrics.recording(self._owner() if self._owner is not None else None):
             self._flush()
 
     def _flush(self):

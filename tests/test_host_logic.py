@@ -432,3 +432,39 @@ def test_eager_fedavg_defer_raises_at_the_bad_arrival(monkeypatch):
     with pytest.raises(KeyError):
         opt.do(base, c, total=3)
     assert out.pending == 1
+
+
+def test_deferred_queues_free_their_arrivals_without_the_cyclic_gc(monkeypatch):
+    """A deferred aggregate holds its optimizer weakly: dropping the optimizer and the
+    aggregate frees the queued arrivals at once (slab slots return to the slab), with the
+    cyclic garbage collector off."""
+    import gc
+    import weakref
+    import scenarios as S
+    from flame_amd.optimizer import fedavg as F, fedbuff as B
+
+    class W(dict):
+        pass
+    monkeypatch.setattr(F.engine, "accumulate", lambda *a, **k: None)
+    gc.disable()
+    try:
+        w = W(x=torch.ones(3))
+        ref = weakref.ref(w)
+        fb = B.FedBuff()
+        c = S.SortedCache()
+        c["a"] = S.TR(w, 1, 0)
+        agg = fb.do(None, c, total=1, version=0)
+        assert agg._pending
+        del w, c, fb, agg
+        assert ref() is None, "FedBuff's queue outlived its optimizer and aggregate"
+        w = W(x=torch.ones(3))
+        ref = weakref.ref(w)
+        fa = F.FedAvg(defer=True)
+        c = S.SortedCache()
+        c["a"] = S.TR(w, 1)
+        out = fa.do({"x": torch.zeros(3)}, c, total=1)
+        assert out.pending == 1
+        del w, c, fa, out
+        assert ref() is None, "FedAvg's queue outlived its optimizer"
+    finally:
+        gc.enable()
