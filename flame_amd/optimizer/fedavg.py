@@ -60,7 +60,9 @@ class DeferredWeights(collections.abc.Mapping):
         for k in w.keys():
             if k not in self._base:
                 raise KeyError(k)
-            engine._check_cast(self._base[k].dtype, engine.weight_dtype(w, k))
+            acc, dt = self._base[k].dtype, engine.weight_dtype(w, k)
+            if dt != acc:
+                engine._check_cast(acc, dt)
 
     def _queue(self, entries):
         for w, _ in entries:

@@ -59,7 +59,9 @@ class DeferredAggregate(collections.abc.Mapping):
                 if k not in self._meta:
                     raise KeyError(k)
                 # `agg[k] += tmp` (fedbuff.py:157) raises from the do() that brings it
-                engine._check_cast(self._meta[k][1], engine.weight_dtype(w, k))
+                dt = engine.weight_dtype(w, k)
+                if dt != self._meta[k][1]:
+                    engine._check_cast(self._meta[k][1], dt)
         # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
         # before do() returns: the sender may rewrite the segment while it waits in the queue
         entries = [(_own_shm_views(w), r) for w, r in entries]
