@@ -839,7 +839,7 @@ def test_middle_group_flush_and_scale_add_many(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("placement", ["slab", "tensors"])
+@pytest.mark.parametrize("placement", ["slab", "tensors", "mixed"])
 @pytest.mark.parametrize("top_start", ["none", "existing"])
 @pytest.mark.parametrize("M", [5, 21])
 def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
@@ -863,7 +863,7 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
     mid_ver = [rnd - (m % 3) for m in range(M)]
     goals = [[C, C + 1, C, 3, C][m % 5] for m in range(M)]
     slab = UpdateSlab({k: torch.empty(s, dtype=dtype) for k, s in shapes.items()}, capacity=M * C, device=DEV) \
-        if placement == "slab" else None
+        if placement != "tensors" else None
 
     def arrivals():
         opts, aggs = [make_amd("fedbuff") for _ in range(M)], [None] * M
@@ -871,7 +871,9 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
             for t in range(C):
                 w = {k: v.to(DEV) for k, v in ups[m][t].items()}
                 cache = S.SortedCache()
-                cache["a"] = S.TR(slab.put(w) if slab is not None else w, 1, vers[m][t])
+                # "mixed": a middle's arrivals alternate between slab slots and plain tensors
+                in_slab = slab is not None and (placement == "slab" or (m + t) % 2 == 0)
+                cache["a"] = S.TR(slab.put(w) if in_slab else w, 1, vers[m][t])
                 aggs[m] = opts[m].do(aggs[m], cache, total=1, version=rnd)
         return aggs
 
