@@ -43,6 +43,7 @@ class DeferredAggregate(collections.abc.Mapping):
         # the optimizer (weakly: it holds this object; a cycle would keep queued slab slots
         # alive until the cyclic GC): its metric_collector sees the flush's launches
         self._owner = weakref.ref(owner) if owner is not None else None
+        self._slabs_ok = []        # slabs whose slots passed _queue's key / dtype checks
         self._keys = list(weights.keys())
         self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
@@ -55,6 +56,10 @@ class DeferredAggregate(collections.abc.Mapping):
 
     def _queue(self, entries):
         for w, _ in entries:
+            slab = getattr(w, "slab", None)
+            whole_slot = slab is not None and getattr(w, "ranges", None) is None
+            if whole_slot and slab in self._slabs_ok:
+                continue              # the slots of one slab share keys and dtypes: checked once
             for k in w.keys():
                 if k not in self._meta:
                     raise KeyError(k)
@@ -62,6 +67,8 @@ class DeferredAggregate(collections.abc.Mapping):
                 dt = engine.weight_dtype(w, k)
                 if dt != self._meta[k][1]:
                     engine._check_cast(self._meta[k][1], dt)
+            if whole_slot:
+                self._slabs_ok.append(slab)
         # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
         # before do() returns: the sender may rewrite the segment while it waits in the queue
         entries = [(_own_shm_views(w), r) for w, r in entries]
