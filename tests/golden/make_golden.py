@@ -835,7 +835,46 @@ def narrow_cases():
     print("wrote narrow.npz")
 
 
-CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "narrow_cases": narrow_cases, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+def feddyn_narrow():
+    """feddyn_rounds' call pattern over a model that also carries a bool mask and a uint8
+    buffer (histories `h + w`, the mean `rate * h` and `cld = avg + mean` in torch's dtypes)."""
+    gen = torch.Generator().manual_seed(83)
+    all_ends = [f"e{i}" for i in range(4)]
+    rounds = [["e0", "e1", "e2"], ["e1", "e2", "e3"], ["e0", "e3", "x7"]]
+
+    def model(scale):
+        w = small_weights(gen, FEDDYN_SHAPES, scale)
+        w["mask"] = torch.rand(257, generator=gen) < 0.4
+        w["u8"] = torch.randint(0, 60, (65,), generator=gen).to(torch.uint8)
+        return w
+    weights = model(1.0)
+    opt = optimizer_provider.get("feddyn", alpha=0.01)
+    fw = FixtureWriter()
+    fw.put_weights("weights0", weights)
+    cld = weights
+    all_counts, orders = [], []
+    for r, ends in enumerate(rounds):
+        opt.save_state(TrainState.PRE, active_ends=all_ends)
+        clients = [model(1e-2) for _ in ends]
+        counts = [int(x) for x in torch.randint(1, 1001, (len(ends),), generator=gen)]
+        cache = Cache()
+        for e, w, c in zip(ends, clients, counts):
+            cache[e] = TrainResult(w, c)
+        orders.append(list(cache.iterkeys()))
+        all_counts.append(counts)
+        out = opt.do(deepcopy(cld), cache, total=sum(counts), num_trainers=len(ends))
+        cld = opt.cld_model if opt.cld_model is not None else out
+        for i, w in enumerate(clients):
+            fw.put_weights(f"r{r}/client{i}", w)
+        fw.put_weights(f"r{r}/avg", out)
+        fw.put_weights(f"r{r}/cld", opt.cld_model)
+    fw.meta.update({"kind": "feddyn_rounds", "alpha": 0.01, "all_ends": all_ends, "rounds": rounds,
+                    "orders": orders, "counts": all_counts})
+    fw.save(os.path.join(HERE, "feddyn_narrow.npz"))
+    print("wrote feddyn_narrow.npz")
+
+
+CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "narrow_cases": narrow_cases, "feddyn_narrow": feddyn_narrow, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -868,6 +907,7 @@ def main():
     hier_fedbuff_wide()
     downcast_cases()
     narrow_cases()
+    feddyn_narrow()
 
 
 if __name__ == "__main__":

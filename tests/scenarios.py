@@ -521,6 +521,7 @@ BITWISE_FIXTURES = [
     ("downcast.npz", run_downcast),
     ("narrow.npz", run_narrow),
     ("feddyn_rounds.npz", run_feddyn),
+    ("feddyn_narrow.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
     ("hier_fedavg_small.npz", run_hier_fedavg),
