@@ -138,3 +138,39 @@ def test_slab_holds_kernel_keys_beside_narrow_buffers():
         w[k] += ref[k] / 6
     new = opt.scale_add_agg_weights({k: base[k].to(DEV) for k in fl}, agg, 6)
     S.assert_bitwise("scale_add", {k: new[k] for k in fl}, w)
+
+
+def test_sync_hierarchy_with_narrow_buffers_vs_oracle():
+    """The synchronous hierarchy over a model with a uint8 buffer and an int16 buffer next
+    to f32 / bf16 keys: the fused kernel keys and the composed narrow keys == the oracle's
+    op sequence (middle FedAvg, delta new - old, the top's FedAvg of the deltas), bitwise."""
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    g = torch.Generator().manual_seed(61)
+    shapes = {"w": ((3001,), torch.float32), "bf": ((515,), torch.bfloat16), "u8": ((77,), torch.uint8),
+              "i16": ((33,), torch.int16)}
+
+    def model(scale):
+        return {k: _rand(g, dt, s[0], scale) for k, (s, dt) in shapes.items()}
+    M, C = 5, 3
+    mids = [model(1.0) for _ in range(M)]
+    ups = [[model(1e-1) for _ in range(C)] for _ in range(M)]
+    counts = [[2 + m + 3 * t for t in range(C)] for m in range(M)]
+    top = model(1.0)
+
+    def run(dev, fn):
+        mw = [{k: v.clone().to(dev) for k, v in w.items()} for w in mids]
+        tw = {k: v.clone().to(dev) for k, v in top.items()}
+        middles = []
+        for m in range(M):
+            c = S.SortedCache()
+            for t in range(C):
+                c[f"t{t}"] = S.TR({k: v.clone().to(dev) for k, v in ups[m][t].items()}, counts[m][t])
+            middles.append((mw[m], c, sum(counts[m])))
+        tw, deltas = fn(middles, tw, with_delta=True)
+        return S.to_cpu(tw), [S.to_cpu(d) for d in deltas], [S.to_cpu(w) for w in mw]
+    got = run(DEV, sync_hierarchy_round)
+    exp = run("cpu", S.oracle_sync_hierarchy_round)
+    S.assert_bitwise("top", got[0], exp[0])
+    for m in range(M):
+        S.assert_bitwise(f"delta m{m}", got[1][m], exp[1][m])
+        S.assert_bitwise(f"mid m{m}", got[2][m], exp[2][m])
