@@ -24,6 +24,7 @@ anything reads the result (``w[k]``, ``items()``, ``load_state_dict``, ``deepcop
 ``max_pending`` arrivals / ``max_pending_bytes`` are queued.  ``base_weights`` itself
 (a plain dict) lags until then: read the returned object, as flame's roles do.
 """
+import collections
 import collections.abc
 import copy
 import logging
@@ -102,6 +103,10 @@ class DeferredWeights(collections.abc.Mapping):
     def __deepcopy__(self, memo):
         self.flush()
         return copy.deepcopy(self._base, memo)
+
+    def __reduce__(self):
+        # pickling (torch.save, a checkpoint) stores the reduced model as a state_dict-style OrderedDict
+        return (collections.OrderedDict, (list(self.items()),))
 
     def materialize(self):
         """``base_weights`` itself, every queued arrival reduced into it."""

@@ -121,6 +121,11 @@ class DeferredAggregate(collections.abc.Mapping):
         self.flush()
         return copy.deepcopy(dict(self._data), memo)
 
+    def __reduce__(self):
+        # pickling (torch.save, a checkpoint) stores the reduced aggregate as a state_dict-style OrderedDict
+        self.flush()
+        return (collections.OrderedDict, (list(self._data.items()),))
+
     def materialize(self):
         """The aggregate as a plain dict of tensors (flushes)."""
         self.flush()
