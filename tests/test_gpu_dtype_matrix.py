@@ -174,3 +174,43 @@ def test_sync_hierarchy_with_narrow_buffers_vs_oracle():
     for m in range(M):
         S.assert_bitwise(f"delta m{m}", got[1][m], exp[1][m])
         S.assert_bitwise(f"mid m{m}", got[2][m], exp[2][m])
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedadagrad"])
+def test_fedopt_with_narrow_buffers_vs_oracle(sort):
+    """FedOPT over a model with uint8 / int16 buffers next to f32 / bf16 keys, 3 rounds: the
+    reduction in the kernels (narrow keys: fp32 tmp + cast, wrapping adds), the adaptive step
+    of the narrow keys as the reference's torch op sequence (their d, m, v, current promote
+    to fp32) -- against the oracle within the SURVEY §8(c) FedOPT contract."""
+    from oracle import oracle as O
+    g = torch.Generator().manual_seed(71)
+    shapes = {"w": ((2049,), torch.float32), "bf": ((300,), torch.bfloat16), "u8": ((65,), torch.uint8),
+              "i16": ((33,), torch.int16)}
+
+    def model(scale):
+        return {k: _rand(g, dt, s[0], scale) for k, (s, dt) in shapes.items()}
+    hyper = dict(beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    ora = O.OracleFedOPT(sort, **hyper)
+    from flame_amd.optimizers import optimizer_provider
+    amd = optimizer_provider.get(sort, **hyper)
+    w = model(1.0)
+    wa, wo = {k: v.to(DEV) for k, v in w.items()}, {k: v.clone() for k, v in w.items()}
+    for rnd in range(3):
+        ups = [model(1e-1) for _ in range(4)]
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i, u in enumerate(ups):
+            ca[f"e{i}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, 5 + i)
+            co[f"e{i}"] = S.TR({k: v.clone() for k, v in u.items()}, 5 + i)
+        wa = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=26)
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, co, total=26)
+        got = S.to_cpu(wa)
+        for k in shapes:
+            assert got[k].dtype == wo[k].dtype, (rnd, k, got[k].dtype, wo[k].dtype)
+            if got[k].is_floating_point():
+                # int16's d**2 wraps negative in the reference, so sqrt(v) is NaN there: the
+                # NaNs must land where the oracle's do; the rest is checked by the contract
+                nan = torch.isnan(wo[k])
+                assert torch.equal(torch.isnan(got[k]), nan), (sort, rnd, k)
+                got[k] = got[k].masked_fill(nan, 0)
+        exp = {k: (v.masked_fill(torch.isnan(v), 0) if v.is_floating_point() else v) for k, v in wo.items()}
+        S.assert_close_fedopt(f"{sort} r{rnd}", got, exp, elementwise=(rnd < 2))
