@@ -428,6 +428,53 @@ def scaffold_rounds():
     print("wrote scaffold_rounds.npz")
 
 
+def scaffold_narrow():
+    """scaffold_rounds over a model that also carries a bool mask and a uint8 buffer (their
+    control variates arrive as fp32).  SCAFFOLD as its top aggregator drives it (scaffold/top_aggregator.py:115-126,160,177):
+    save_state(PRE, dataset_sizes=...) once, save_state(PRE, glob_weights=weights) every
+    round, do(deepcopy(weights), cache, ..., control_cache=control_cache).  The int64
+    buffer's control variate arrives as fp32 (the reference casts it back, scaffold.py:143-148)."""
+    gen = torch.Generator().manual_seed(84)
+    ends = [f"e{i}" for i in range(7)]
+    sizes = {e: int(x) for e, x in zip(ends, torch.randint(100, 5000, (len(ends),), generator=gen))}
+    rounds = [ends[:5], ends[2:], ends[::2]]
+    weights = small_weights(gen, FEDDYN_SHAPES, 1.0)
+    weights["mask"] = torch.rand(129, generator=gen) < 0.4
+    weights["u8"] = torch.randint(0, 60, (33,), generator=gen).to(torch.uint8)
+    opt = optimizer_provider.get("scaffold", k=3)
+    opt.save_state(TrainState.PRE, dataset_sizes=sizes)
+    fw = FixtureWriter()
+    fw.put_weights("weights0", weights)
+    orders = []
+    for r, rends in enumerate(rounds):
+        opt.save_state(TrainState.PRE, glob_weights=weights)
+        clients = [small_weights(gen, FEDDYN_SHAPES, 1e-2) for _ in rends]
+        controls = [small_weights(gen, FEDDYN_SHAPES, 1e-3) for _ in rends]
+        for i, (c, cv) in enumerate(zip(clients, controls)):
+            c["nbt"] = torch.tensor(7 * r + i, dtype=torch.int64)
+            cv["nbt"] = torch.tensor(9.25 * (i + 1) + r, dtype=torch.float32)
+            c["mask"] = torch.rand(129, generator=gen) < 0.4
+            c["u8"] = torch.randint(0, 60, (33,), generator=gen).to(torch.uint8)
+            cv["mask"] = torch.randn(129, generator=gen) * 1e-3
+            cv["u8"] = torch.randn(33, generator=gen) * 1e-3
+        cache, control_cache = Cache(), Cache()
+        for e, w, cv in zip(rends, clients, controls):
+            cache[e] = TrainResult(w, sizes[e])
+            control_cache[e] = TrainResult(cv)
+        orders.append(list(cache.iterkeys()))
+        weights = opt.do(deepcopy(weights), cache, total=sum(sizes[e] for e in rends),
+                         num_trainers=len(rends), control_cache=control_cache)
+        for i, (w, cv) in enumerate(zip(clients, controls)):
+            fw.put_weights(f"r{r}/client{i}", w)
+            fw.put_weights(f"r{r}/control{i}", cv)
+        fw.put_weights(f"r{r}/out", weights)
+        fw.put_weights(f"r{r}/c_glob", opt.c_glob)
+    fw.meta.update({"kind": "scaffold_rounds", "k": 3, "dataset_sizes": sizes, "rounds": rounds,
+                    "orders": orders})
+    fw.save(os.path.join(HERE, "scaffold_narrow.npz"))
+    print("wrote scaffold_narrow.npz")
+
+
 def fedgft_rounds():
     """FedGFT as its top aggregator drives it (fedgft/top_aggregator.py:52-86 + syncfl
     aggregate): do(deepcopy(weights), cache, total=...) -- inherited FedAvg.do
@@ -874,7 +921,7 @@ def feddyn_narrow():
     print("wrote feddyn_narrow.npz")
 
 
-CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "narrow_cases": narrow_cases, "feddyn_narrow": feddyn_narrow, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
+CASES = {"hier_fedbuff_wide": hier_fedbuff_wide, "downcast_cases": downcast_cases, "narrow_cases": narrow_cases, "feddyn_narrow": feddyn_narrow, "scaffold_narrow": scaffold_narrow, "fedopt_mixed_more": fedopt_mixed_more, "nonfinite": nonfinite, "fedbuff_dtypes": fedbuff_dtypes, "subset_cases": subset_cases, "fedopt_eager": fedopt_eager, "feddyn_rounds": feddyn_rounds, "hier_fedavg_small": hier_fedavg_small, "scaffold_rounds": scaffold_rounds, "fedgft_rounds": fedgft_rounds}
 
 
 def main():
@@ -908,6 +955,7 @@ def main():
     downcast_cases()
     narrow_cases()
     feddyn_narrow()
+    scaffold_narrow()
 
 
 if __name__ == "__main__":

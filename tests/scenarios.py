@@ -523,6 +523,7 @@ BITWISE_FIXTURES = [
     ("feddyn_rounds.npz", run_feddyn),
     ("feddyn_narrow.npz", run_feddyn),
     ("scaffold_rounds.npz", run_scaffold),
+    ("scaffold_narrow.npz", run_scaffold),
     ("fedgft_rounds.npz", run_fedgft),
     ("hier_fedavg_small.npz", run_hier_fedavg),
 ]
