@@ -20,6 +20,9 @@ Other workloads (DESIGN.md numbers; the driver's bench line is the default):
                                           one GPU's 15.6M-param shard at N=1; at N>1 the
                                           product's ShardedHierarchy over a (15.6M x N)-param
                                           model with the top model all-gathered over RCCL
+  --workload fedavg_eager [--eager-defer on|off]
+                                          the eager top aggregator's round: one do() per
+                                          arrival, batched into one launch (on) or not
   --e2e                                   host-resident updates: H2D + kernel + D2H
 """
 import argparse
