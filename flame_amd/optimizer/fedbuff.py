@@ -55,8 +55,13 @@ class DeferredAggregate(collections.abc.Mapping):
                                   for s, dt in self._meta.values())
 
     def _queue(self, entries):
+        held = 0
         for w, _ in entries:
             slab = getattr(w, "slab", None)
+            if slab is None:
+                # a queued arrival keeps its update alive (the reference frees it once folded
+                # in); slab slots are preallocated, anything else counts against max_pending_bytes
+                held += self._arrival_bytes
             whole_slot = slab is not None and getattr(w, "ranges", None) is None
             if whole_slot and slab in self._slabs_ok:
                 continue              # the slots of one slab share keys and dtypes: checked once
@@ -71,11 +76,10 @@ class DeferredAggregate(collections.abc.Mapping):
                 self._slabs_ok.append(slab)
         # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
         # before do() returns: the sender may rewrite the segment while it waits in the queue
-        entries = [(_own_shm_views(w), r) for w, r in entries]
+        if shm_lease.active():
+            entries = [(_own_shm_views(w), r) for w, r in entries]
         self._pending.extend(entries)
-        # a queued arrival keeps its update alive (the reference frees it once folded in); slab
-        # slots are preallocated, anything else counts against max_pending_bytes
-        self._held += sum(self._arrival_bytes for w, _ in entries if getattr(w, "slab", None) is None)
+        self._held += held
         if len(self._pending) >= self._max_pending or (self._max_bytes is not None and self._held > self._max_bytes):
             self.flush()
 
