@@ -51,7 +51,7 @@ class DeferredAggregate(collections.abc.Mapping):
         self._max_pending = max_pending
         self._max_bytes = max_pending_bytes
         self._held = 0             # bytes of queued arrivals that own their memory (not slab slots)
-        self._arrival_bytes = sum(math.prod(s) * torch.empty(0, dtype=dt).element_size()
+        self._arrival_bytes = sum(math.prod(s) * dt.itemsize
                                   for s, dt in self._meta.values())
 
     def _queue(self, entries):
