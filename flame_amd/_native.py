@@ -29,6 +29,8 @@ FLAME_DYN_W, FLAME_DYN_AVG, FLAME_DYN_HIN, FLAME_DYN_HOUT, FLAME_DYN_MEAN = 1, 2
 HIER_SEGMENT_INT64S = 8  # sizeof(flame_hier_segment) / 8
 DYN_SEGMENT_INT64S = 8  # sizeof(flame_dyn_segment) / 8
 SEGMENT_INT64S = 10  # sizeof(flame_segment) / 8
+TILE_COPY_INT64S = 4  # sizeof(flame_tile_copy) / 8
+FLAME_TILE_BYTES = 4096
 
 # every symbol include/flame_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -36,6 +38,7 @@ EXPORTS = (
     "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
     "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
+    "flame_slab_write", "flame_slab_write_2d",
 )
 
 
@@ -96,6 +99,10 @@ def lib() -> ctypes.CDLL:
     L.flame_host_unregister.argtypes = [vp]
     L.flame_host_device_pointer.restype = ctypes.c_int
     L.flame_host_device_pointer.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p)]
+    L.flame_slab_write.restype = ctypes.c_int
+    L.flame_slab_write.argtypes = [vp, i32, vp]
+    L.flame_slab_write_2d.restype = ctypes.c_int
+    L.flame_slab_write_2d.argtypes = [vp, i32, vp]
     if L.flame_abi_version() != 1:
         raise ImportError(f"flame_amd ABI mismatch: library {L.flame_abi_version()} != 1")
     _lib = L

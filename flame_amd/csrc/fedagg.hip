@@ -1342,6 +1342,56 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
     }
 }
 
+// ---------------------------------------------------------------- slab insert (tiling copy)
+// The role's `self.cache[end] = tres` (syncfl/top_aggregator.py:154-156) lands one update
+// in a slab slot: each key's contiguous bytes are cut into 4 KiB tiles (one reduction
+// chunk of any dtype) written `dst_tile_stride` apart (the slab's capacity x 4 KiB).  One
+// workgroup copies kSlabTPW tiles, every lane 16 B of each (all its loads issued before its
+// stores); the entry table rides in the kernel arguments, so an insert is ONE launch and no
+// H2D of metadata.
+constexpr int kSlabTPW = 4;
+struct SlabEntry { const uint8_t* src; uint8_t* dst; int64_t nbytes; int64_t stride; int64_t tile_begin; };
+constexpr int kSlabMaxEntries = static_cast<int>(sizeof(ArgMeta) / sizeof(SlabEntry));
+static_assert(FLAME_TILE_BYTES == kBlock * 16, "a slab tile is one 16-byte vector per lane");
+
+__global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, int n_entries, int64_t n_tiles) {
+    (void)sizeof(meta);
+    const SlabEntry* ents = (const SlabEntry*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int lane = threadIdx.x;
+    V16 v[kSlabTPW];
+    uint8_t* dp[kSlabTPW];
+    int kind[kSlabTPW];   // 0 none, 1 vector, 2 bytes
+#pragma unroll
+    for (int j = 0; j < kSlabTPW; ++j) {
+        const int64_t tile = static_cast<int64_t>(blockIdx.x) * kSlabTPW + j;
+        kind[j] = 0;
+        dp[j] = nullptr;
+        if (tile >= n_tiles) continue;
+        int lo = 0, hi = n_entries - 1;           // wave-uniform: last entry with tile_begin <= tile
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ents[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
+        }
+        const SlabEntry& e = ents[lo];
+        const int64_t t = tile - e.tile_begin;
+        const int64_t off = t * FLAME_TILE_BYTES + lane * 16;
+        if (off >= e.nbytes) continue;
+        dp[j] = e.dst + t * e.stride + lane * 16;
+        const uint8_t* sp = e.src + off;
+        if (off + 16 <= e.nbytes && (reinterpret_cast<uintptr_t>(sp) & 15) == 0) {
+            v[j] = ld_nt(sp);
+            kind[j] = 1;
+        } else {                                  // ragged tail or a misaligned source view
+            const int nb = static_cast<int>(e.nbytes - off < 16 ? e.nbytes - off : 16);
+            for (int b = 0; b < nb; ++b) st1(dp[j] + b, ld1(sp + b));
+            kind[j] = 2;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kSlabTPW; ++j)
+        if (kind[j] == 1) st_pol<1>(dp[j], v[j]);
+}
+
 constexpr int kClientUnroll = FLAME_CU;
 constexpr int kClientUnroll16 = FLAME_CU16;
 constexpr int kHierUnroll16 = FLAME_HCU16;
@@ -1783,6 +1833,71 @@ int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_
     default: return set_err(FLAME_ENOTSUP, "flame_synth_fill: dtype %d not supported", dtype);
     }
     return check_launch("flame_synth_fill");
+}
+
+static int check_tile_copies(const flame_tile_copy* t, int32_t n, const char* who) {
+    if (n < 0 || (n > 0 && !t)) return set_err(FLAME_EINVAL, "%s: NULL table or n_entries < 0", who);
+    for (int32_t i = 0; i < n; ++i) {
+        if (t[i].nbytes < 0) return set_err(FLAME_EINVAL, "%s: entry %d: nbytes < 0", who, i);
+        if (t[i].nbytes == 0) continue;
+        if (!t[i].src || !t[i].dst) return set_err(FLAME_EINVAL, "%s: entry %d: NULL pointer", who, i);
+        if (reinterpret_cast<uintptr_t>(t[i].dst) % 16)
+            return set_err(FLAME_EINVAL, "%s: entry %d: dst not 16-byte aligned", who, i);
+        if (t[i].nbytes > FLAME_TILE_BYTES && (t[i].dst_tile_stride < FLAME_TILE_BYTES || t[i].dst_tile_stride % 16))
+            return set_err(FLAME_EINVAL, "%s: entry %d: dst_tile_stride %lld must be >= %d and a multiple of 16", who,
+                           i, static_cast<long long>(t[i].dst_tile_stride), FLAME_TILE_BYTES);
+    }
+    return FLAME_OK;
+}
+
+int flame_slab_write(const flame_tile_copy* table, int32_t n_entries, void* stream) {
+    int rc = check_tile_copies(table, n_entries, "flame_slab_write");
+    if (rc) return rc;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    g_err[0] = 0;
+    int32_t i = 0;
+    while (i < n_entries) {           // up to kSlabMaxEntries keys per launch (one launch for most models)
+        ArgMeta m;
+        SlabEntry* ents = reinterpret_cast<SlabEntry*>(m.w);
+        int n = 0;
+        int64_t tiles = 0;
+        for (; i < n_entries && n < kSlabMaxEntries; ++i) {
+            if (table[i].nbytes == 0) continue;
+            ents[n] = SlabEntry{static_cast<const uint8_t*>(table[i].src), static_cast<uint8_t*>(table[i].dst),
+                                table[i].nbytes, table[i].dst_tile_stride, tiles};
+            tiles += (table[i].nbytes + FLAME_TILE_BYTES - 1) / FLAME_TILE_BYTES;
+            ++n;
+        }
+        if (n == 0) break;
+        const int64_t blocks = (tiles + kSlabTPW - 1) / kSlabTPW;
+        if (blocks > 0x7FFFFFFFll) return set_err(FLAME_EINVAL, "flame_slab_write: %lld tiles", (long long)tiles);
+        hipLaunchKernelGGL(slab_write_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, m, n, tiles);
+        rc = check_launch("flame_slab_write");
+        if (rc) return rc;
+    }
+    return FLAME_OK;
+}
+
+int flame_slab_write_2d(const flame_tile_copy* table, int32_t n_entries, void* stream) {
+    int rc = check_tile_copies(table, n_entries, "flame_slab_write_2d");
+    if (rc) return rc;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    for (int32_t i = 0; i < n_entries; ++i) {
+        const flame_tile_copy& t = table[i];
+        if (t.nbytes == 0) continue;
+        const int64_t full = t.nbytes / FLAME_TILE_BYTES, rem = t.nbytes % FLAME_TILE_BYTES;
+        hipError_t e = hipSuccess;
+        if (full)
+            e = hipMemcpy2DAsync(t.dst, static_cast<size_t>(t.dst_tile_stride), t.src, FLAME_TILE_BYTES,
+                                 FLAME_TILE_BYTES, static_cast<size_t>(full), hipMemcpyDefault, st);
+        if (e == hipSuccess && rem)
+            e = hipMemcpyAsync(static_cast<uint8_t*>(t.dst) + full * t.dst_tile_stride,
+                               static_cast<const uint8_t*>(t.src) + full * FLAME_TILE_BYTES, static_cast<size_t>(rem),
+                               hipMemcpyDefault, st);
+        if (e != hipSuccess) return set_err(FLAME_EHIP, "flame_slab_write_2d: entry %d: %s", i, hipGetErrorString(e));
+    }
+    g_err[0] = 0;
+    return FLAME_OK;
 }
 
 }  // extern "C"

@@ -186,6 +186,16 @@ class _Staging:
             ev, _ = self._inflight.popleft()
             ev.synchronize()
 
+    def hold_on(self, stream, host_tensors) -> None:
+        """Keep host tensors an asynchronous copy on ``stream`` reads alive until it has passed
+        this point (a view of a sender's shared-memory segment: wait here, see ``hold``)."""
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        if any(shm_lease.aliases(t) for t in host_tensors):
+            ev.synchronize()
+            return
+        self._inflight.append((ev, list(host_tensors)))
+
     def hold(self, host_tensor: torch.Tensor, device) -> None:
         """Keep a host tensor a kernel reads directly alive until the stream passes this point.
         A view into a sender's shared-memory segment is instead waited for here: the sender

@@ -29,8 +29,10 @@ import collections
 import collections.abc
 from typing import Dict, List
 
+import numpy as np
 import torch
 
+from . import _native as N
 from . import engine
 
 
@@ -119,6 +121,7 @@ class UpdateSlab:
         self._free = collections.deque(range(self.capacity))
         self._ready = {}         # slot -> event the next writer must wait for
         self._stream = None
+        self._wt = None          # per-key insert table (see _write_table)
 
     # ------------------------------------------------------------------ slots
     def nbytes(self) -> int:
@@ -160,30 +163,77 @@ class UpdateSlab:
         return self.storage[dt][tile0:tile0 + tiles, slot, :]
 
     # ------------------------------------------------------------------ writes
+    def _write_table(self):
+        """Per key: (address of slot 0's first tile, bytes, tile stride) -- the slot-independent
+        part of a flame_tile_copy row (``include/flame_amd.h``)."""
+        if self._wt is None:
+            rows = []
+            for k in self.keys:
+                dt, n, base, slot_bytes, tile_stride = self.key_layout(k)
+                if slot_bytes != N.FLAME_TILE_BYTES:
+                    raise AssertionError(f"slab tile of {k} is {slot_bytes} B, the insert kernel copies "
+                                         f"{N.FLAME_TILE_BYTES} B tiles")
+                rows.append((base, n * self.storage[dt].element_size(), tile_stride))
+            self._wt = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
+        return self._wt
+
     def write(self, slot: int, weights: Dict[str, torch.Tensor], stream=None) -> None:
-        """Copy one client's update (host or device tensors) into ``slot`` on ``stream``."""
+        """Copy one client's update (host or device tensors) into ``slot`` on ``stream``.
+
+        Device sources: ONE ``flame_slab_write`` launch tiles every key into the slot (the
+        table rides in the kernel arguments).  Host sources (pinned, registered or pageable):
+        ``flame_slab_write_2d``, one pitched copy-engine transfer per key, no staging tensor.
+        """
         st = stream or torch.cuda.current_stream(self.device)
         ev = self._ready.pop(slot, None)
         if ev is not None:
             st.wait_event(ev)
-        with torch.cuda.stream(st):
-            for k in self.keys:
-                if k not in weights:
-                    raise KeyError(k)
-                dt, shape, n, tile0, tiles = self.meta[k]
-                src = weights[k]
-                if src.numel() != n:
-                    raise RuntimeError(f"{k}: {src.numel()} elements, slab expects {n}")
-                src = src.reshape(-1)
-                if src.dtype != dt:
-                    raise NotImplementedError(f"{k}: dtype {src.dtype} != slab dtype {dt}")
-                view = self.slot_view(slot, k)            # (tiles, T), row stride capacity*T
-                T = view.shape[1]
-                full = n // T
-                if full:
-                    view[:full].copy_(src[:full * T].view(full, T), non_blocking=True)
-                if n % T:
-                    view[full, :n % T].copy_(src[full * T:], non_blocking=True)
+        wt = self._write_table()
+        dev_rows, host_rows, keep = [], [], []
+        sync = False
+        for i, k in enumerate(self.keys):
+            if k not in weights:
+                raise KeyError(k)
+            dt, shape, n, tile0, tiles = self.meta[k]
+            src = weights[k]
+            if src.numel() != n:
+                raise RuntimeError(f"{k}: {src.numel()} elements, slab expects {n}")
+            if src.dtype != dt:
+                raise NotImplementedError(f"{k}: dtype {src.dtype} != slab dtype {dt}")
+            if src.is_cuda and src.device != self.device:
+                with torch.cuda.stream(st):
+                    src = src.to(self.device, non_blocking=True)
+            if not src.is_contiguous():
+                if src.is_cuda:
+                    with torch.cuda.stream(st):
+                        src = src.contiguous()
+                else:
+                    src = src.contiguous()
+                    sync = True        # a host temporary: the copy must finish before it is freed
+            if n == 0:
+                continue
+            row = (src.data_ptr(), int(wt[i, 0]) + slot * N.FLAME_TILE_BYTES, int(wt[i, 1]), int(wt[i, 2]))
+            if src.is_cuda:
+                dev_rows.append(row)
+                keep.append(src)
+            else:
+                host_rows.append(row)
+                keep.append(src)
+        L = N.lib()
+        if dev_rows:
+            tab = np.asarray(dev_rows, dtype=np.uint64).view(np.int64)
+            N.check(L.flame_slab_write(tab.ctypes.data, len(dev_rows), st.cuda_stream))
+            if st != torch.cuda.current_stream(self.device):
+                for t in keep:
+                    if t.is_cuda:
+                        t.record_stream(st)       # read on `st`: keep the caching allocator off it
+        if host_rows:
+            tab = np.asarray(host_rows, dtype=np.uint64).view(np.int64)
+            N.check(L.flame_slab_write_2d(tab.ctypes.data, len(host_rows), st.cuda_stream))
+            if sync:
+                st.synchronize()
+            else:       # the copy engine reads the host tensors after this returns: hold them
+                engine._staging.hold_on(st, [t for t in keep if not t.is_cuda])
 
     def put(self, weights: Dict[str, torch.Tensor], stream=None) -> SlotWeights:
         """Acquire a slot, write ``weights`` into it, return its tiled views."""

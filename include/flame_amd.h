@@ -329,6 +329,34 @@ int flame_host_device_pointer(void *host, void **device);
 int flame_synth_fill(int dtype, void *out, int64_t numel, uint64_t seed, uint64_t stream_id,
                      int64_t start, float scale, void *stream);
 
+/*
+ * Slab insert: the aggregator role's `self.cache[end] = tres` (mode/horizontal/syncfl/
+ * top_aggregator.py:154-156, asyncfl/top_aggregator.py:85-87) into a tiled update slab
+ * (flame_amd/slab.py).  Per entry (one state_dict key of one update): the `nbytes`
+ * contiguous bytes at `src` are cut into FLAME_TILE_BYTES tiles (one reduction chunk of
+ * every dtype, = flame_chunk_elems(dtype) x itemsize) and tile t is written to
+ * dst + t * dst_tile_stride; the last tile may be partial (bytes past nbytes untouched).
+ * dst must be 16-byte aligned, dst_tile_stride >= FLAME_TILE_BYTES and a multiple of 16
+ * when the entry spans more than one tile; src may have any alignment; nbytes == 0 entries
+ * are skipped.
+ *   flame_slab_write    : ONE kernel launch for up to 89 entries (the table travels as a
+ *                         kernel argument, no metadata H2D); src is a device pointer (or a
+ *                         mapped pinned-host pointer, read over PCIe).
+ *   flame_slab_write_2d : per entry one hipMemcpy2DAsync (pitch = dst_tile_stride) plus one
+ *                         hipMemcpyAsync for a ragged tail, on the copy engines; for host
+ *                         sources (pinned, registered or pageable).
+ * Both are asynchronous on `stream`.
+ */
+#define FLAME_TILE_BYTES 4096
+typedef struct flame_tile_copy {
+    const void *src;
+    void *dst;
+    int64_t nbytes;
+    int64_t dst_tile_stride;
+} flame_tile_copy;
+int flame_slab_write(const flame_tile_copy *table, int32_t n_entries, void *stream);
+int flame_slab_write_2d(const flame_tile_copy *table, int32_t n_entries, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

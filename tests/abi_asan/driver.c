@@ -62,6 +62,20 @@ int main(void) {
                FLAME_EINVAL, "middle");
     EXPECT_ERR(flame_hier_fedbuff(0, FLAME_HIER_SYNC, fake, 1, 1, 1, 1, fake, NULL, fake, fake, fake, fake, 0.f,
                                   NULL), FLAME_EINVAL, "SYNC");
+    {   /* slab inserts: table checks run before any HIP call */
+        flame_tile_copy tc[3] = {{fake, fake, 0, 0}, {fake, (char *)fake + 8, 100, 4096}, {NULL, fake, 5, 4096}};
+        EXPECT_ERR(flame_slab_write(NULL, 1, NULL), FLAME_EINVAL, "NULL table");
+        EXPECT_ERR(flame_slab_write(tc, -1, NULL), FLAME_EINVAL, "");
+        EXPECT(flame_slab_write(tc, 1, NULL) == FLAME_OK, "slab_write: empty entries launch nothing");
+        EXPECT_ERR(flame_slab_write(tc, 2, NULL), FLAME_EINVAL, "aligned");
+        EXPECT_ERR(flame_slab_write_2d(tc + 2, 1, NULL), FLAME_EINVAL, "NULL pointer");
+        tc[1].dst = fake;
+        tc[1].nbytes = 3 * FLAME_TILE_BYTES;
+        tc[1].dst_tile_stride = 100;
+        EXPECT_ERR(flame_slab_write_2d(tc, 2, NULL), FLAME_EINVAL, "dst_tile_stride");
+        tc[1].nbytes = -1;
+        EXPECT_ERR(flame_slab_write(tc, 2, NULL), FLAME_EINVAL, "nbytes");
+    }
 
     uint64_t blk[64];
     memset(blk, 0, sizeof blk);

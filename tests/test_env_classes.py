@@ -44,3 +44,40 @@ def test_regularizers_with_and_without_flame():
     assert alone["fedprox_term"] == with_flame["fedprox_term"]
     assert alone["fedgft_bias"] == with_flame["fedgft_bias"]
     assert alone["default_term"] == with_flame["default_term"]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_install_into_flame_provider():
+    """``flame_amd.optimizers.install()`` with no argument re-registers every key of flame's own
+    provider (optimizers.py:39-48, closed enum config.py:55-70), so a role's
+    ``optimizer_provider.get(config.optimizer.sort, **config.optimizer.kwargs)``
+    (syncfl/top_aggregator.py:97-99) on a job's optimizer block parsed by flame's pydantic
+    ``Optimizer`` model (config.py:121-123, the type of ``Config.optimizer``) yields the drop-in with
+    the job's kwargs."""
+    shim = os.path.join(ROOT, "tests", "golden", "_shim")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    env["PYTHONPATH"] = os.pathsep.join(p for p in (shim, REF, env.get("PYTHONPATH", "")) if p)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "install_probe.py"), ROOT], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    keys = {"fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "fedprox", "feddyn", "scaffold", "fedgft"}
+    assert set(out["before"]) == keys and set(out["after"]) == keys
+    for k in keys:
+        assert out["before"][k].startswith("flame.optimizer."), (k, out["before"][k])
+        assert out["after"][k]["cls"].startswith("flame_amd.optimizer."), (k, out["after"][k])
+        assert out["after"][k]["same_as_drop_in"], k
+    assert out["returned_flame_provider"] is True
+    assert out["unknown_key"] == "ValueError:fedsgd"
+    c = out["config"]
+    assert c["fedyogi"]["cls"] == "flame_amd.optimizer.fedyogi.FedYogi" and c["fedyogi"]["sort"] == "fedyogi"
+    assert c["fedyogi"]["hyper"] == [0.85, 0.995, 0.02, 0.002]
+    assert c["fedadam"]["cls"] == "flame_amd.optimizer.fedadam.FedAdam"
+    assert c["fedadam"]["hyper"] == [0.9, 0.99, 0.01, 0.001]
+    assert c["fedbuff"]["cls"] == "flame_amd.optimizer.fedbuff.FedBuff"
+    assert c["fedavg_default"]["cls"] == "flame_amd.optimizer.fedavg.FedAvg"
+    assert c["fedavg_default"]["sort"] == "fedavg"
+    for name in c:      # flame's own regularizer class when flame is importable; empty round -> None
+        assert c[name]["regularizer"].startswith("flame."), (name, c[name])
+        assert c[name]["empty_do"] == "None", (name, c[name])
+    assert out["bad_sort"] == "ValidationError"

@@ -1229,10 +1229,13 @@ def test_sharded_fedadam_two_ranks_one_gpu():
     assert res == {0: True, 1: True}, res
 
 
-def test_c4_full_size_fedadam_sampled_columns():
-    """Config 4 at full size (FedAdam, 1024 x 25M fp32 in a tiled slab, round 1 passthrough then
-    an adaptive round): cur / m / v at 65,536 random elements and 7 whole chunks vs the oracle FedOPT run on
-    those columns (round 1 bitwise; the adaptive round within the §8(c) contract)."""
+@pytest.mark.parametrize("variant", ["fedadam", "fedyogi", "fedadagrad"])
+def test_c4_full_size_sampled_columns(variant):
+    """Config 4 at full size (FedAdam / FedYogi / FedAdaGrad, 1024 x 25M fp32 in a tiled slab, round 1
+    passthrough then an adaptive round; fedadam.py:33-35, fedyogi.py:34-36, fedadagrad.py:33-35,
+    fedopt.py:102-129): cur / m / v at 65,536 random elements and 7 whole chunks vs the oracle FedOPT
+    run on those columns (round 1 bitwise; the adaptive round within the §8(c) contract, its
+    FedAvg part bitwise)."""
     from flame_amd import synth, engine
     from flame_amd.slab import UpdateSlab
     O = _oracle()
@@ -1253,8 +1256,8 @@ def test_c4_full_size_fedadam_sampled_columns():
     it = torch.from_numpy(idx).to(DEV)
     cols = slab.storage[torch.float32][it // T, :, it % T].t().cpu()        # [n, 65538]
     base_cols = base[it].cpu()
-    amd = make_amd("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
-    ora = O.OracleFedOPT("fedadam", beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    amd = make_amd(variant, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
+    ora = O.OracleFedOPT(variant, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3)
     wa, wo = {"model": base}, {"model": base_cols.clone()}
     for r in range(2):
         counts = synth.counts(3 + r, n)
@@ -1270,10 +1273,12 @@ def test_c4_full_size_fedadam_sampled_columns():
         if r == 0:
             S.assert_bitwise("c4/r0/cur", got, wo)
         else:
-            S.assert_close_fedopt("c4/r1/cur", got, wo)
-            S.assert_close_fedopt("c4/r1/m", {"model": amd.m_t["model"][it].cpu()}, {"model": ora.m_t["model"]})
-            S.assert_close_fedopt("c4/r1/v", {"model": amd.v_t["model"][it].cpu()}, {"model": ora.v_t["model"]})
-            S.assert_bitwise("c4/r1/avg", {"model": amd.agg_weights["model"][it].cpu()},
+            S.assert_close_fedopt(f"c4/{variant}/r1/cur", got, wo)
+            S.assert_close_fedopt(f"c4/{variant}/r1/m", {"model": amd.m_t["model"][it].cpu()},
+                                  {"model": ora.m_t["model"]})
+            S.assert_close_fedopt(f"c4/{variant}/r1/v", {"model": amd.v_t["model"][it].cpu()},
+                                  {"model": ora.v_t["model"]})
+            S.assert_bitwise(f"c4/{variant}/r1/avg", {"model": amd.agg_weights["model"][it].cpu()},
                              {"model": ora.agg_weights["model"]})
     del ws, slab, wa, amd
     torch.cuda.empty_cache()
