@@ -1349,7 +1349,13 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 // workgroup copies kSlabTPW tiles, every lane 16 B of each (all its loads issued before its
 // stores); the entry table rides in the kernel arguments, so an insert is ONE launch and no
 // H2D of metadata.
-constexpr int kSlabTPW = 4;
+#ifndef FLAME_SLAB_TPW
+#define FLAME_SLAB_TPW 2   // slab insert: 4 KiB tiles per workgroup (1-8 within noise, profiles/r03b_slab_sweep.log)
+#endif
+#ifndef FLAME_SLAB_ST
+#define FLAME_SLAB_ST 0    // slab insert: store policy (encoding of FLAME_ST_NT; plain stores measured best)
+#endif
+constexpr int kSlabTPW = FLAME_SLAB_TPW;
 struct SlabEntry { const uint8_t* src; uint8_t* dst; int64_t nbytes; int64_t stride; int64_t tile_begin; };
 constexpr int kSlabMaxEntries = static_cast<int>(sizeof(ArgMeta) / sizeof(SlabEntry));
 static_assert(FLAME_TILE_BYTES == kBlock * 16, "a slab tile is one 16-byte vector per lane");
@@ -1389,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, 
     }
 #pragma unroll
     for (int j = 0; j < kSlabTPW; ++j)
-        if (kind[j] == 1) st_pol<1>(dp[j], v[j]);
+        if (kind[j] == 1) st_pol<FLAME_SLAB_ST>(dp[j], v[j]);
 }
 
 constexpr int kClientUnroll = FLAME_CU;

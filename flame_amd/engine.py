@@ -994,8 +994,8 @@ def _accumulate_promoted(agg: dict, k, entries, device) -> None:
 
 def tmp_of(v: torch.Tensor, rate: float, device, shape=None) -> torch.Tensor:
     """``(v * rate).to(v.dtype)`` (fedavg.py:93-102) as a new device tensor.  Kernel dtypes:
-    one init-first launch.  bool / uint8 / int8 / int16: ``v * rate`` is fp32 in torch
-    (the integral tensor and the rate both cast to fp32), formed by the fp32 kernel, then
+    one init-first launch.  bool / uint8 / int8 / int16: ``v * rate`` is in torch's default
+    dtype (fp32: the integral tensor and the rate both cast to it), formed by that dtype's kernel, then
     cast to v's dtype on the device (bool: != 0; integers: truncation -- in range, as
     ``|v * rate| <= |v|`` for the callers' rates <= 1).  ``shape``: the key's model shape
     (``v`` may be a tiled slab view)."""
@@ -1006,8 +1006,11 @@ def tmp_of(v: torch.Tensor, rate: float, device, shape=None) -> torch.Tensor:
         return tmp
     if v.dtype not in NARROW:
         dtype_code(v.dtype)          # raises: unsupported (complex, fp8, ...)
-    vf = v.to(device).to(torch.float32)
-    tf = torch.empty(shape, dtype=torch.float32, device=device)
+    # torch computes an integral tensor times a Python float in the DEFAULT dtype (fp32 unless
+    # torch.set_default_dtype changed it; fp64 then uses the rate unrounded)
+    ft = torch.get_default_dtype()
+    vf = v.to(device).to(ft)
+    tf = torch.empty(shape, dtype=ft, device=device)
     reduce_([tf], None, [[vf]], [rate], init_first=True)
     return tf.to(v.dtype)
 

@@ -43,7 +43,8 @@ class DeferredAggregate(collections.abc.Mapping):
         # the optimizer (weakly: it holds this object; a cycle would keep queued slab slots
         # alive until the cyclic GC): its metric_collector sees the flush's launches
         self._owner = weakref.ref(owner) if owner is not None else None
-        self._slabs_ok = []        # slabs whose slots passed _queue's key / dtype checks
+        self._slabs_ok = weakref.WeakSet()   # slabs whose slots passed _queue's key / dtype checks (weak: a
+                                             # replaced cache must not keep its multi-GB slab alive)
         self._keys = list(weights.keys())
         self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
@@ -73,7 +74,7 @@ class DeferredAggregate(collections.abc.Mapping):
                 if dt != self._meta[k][1]:
                     engine._check_cast(self._meta[k][1], dt)
             if whole_slot:
-                self._slabs_ok.append(slab)
+                self._slabs_ok.add(slab)
         # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
         # before do() returns: the sender may rewrite the segment while it waits in the queue
         if shm_lease.active():

@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import collections
 import math
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -224,6 +225,22 @@ def _slice(t: torch.Tensor, lo: int, hi: int, numel: int) -> torch.Tensor:
 
 
 # -------------------------------------------------------------------- collectives
+# one coalesced group per wave (RCCL: a single grouped launch); False = one async collective
+# per piece through the public API only (FLAME_AMD_COALESCE=0)
+COALESCE = os.environ.get("FLAME_AMD_COALESCE", "1") != "0"
+# collectives issued per path ("coalesced" groups, "async" single gathers, "host_staged"), for tests
+GATHER_STATS = collections.Counter()
+
+
+def _coalescing_manager():
+    """torch's private ``_coalescing_manager`` context factory, or None if this torch lacks it."""
+    try:
+        from torch.distributed.distributed_c10d import _coalescing_manager as cm
+    except ImportError:
+        return None
+    return cm
+
+
 class _Comm:
     """The process group (none at world 1) and the in-place all-gathers of one call."""
 
@@ -234,33 +251,46 @@ class _Comm:
         self.world = dist.get_world_size(group) if self.dist else 1
         self.rank = dist.get_rank(group) if self.dist else 0
         self.backend = dist.get_backend(group) if self.dist else None
+        self.coalesce = COALESCE
         self._works = []
 
     def all_gather_inplace(self, pairs) -> None:
         """``pairs``: [(piece, owned)] with ``owned`` this rank's range inside ``piece``.
-        RCCL: async, in place (NCCL's in-place all-gather, ``sendbuff == recvbuff + rank *
-        count``), one coalesced group per call; gloo (CPU tests): synchronous."""
+
+        One body for RCCL and for gloo on CPU tensors (the world 2 / 3 / 8 CPU tests run it):
+        async, in place (NCCL's in-place all-gather, ``sendbuff == recvbuff + rank * count``),
+        the call's pieces of one dtype in one coalesced group (``_coalescing_manager``; without it -- a torch
+        that lacks the private helper, or ``coalesce=False`` -- one async public
+        ``all_gather_into_tensor`` per piece).  Only gloo with CUDA tensors (tests where ranks
+        share one GPU; gloo has no device all-gather) stages through the host synchronously."""
         if not pairs or self.dist is None:
             return
         d = self.dist
-        if self.backend == "gloo":
+        if self.backend == "gloo" and pairs[0][0].is_cuda:
             for piece, owned in pairs:
-                if piece.is_cuda:   # ranks sharing a GPU in tests: host staging
-                    host = torch.empty(piece.numel(), dtype=piece.dtype)
-                    d.all_gather_into_tensor(host, owned.cpu(), group=self.group)
-                    piece.copy_(host)
-                else:
-                    d.all_gather_into_tensor(piece, owned.clone(), group=self.group)
+                host = torch.empty(piece.numel(), dtype=piece.dtype)
+                d.all_gather_into_tensor(host, owned.cpu(), group=self.group)
+                piece.copy_(host)
+            GATHER_STATS["host_staged"] += len(pairs)
             return
-        if len(pairs) == 1:
-            piece, owned = pairs[0]
-            self._works.append(d.all_gather_into_tensor(piece, owned, group=self.group, async_op=True))
-            return
-        from torch.distributed.distributed_c10d import _coalescing_manager
-        with _coalescing_manager(group=self.group, async_ops=True) as cm:
-            for piece, owned in pairs:
-                d.all_gather_into_tensor(piece, owned, group=self.group)
-        self._works.append(cm)
+        cm_factory = _coalescing_manager() if self.coalesce else None
+        by_dtype = collections.OrderedDict()
+        for piece, owned in pairs:
+            by_dtype.setdefault(piece.dtype, []).append((piece, owned))
+        for group in by_dtype.values():
+            # one group per dtype: gloo's coalesced all-gather flattens a group into ONE buffer of
+            # its first tensor's dtype (a bf16 + fp32 group came back with the fp32 values rounded
+            # to bf16); RCCL would take mixed dtypes, the per-dtype split costs it nothing measurable
+            if cm_factory is None or len(group) == 1:
+                for piece, owned in group:
+                    self._works.append(d.all_gather_into_tensor(piece, owned, group=self.group, async_op=True))
+                GATHER_STATS["async"] += len(group)
+                continue
+            with cm_factory(group=self.group, async_ops=True) as cm:
+                for piece, owned in group:
+                    d.all_gather_into_tensor(piece, owned, group=self.group)
+            self._works.append(cm)
+            GATHER_STATS["coalesced"] += 1
 
     def wait(self) -> None:
         """Order the launch stream after every gather issued so far (host does not block)."""
@@ -581,7 +611,8 @@ class ShardedOptimizer:
             missing = [n for n in plan.names if n in res and n not in gat.target]
             if missing:      # not produced through the allocator: gathered after the fact
                 gat.collect(res, local, missing)
-                gat.issued.clear()
+                # re-issue only the waves holding such names (the others went out behind their launches)
+                gat.issued -= {plan.by_name[n].wave for n in missing}
             return self._remember(res, gat.finish())
         if self.waves:
             # any other stateless optimizer (e.g. the CPU oracle in tests): one do() per wave on
@@ -762,8 +793,10 @@ __all__ = ["ShardPlan", "ShardedOptimizer", "ShardedHierarchy", "ALIGN_ELEMS", "
 
 
 def plan_for(model, group=None, **kw) -> ShardPlan:
-    """The plan a ShardedOptimizer / ShardedHierarchy over ``group`` would use for ``model``
-    (e.g. for ``DeviceUpdateCache(shard=...)`` before the optimizer has seen a model)."""
+    """The plan a ShardedOptimizer over ``group`` (default ``fracs`` / ``align``) would use for
+    ``model`` (e.g. for ``DeviceUpdateCache(shard=...)`` before the optimizer has seen a model).
+    Not a ShardedHierarchy's plan (other wave fractions, a last wave sized by the kernel's
+    residency): use ``hier.plan`` there."""
     c = _Comm(group)
     return ShardPlan(model, c.world, c.rank, **kw)
 

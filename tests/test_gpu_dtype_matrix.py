@@ -214,3 +214,27 @@ def test_fedopt_with_narrow_buffers_vs_oracle(sort):
                 got[k] = got[k].masked_fill(nan, 0)
         exp = {k: (v.masked_fill(torch.isnan(v), 0) if v.is_floating_point() else v) for k, v in wo.items()}
         S.assert_close_fedopt(f"{sort} r{rnd}", got, exp, elementwise=(rnd < 2))
+
+
+def test_narrow_buffers_under_float64_default_dtype():
+    """torch.set_default_dtype(torch.float64): the reference's ``(v * rate)`` on a bool / uint8 /
+    int8 / int16 buffer is then fp64 (rate unrounded) -- the drop-in's tmp follows the default
+    dtype (engine.tmp_of); FedAvg bitwise vs torch CPU, the default restored after."""
+    old = torch.get_default_dtype()
+    g = torch.Generator().manual_seed(31)
+    try:
+        torch.set_default_dtype(torch.float64)
+        for dt in (torch.bool, torch.uint8, torch.int8, torch.int16):
+            acc = _rand(g, dt, 4099, 1.0)
+            vs = [_rand(g, dt, 4099, 1e-1) for _ in range(3)]
+            counts = [5, 11, 17]
+            exp = acc.clone()
+            for v, c in zip(vs, counts):
+                _reference(exp, v, c / sum(counts))
+            cache = S.SortedCache()
+            for i, (v, c) in enumerate(zip(vs, counts)):
+                cache[f"{i}"] = S.TR({"x": v.to(DEV)}, c)
+            got = _drop_in("fedavg").do({"x": acc.to(DEV)}, cache, total=sum(counts))
+            assert got["x"].dtype == dt and torch.equal(got["x"].cpu(), exp), dt
+    finally:
+        torch.set_default_dtype(old)

@@ -1,5 +1,9 @@
 """Parameter sharding (flame_amd.shard) over world-size-2 gloo groups on CPU.
 
+The all-gathers run the same code RCCL runs (``_Comm.all_gather_inplace``: async, in place,
+one coalesced group per wave; gloo accepts it for CPU tensors) -- the workers check that no
+host-staged gather happened.
+
 The plan / slicing / replay / in-place all-gather logic of ShardedOptimizer and
 ShardedHierarchy must reproduce the single-process result bitwise.  The per-rank
 arithmetic is the oracle here (no GPU); the product runs the HIP drop-ins per rank
@@ -163,6 +167,11 @@ def _fedavg_worker(rank, world, port, q):
             O.OracleFedAvg().do(ref, cb, total=sum(counts))
             ok = ok and all(_eq(out[k], ref[k]) for k in ref)
             base = ref
+        # the gathers ran the body RCCL runs (async, in place; coalesced per wave unless disabled)
+        st = shard.GATHER_STATS
+        ok = ok and st["host_staged"] == 0 and st["coalesced"] + st["async"] > 0
+        ok = ok and (st["coalesced"] > 0 if shard.COALESCE and world == 2 else True)
+        ok = ok and (st["coalesced"] == 0 if not shard.COALESCE else True)
         # None results (fedavg.py:76-77)
         ok = ok and opt.do({k: v.clone() for k, v in base.items()}, S.SortedCache(), total=3) is None
         c = S.SortedCache()
@@ -177,6 +186,16 @@ def _fedavg_worker(rank, world, port, q):
 
 def test_sharded_fedavg_waves_gloo_world2():
     _run(_fedavg_worker)
+
+
+def _fedavg_worker_public(rank, world, port, q):
+    shard.COALESCE = False        # FLAME_AMD_COALESCE=0: one public async all-gather per piece
+    _fedavg_worker(rank, world, port, q)
+
+
+def test_sharded_fedavg_waves_gloo_world2_public_collectives():
+    """The same rounds without torch's private coalescing helper (the fallback path)."""
+    _run(_fedavg_worker_public)
 
 
 def _opt_worker(rank, world, port, q):
@@ -229,6 +248,8 @@ def _opt_worker(rank, world, port, q):
         out = fs.scale_add_agg_weights(ms, agg_s, 4)
         f1.scale_add_agg_weights(mr, agg_r, 4)
         ok = ok and out is ms and all(_eq(ms[k], mr[k]) for k in mr)
+        st = shard.GATHER_STATS
+        ok = ok and st["host_staged"] == 0 and st["coalesced"] + st["async"] > 0
         q.put((rank, bool(ok)))
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -292,6 +313,7 @@ def _hier_worker(rank, world, port, q):
                 specs.append((mids[j], cache, sum(mm["counts"])))
             out, _ = hs.sync_round(specs, top)
             ok = ok and out is top and all(_eq(top[k], fs.weights(f"r{r}/top")[k]) for k in top)
+            ok = ok and shard.GATHER_STATS["host_staged"] == 0
             # keys whose middle weights this rank updated in full (the tails) match the reference
             for j in range(3):
                 exp = hs.plan.slice_update(fs.weights(f"r{r}/m{j}/new"))
