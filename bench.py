@@ -92,6 +92,9 @@ def parse():
                     help="params per GPU (default 25,000,000; hier_fedbuff 125M/8 = 15,625,000)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: do not pipeline the all-gather")
+    ap.add_argument("--hier-arrivals", default="batched", choices=["batched", "per-do"],
+                    help="hier_fedbuff fused: each middle's round of arrivals in ONE FedBuff.do_arrivals call "
+                         "(batched) or one do() per arrival as the async middle role issues them (per-do)")
     ap.add_argument("--hier-wave-quantum", default="on", choices=["on", "off"],
                     help="sharded hierarchy: size the last wave to whole rounds of resident workgroups")
     ap.add_argument("--shard-fracs", default=None,
@@ -715,6 +718,29 @@ def bench_sharded(args, world, rank, dev, n, P):
         dist.destroy_process_group()
 
 
+def _middle_arrivals(args, M, C, client_w, stale, rnd):
+    """The middles' arrivals of one round (asyncfl/middle_aggregator.py:164-203): each arrival
+    is a TrainResult (count 1, version rnd - staleness) the middle role builds from its
+    message; ``--hier-arrivals batched`` hands a middle's round to ONE
+    ``FedBuff.do_arrivals`` call, ``per-do`` calls ``do()`` per arrival with a one-entry
+    cache as the role does.  Returns the middles' aggregates."""
+    def batched(mid_opts):
+        return [mid_opts[m].do_arrivals(None, [TR(client_w[i], 1, rnd - stale[i]) for i in range(m * C, (m + 1) * C)],
+                                        version=rnd) for m in range(M)]
+
+    def per_do(mid_opts):
+        aggs = [None] * M
+        for m in range(M):
+            opt = mid_opts[m]
+            for t in range(C):
+                i = m * C + t
+                cache = Cache()
+                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
+                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        return aggs
+    return batched if args.hier_arrivals == "batched" else per_do
+
+
 def bench_hier_sharded(args, world, rank, dev, M, C, P):
     """Config 5 as named (hierarchical FedBuff parameter-sharded over the node's GPUs with an
     RCCL all-gather) through the product's ShardedHierarchy: the model has P x world bf16
@@ -754,15 +780,10 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
     mid_opts = [hier.middle_optimizer() for _ in range(M)]
     torch.cuda.synchronize()
 
+    middle_arrivals = _middle_arrivals(args, M, C, client_w, stale, rnd)
+
     def step_fused():
-        aggs = [None] * M
-        for m in range(M):
-            opt = mid_opts[m]
-            for t in range(C):        # one arrival per do(), as the middle role hands them over
-                i = m * C + t
-                cache = Cache()
-                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
-                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        aggs = middle_arrivals(mid_opts)
         hier.round([(mids[m], aggs[m], C, rnd - (m % 2)) for m in range(M)], None, version=rnd,
                    top_weights={"model": gw}, top_goal=M, update_middle_weights=not fetched)
 
@@ -800,7 +821,7 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                                    f"bf16 params, parameter-sharded over {world} rank(s) "
                                    f"(flame_amd.shard.ShardedHierarchy, {plan.owned_elements()} params per rank)",
                        "middles": args.hier_mode, "middle_weights": args.hier_middles,
-                       "middle_layout": args.hier_mid_layout,
+                       "middle_layout": args.hier_mid_layout, "arrivals": args.hier_arrivals,
                        "params_per_gpu": P, "global_params": G, "parallelism": f"param-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "traffic": None,
@@ -901,6 +922,7 @@ def bench_hier(args, world, rank, dev):
     rnd = 10
     mid_opts = [optimizer_provider.get("fedbuff") for _ in range(M)]
     top_opt = optimizer_provider.get("fedbuff")
+    middle_arrivals = _middle_arrivals(args, M, C, client_w, stale, rnd)
     torch.cuda.synchronize()
 
     def step_group():
@@ -947,14 +969,7 @@ def bench_hier(args, world, rank, dev):
         # every middle's arrivals queue (DeferredAggregate); ONE launch then reduces each
         # middle, applies its scale_add, feeds its delta to the top FedBuff and applies the
         # top's scale_add -- the middle aggregates and deltas stay in registers
-        aggs = [None] * M
-        for m in range(M):
-            opt = mid_opts[m]
-            for t in range(C):
-                i = m * C + t
-                cache = Cache()
-                cache[f"{i:05d}"] = TR(client_w[i], 1, rnd - stale[i])
-                aggs[m] = opt.do(aggs[m], cache, total=1, version=rnd)
+        aggs = middle_arrivals(mid_opts)
         fetched = args.hier_middles == "fetched"
         hierarchy_round([({"model": gw_fetched} if fetched else mid_w[m], aggs[m], C, rnd - (m % 2))
                          for m in range(M)], None, version=rnd, top_weights={"model": gw}, top_goal=M,
@@ -1027,7 +1042,8 @@ def bench_hier(args, world, rank, dev):
             "host_issue_ms_per_step": ISSUE_S / args.steps * 1e3,
             "dtype": "bf16", "config": {"workload": f"{'hier_fedavg' if sync else 'hier_fedbuff'}: {M} middles x {C} "
                                                     f"clients x {P} bf16 per GPU",
-                                        "middles": args.hier_mode, "middle_weights": args.hier_middles},
+                                        "middles": args.hier_mode, "middle_weights": args.hier_middles,
+                                        "arrivals": args.hier_arrivals},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,
                          "kernel": names[0]},

@@ -1384,10 +1384,29 @@ __global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, 
         if (off >= e.nbytes) continue;
         dp[j] = e.dst + t * e.stride + lane * 16;
         const uint8_t* sp = e.src + off;
-        if (off + 16 <= e.nbytes && (reinterpret_cast<uintptr_t>(sp) & 15) == 0) {
+        const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(sp) & 15);   // uniform per entry
+        if (off + 16 <= e.nbytes && sh == 0) {
             v[j] = ld_nt(sp);
             kind[j] = 1;
-        } else {                                  // ragged tail or a misaligned source view
+        } else if (off + 16 <= e.nbytes) {
+            // misaligned source (e.g. tensor bytes inside a channel payload): two aligned loads
+            // and a byte funnel shift.  The second 16-byte block starts before the entry's last
+            // byte, so it never leaves that byte's (4 KiB-aligned) page.
+            const uint8_t* ab = sp - sh;
+            const V16 lo = ld_nt(ab), hi = ld_nt(ab + 16);
+            const uint32_t w[8] = {lo.w[0], lo.w[1], lo.w[2], lo.w[3], hi.w[0], hi.w[1], hi.w[2], hi.w[3]};
+            const unsigned r = static_cast<unsigned>(sh & 3);
+#define FLAME_SLAB_FUNNEL(Q) \
+    for (int i = 0; i < 4; ++i) v[j].w[i] = __builtin_amdgcn_alignbyte(w[i + (Q) + 1], w[i + (Q)], r);
+            switch (sh >> 2) {
+            case 0: FLAME_SLAB_FUNNEL(0) break;
+            case 1: FLAME_SLAB_FUNNEL(1) break;
+            case 2: FLAME_SLAB_FUNNEL(2) break;
+            default: FLAME_SLAB_FUNNEL(3) break;
+            }
+#undef FLAME_SLAB_FUNNEL
+            kind[j] = 1;
+        } else {                                  // ragged tail
             const int nb = static_cast<int>(e.nbytes - off < 16 ? e.nbytes - off : 16);
             for (int b = 0; b < nb; ++b) st1(dp[j] + b, ld1(sp + b));
             kind[j] = 2;

@@ -898,6 +898,14 @@ def slab_rows(ws, keys, numels, dtypes, device):
         if ranges is None and len(w) != nk:
             return None
     slots = np.fromiter((w.slot for w in ws), dtype=np.uint64, count=len(ws))
+    return slot_rows(slab, ranges, slots, keys, numels, dtypes, device)
+
+
+def slot_rows(slab, ranges, slots, keys, numels, dtypes, device):
+    """:func:`slab_rows` from slot numbers already known (``slots``: uint64, client order) of
+    ``slab`` (whole slots with ``ranges`` None, or one shared ``ranges`` table)."""
+    if slab.device != device:
+        return None
     rows = {}
     for k in keys:
         if ranges is not None:

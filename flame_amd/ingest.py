@@ -37,6 +37,10 @@ from typing import Any, Dict
 
 import torch
 
+# torch.frombuffer warns on a read-only buffer (a received `bytes` payload); the views are only
+# read, so that one warning is silenced (once, instead of a catch_warnings block per tensor)
+warnings.filterwarnings("ignore", message="The given buffer is not writable", category=UserWarning)
+
 # ------------------------------------------------------------------ legacy storage stream
 _STORAGE_DTYPES = {
     "FloatStorage": torch.float32, "DoubleStorage": torch.float64, "HalfStorage": torch.float16,
@@ -58,9 +62,7 @@ class _StorageRef:
     def tensor(self) -> torch.Tensor:
         if self.numel == 0:
             return torch.empty(0, dtype=self.dtype)
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore")  # read-only payload buffer: views are only read
-            return torch.frombuffer(self.buf, dtype=self.dtype, count=self.numel, offset=self.offset)
+        return torch.frombuffer(self.buf, dtype=self.dtype, count=self.numel, offset=self.offset)
 
 
 class _PersistentStorage:
@@ -75,6 +77,9 @@ def _rebuild_tensor_v2(storage, storage_offset, size, stride, requires_grad=Fals
         raise pickle.UnpicklingError("tensor rebuild without a storage")
     base = storage.tensor()
     t = base.as_strided(tuple(size), tuple(stride), storage_offset)
+    # the payload buffer the view reads: UpdateSlab.write copies one update's tensors that
+    # share a payload with ONE host->device transfer (flame_amd/slab.py)
+    t._flame_payload = storage.buf
     return t
 
 
@@ -279,6 +284,18 @@ class PayloadDecoder:
             _sysinfo, q = self.load(q)
             if len(_STORAGE_HEADERS) < 8:
                 _STORAGE_HEADERS.append(bytes(self.mv[span.start:q]))
+        # the storage record (object pickle + key-list pickle + numel) of a given tensor repeats
+        # byte for byte in every payload of the same model: parse results are kept by their
+        # exact bytes (the VM is a pure function of them), grouped by record length
+        for n_rec, seen in _STORAGE_RECORDS.items():
+            hit = seen.get(bytes(self.mv[q:q + n_rec]))
+            if hit is not None:
+                dtype, numel, nbytes = hit
+                q += n_rec
+                if q + nbytes > span.start + span.n:
+                    raise pickle.UnpicklingError("storage runs past its bytes")
+                return _StorageRef(self.buf, q, numel, dtype)
+        rec0 = q
         found = []
 
         def pload(pid):
@@ -299,10 +316,14 @@ class PayloadDecoder:
         nbytes = numel * torch.empty(0, dtype=obj.dtype).element_size()
         if q + nbytes > span.start + span.n:
             raise pickle.UnpicklingError("storage runs past its bytes")
+        seen = _STORAGE_RECORDS.setdefault(q - rec0, {})
+        if len(seen) < 4096:
+            seen[bytes(self.mv[rec0:q])] = (obj.dtype, numel, nbytes)
         return _StorageRef(self.buf, q, numel, obj.dtype)
 
 
 _STORAGE_HEADERS = []   # validated legacy-stream headers (bytes)
+_STORAGE_RECORDS = {}   # record length -> {record bytes: (dtype, numel, nbytes)} (see _storage_from_span)
 
 
 class _Span:

@@ -22,6 +22,7 @@ operation sequence (bit-identical), the moment anything reads the aggregate
 import collections
 import collections.abc
 import copy
+import itertools
 import logging
 import math
 import weakref
@@ -49,6 +50,11 @@ class DeferredAggregate(collections.abc.Mapping):
         self._meta = {k: (engine.logical_shape(weights, k), engine.weight_dtype(weights, k)) for k in self._keys}
         self._data = None          # dict of device tensors once materialised
         self._pending = []         # [(weights, rate)] in arrival order
+        # while every queued arrival is a whole slot of ONE slab: that slab and the slots in
+        # queue order (pointer rows then come from slot numbers, no per-arrival pass); None =
+        # nothing queued, False = mixed
+        self._pend_slab = None
+        self._pend_slots = []
         self._max_pending = max_pending
         self._max_bytes = max_pending_bytes
         self._held = 0             # bytes of queued arrivals that own their memory (not slab slots)
@@ -57,6 +63,8 @@ class DeferredAggregate(collections.abc.Mapping):
 
     def _queue(self, entries):
         held = 0
+        last_ok = None                # the slab whose slots the previous entry was checked against
+        ps, slots = self._pend_slab, []   # committed with the entries (a KeyError leaves both as they were)
         for w, _ in entries:
             slab = getattr(w, "slab", None)
             if slab is None:
@@ -64,22 +72,33 @@ class DeferredAggregate(collections.abc.Mapping):
                 # in); slab slots are preallocated, anything else counts against max_pending_bytes
                 held += self._arrival_bytes
             whole_slot = slab is not None and getattr(w, "ranges", None) is None
-            if whole_slot and slab in self._slabs_ok:
-                continue              # the slots of one slab share keys and dtypes: checked once
-            for k in w.keys():
-                if k not in self._meta:
-                    raise KeyError(k)
-                # `agg[k] += tmp` (fedbuff.py:157) raises from the do() that brings it
-                dt = engine.weight_dtype(w, k)
-                if dt != self._meta[k][1]:
-                    engine._check_cast(self._meta[k][1], dt)
+            if not (whole_slot and (slab is last_ok or slab in self._slabs_ok)):
+                for k in w.keys():    # (the slots of one slab share keys and dtypes: checked once)
+                    if k not in self._meta:
+                        raise KeyError(k)
+                    # `agg[k] += tmp` (fedbuff.py:157) raises from the do() that brings it
+                    dt = engine.weight_dtype(w, k)
+                    if dt != self._meta[k][1]:
+                        engine._check_cast(self._meta[k][1], dt)
+                if whole_slot:
+                    self._slabs_ok.add(slab)
             if whole_slot:
-                self._slabs_ok.add(slab)
+                last_ok = slab
+                if ps is None or ps is slab:
+                    ps = slab
+                    slots.append(w.slot)
+                else:
+                    ps = False
+            else:
+                ps = False
         # an arrival decoded in place from a sender's shared-memory segment is copied to HBM
         # before do() returns: the sender may rewrite the segment while it waits in the queue
         if shm_lease.active():
             entries = [(_own_shm_views(w), r) for w, r in entries]
         self._pending.extend(entries)
+        self._pend_slab = ps
+        if ps:
+            self._pend_slots.extend(slots)
         self._held += held
         if len(self._pending) >= self._max_pending or (self._max_bytes is not None and self._held > self._max_bytes):
             self.flush()
@@ -109,7 +128,12 @@ class DeferredAggregate(collections.abc.Mapping):
                            [r for _, r in self._pending], init_first=True)
         else:
             engine.accumulate(self._data, self._pending)
+        self._clear_pending()
+
+    def _clear_pending(self):
         self._pending = []
+        self._pend_slab = None
+        self._pend_slots = []
         self._held = 0
 
     def __getitem__(self, k):
@@ -183,6 +207,44 @@ class FedBuff(AbstractOptimizer):
                 entries.append((tres.weights, rate))
         finally:
             self._apply(entries)  # what the reference had applied before any exception
+        return self.agg_goal_weights
+
+    def do_arrivals(self, agg_goal_weights, arrivals, *, version: int = 0):
+        """Several arrivals in ONE call -- the batched form of the async roles' loop.
+
+        Identical to running, for each ``TrainResult`` in ``arrivals`` (arrival order), what
+        ``asyncfl/middle_aggregator.py:190-203`` / ``asyncfl/top_aggregator.py:85-92`` do per
+        received message: ``cache[end] = tres; agg = self.do(agg, cache, total=tres.count,
+        version=version)``.  Same staleness rate per arrival (``1 / math.sqrt(1 + version -
+        tres.version)``, fedbuff.py:94-96 -- numpy's IEEE sqrt and division give the same
+        doubles), the same None-start (the first arrival starts a None aggregate, the rest add
+        to it), and the same error at the same arrival: the arrivals before a stale-version one
+        are applied, then ``ZeroDivisionError`` / ``ValueError`` is raised as by ``math``.
+        Arrivals with ``count <= 0`` are refused (``ValueError``): the roles never hand them to
+        ``do()`` (``if weights is not None and count > 0``, :196).  Returns the aggregate (a
+        :class:`DeferredAggregate` with ``defer=True``: the arrivals join its queue at once).
+        """
+        arrivals = list(arrivals)
+        if not arrivals:
+            return agg_goal_weights
+        n = len(arrivals)
+        if any(t.count <= 0 for t in arrivals):
+            raise ValueError("FedBuff.do_arrivals: an arrival with count <= 0 (the roles skip those)")
+        d = 1 + version - np.fromiter((t.version for t in arrivals), dtype=np.int64, count=n)
+        bad = np.flatnonzero(d <= 0)
+        upto = int(bad[0]) if bad.size else n
+        rates = (1.0 / np.sqrt(d[:upto].astype(np.float64))).tolist()
+        entries = [(t.weights, r) for t, r in zip(arrivals, rates)]
+        self.agg_goal_weights = agg_goal_weights
+        self.is_agg_weights_none = agg_goal_weights is None
+        if entries and self.is_agg_weights_none:
+            self._apply(entries[:1])          # the first arrival's do(): a None-start
+            entries = entries[1:]
+            self.is_agg_weights_none = not entries
+        self._apply(entries)                  # every later do() adds to the aggregate
+        if upto < n:
+            math.sqrt(int(d[upto]))           # raises ValueError (math domain error) when negative
+            raise ZeroDivisionError("float division by zero")
         return self.agg_goal_weights
 
     def _apply(self, entries):
@@ -287,6 +349,11 @@ def _fused_scale_add(base_weights, agg, agg_goal, delta, key_groups=None, after_
 def _uniform(agg: DeferredAggregate) -> bool:
     """Every queued arrival carries every key in the aggregate's dtype, a dtype the kernels
     carry (the one-launch case)."""
+    slab = agg._pend_slab
+    if slab:        # every arrival a whole slot of one slab: its keys / dtypes decide for all
+        return (len(slab.keys) == len(agg._keys)
+                and all(k in slab.meta and slab.meta[k][0] == dt and dt in engine.DTYPE_CODE
+                        for k, (_, dt) in agg._meta.items()))
     return all(agg._meta[k][1] in engine.DTYPE_CODE for k in agg._keys) and all(k in w and engine.weight_dtype(w, k) == agg._meta[k][1]
                for w in engine.representatives([w for w, _ in agg._pending]) for k in agg._keys)
 
@@ -326,7 +393,7 @@ def flush_aggregates(aggs):
                 rows.append(row)
         engine.reduce_(outs, None if init else outs, clients, None, init_first=init, seg_rates=rows)
         for a in members:
-            a._pending = []
+            a._clear_pending()
 
 
 def scale_add_many(pairs, agg_goal: int, with_delta: bool = False):
@@ -401,6 +468,14 @@ def _tiled_stride(ts, n):
 def _hier_rows(aggs, keys, device):
     """Per key: (arrival pointers middle-major, tile stride), or None if no single stride fits."""
     meta = aggs[0]._meta
+    slab = aggs[0]._pend_slab
+    if slab and all(a._pend_slab is slab for a in aggs):
+        # every arrival of every middle is a whole slot of one slab (tracked as they queued)
+        slots = np.fromiter(itertools.chain.from_iterable(a._pend_slots for a in aggs), dtype=np.uint64)
+        rows = engine.slot_rows(slab, None, slots, keys, {k: math.prod(meta[k][0]) for k in keys},
+                                {k: meta[k][1] for k in keys}, device)
+        if rows is not None:
+            return rows, []
     rows = engine.slab_rows([w for a in aggs for w, _ in a._pending], keys,
                             {k: math.prod(meta[k][0]) for k in keys}, {k: meta[k][1] for k in keys}, device)
     if rows is not None:

@@ -22,8 +22,10 @@ without ever touching the caller's (or an UpdateSlab slot's) memory.
 (:class:`_PingPongHistories`, the UpdateSlab layout: one contiguous
 ``[ends][chunk]`` block per chunk) and an arrival's updated history ``h + w`` is
 written to the OTHER store -- a round never writes the addresses it reads, and each
-workgroup streams one contiguous history block.  Measured at 512 x 25M fp32: 6.7 %
-faster than in-place per-end rows, for twice the history memory.
+workgroup streams one contiguous history block.  Opt-in: measured through the drop-in at
+512 ends x 16M fp32 it is SLOWER than the in-place per-end rows (tiled ping-pong 17.75 ms,
+row ping-pong 17.13 ms, rows 16.95 ms; DESIGN.md §4, profiles/r02_feddyn_history_ab.log),
+for twice the history memory; round 1's 12.5M-param probe had suggested a gain.
 """
 import collections
 import collections.abc
@@ -109,6 +111,13 @@ class _PingPongHistories:
             return self.rows[end][store][k].data_ptr()
         _, _, base, slot_bytes, _ = self.stores[store].key_layout(k)
         return base + self.slot[end] * slot_bytes
+
+    def write(self, end, k, h) -> None:
+        """``h`` (the end's whole history of key ``k``) into the store holding its current one."""
+        if not self.tiled:
+            self.rows[end][self.cur[end]][k].copy_(h.reshape(self.rows[end][self.cur[end]][k].shape))
+        else:
+            self.stores[self.cur[end]].write_key(self.slot[end], k, h.reshape(-1))
 
     def tile_stride(self, k) -> int:
         return self.stores[0].key_layout(k)[4] if self.tiled else 0
@@ -198,18 +207,27 @@ class FedDyn(FedAvg):
         rest = [k for k in base_weights if k not in fused]
         new_hist = {e: {} for e, _ in arrivals if e not in had}
         cld = {}
-        if fused:
-            if pp:
+        if pp:
+            # the reference-path keys first: they read the histories from the store holding
+            # them before the fused round flips the arriving ends to the other store; their
+            # updated histories then join that store (_pp_absorb)
+            if rest:
+                self._reference_round(rest, arrivals, had, rate, device, new_hist, cld)
+            if fused:
                 self._fused_round_pp(fused, arrivals, had, rate, device, cld)
-            else:
+            if rest:
+                self._pp_absorb(rest, arrivals, had, new_hist)
+        else:
+            if fused:
                 self._fused_round(fused, arrivals, had, rate, device, new_hist, cld)
-        if rest:
-            self._reference_round(rest, arrivals, had, rate, device, new_hist, cld)
+            if rest:
+                self._reference_round(rest, arrivals, had, rate, device, new_hist, cld)
         for e, w in arrivals:
             if e not in had:
                 if pp:
                     self.local_param_dict[e] = _StoredHistory(self._pp, e, w.keys(),
-                                                              {k: new_hist[e][k] for k in w.keys() if k in rest})
+                                                              {k: new_hist[e][k] for k in w.keys()
+                                                               if k in rest and k in new_hist[e]})
                 else:
                     self.local_param_dict[e] = {k: new_hist[e][k] for k in w.keys()}
         avg_model = self.agg_weights
@@ -246,7 +264,32 @@ class FedDyn(FedAvg):
         t = self._pp.template.get(k)
         if t is None or t.dtype != a.dtype or t.shape != a.shape:
             return False
-        return all(k in w and engine.weight_dtype(w, k) == a.dtype for _, w in arrivals)
+        if not all(k in w and engine.weight_dtype(w, k) == a.dtype for _, w in arrivals):
+            return False
+        # an end whose history of k left the stores (another dtype, see _pp_absorb) keeps the
+        # key on the reference path: the stores do not hold its current value
+        return not any(isinstance(h, _StoredHistory) and k in h.rest for h in self.local_param_dict.values())
+
+    def _pp_absorb(self, keys, arrivals, had, new_hist):
+        """Template keys that took the reference path this round (an arrival in another dtype):
+        each arriving end's updated history goes back into the store holding its current one
+        -- a new end gets its slot -- so a later fused round reads the right bytes.  A history
+        whose dtype or size no longer fits the store (torch promoted it) stays in the end's
+        ``rest`` and the key off the fused path (_fusable_pp)."""
+        pp = self._pp
+        tk = [k for k in keys if k in pp.template]
+        if not tk:
+            return
+        pp.ensure([e for e, _ in arrivals])
+        for e, _ in arrivals:
+            for k in tk:
+                src = new_hist[e] if e not in had else self.local_param_dict[e].rest
+                h = src.get(k)
+                t = pp.template[k]
+                if h is None or h.dtype != t.dtype or h.numel() != t.numel() or not h.is_cuda:
+                    continue
+                pp.write(e, k, h)
+                del src[k]
 
     def _fused_round_pp(self, keys, arrivals, had, rate, device, cld):
         pp = self._pp

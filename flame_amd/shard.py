@@ -643,6 +643,20 @@ class ShardedOptimizer:
             raise RuntimeError("ShardedOptimizer(accumulate_only): call set_layout(model_weights) first")
         return self.inner.do(agg, _SliceCache(cache, self.plan), total=total, version=version, **kwargs)
 
+    def do_arrivals(self, agg, arrivals, *, version: int = 0):
+        """FedBuff's batched arrivals (``FedBuff.do_arrivals``) on this rank's slices of each
+        arrival (``accumulate_only``); the aggregate stays sharded."""
+        if not self.accumulate_only:
+            raise TypeError("ShardedOptimizer.do_arrivals: FedBuff with accumulate_only=True only")
+        if self.plan is None:
+            raise RuntimeError("ShardedOptimizer(accumulate_only): call set_layout(model_weights) first")
+        plan, local = self.plan, []
+        for tres in arrivals:
+            lw = plan.local(tres.weights)
+            local.append(tres if lw is tres.weights else
+                         _SlicedResult(lw, getattr(tres, "count", 0), getattr(tres, "version", 0)))
+        return self.inner.do_arrivals(agg, local, version=version)
+
     def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal: int):
         """fedbuff.py:101-127 on this rank's ranges of ``base_weights``, then the in-place gather."""
         plan = self._ensure_plan(base_weights)

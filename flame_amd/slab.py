@@ -36,6 +36,11 @@ from . import _native as N
 from . import engine
 
 
+# pageable payload spans of at least this many bytes are staged through pinned memory
+PINNED_STAGE_MIN = 256 << 10
+PINNED_RING = 4
+
+
 class SlotWeights(dict):
     """The weights dict of one slab slot: {key: tiled view}; ``shapes`` holds the model
     shapes; releases the slot when dropped."""
@@ -122,6 +127,9 @@ class UpdateSlab:
         self._ready = {}         # slot -> event the next writer must wait for
         self._stream = None
         self._wt = None          # per-key insert table (see _write_table)
+        self._ring_bufs = [None] * PINNED_RING      # pinned staging of pageable payloads (_pinned_stage)
+        self._ring_events = [None] * PINNED_RING
+        self._ring_next = 0
 
     # ------------------------------------------------------------------ slots
     def nbytes(self) -> int:
@@ -181,8 +189,11 @@ class UpdateSlab:
         """Copy one client's update (host or device tensors) into ``slot`` on ``stream``.
 
         Device sources: ONE ``flame_slab_write`` launch tiles every key into the slot (the
-        table rides in the kernel arguments).  Host sources (pinned, registered or pageable):
-        ``flame_slab_write_2d``, one pitched copy-engine transfer per key, no staging tensor.
+        table rides in the kernel arguments).  Host tensors that are views into one decoded
+        channel payload (``ingest.decode``): the payload span holding them crosses PCIe in ONE
+        transfer and joins that launch (:meth:`_stage_payloads`).  Other host sources (pinned,
+        registered or pageable): ``flame_slab_write_2d``, one pitched copy-engine transfer per
+        key, no staging tensor.
         """
         st = stream or torch.cuda.current_stream(self.device)
         ev = self._ready.pop(slot, None)
@@ -219,6 +230,9 @@ class UpdateSlab:
             else:
                 host_rows.append(row)
                 keep.append(src)
+        staged = []
+        if len(host_rows) > 1:
+            dev_rows += self._stage_payloads(host_rows, keep, st, staged)
         L = N.lib()
         if dev_rows:
             tab = np.asarray(dev_rows, dtype=np.uint64).view(np.int64)
@@ -227,6 +241,8 @@ class UpdateSlab:
                 for t in keep:
                     if t.is_cuda:
                         t.record_stream(st)       # read on `st`: keep the caching allocator off it
+            if staged:
+                engine._staging.hold_on(st, staged)
         if host_rows:
             tab = np.asarray(host_rows, dtype=np.uint64).view(np.int64)
             N.check(L.flame_slab_write_2d(tab.ctypes.data, len(host_rows), st.cuda_stream))
@@ -234,6 +250,81 @@ class UpdateSlab:
                 st.synchronize()
             else:       # the copy engine reads the host tensors after this returns: hold them
                 engine._staging.hold_on(st, [t for t in keep if not t.is_cuda])
+
+    def write_key(self, slot: int, key: str, src: torch.Tensor) -> None:
+        """Copy one key of ``slot`` from a device tensor (one ``flame_slab_write`` launch on the
+        current stream); the rest of the slot is untouched."""
+        dt, _, n, _, _ = self.meta[key]
+        if src.numel() != n or src.dtype != dt or not src.is_cuda:
+            raise ValueError(f"{key}: need a device {dt} tensor of {n} elements")
+        if n == 0:
+            return
+        src = src.contiguous()
+        i = self.keys.index(key)
+        wt = self._write_table()
+        tab = np.asarray([(src.data_ptr(), int(wt[i, 0]) + slot * N.FLAME_TILE_BYTES, int(wt[i, 1]), int(wt[i, 2]))],
+                         dtype=np.uint64).view(np.int64)
+        N.check(N.lib().flame_slab_write(tab.ctypes.data, 1, torch.cuda.current_stream(self.device).cuda_stream))
+
+    def _stage_payloads(self, host_rows, keep, st, staged):
+        """Host rows whose tensors are views into ONE decoded channel payload
+        (``ingest.decode`` tags them with it): the payload's byte span holding them goes to
+        the device in ONE transfer, and those rows become device rows reading it (misaligned
+        sources are fine for ``flame_slab_write``).  Removes them from ``host_rows``; the host
+        spans copied go to ``staged`` (held until the copy has run: a pinned payload's copy is
+        asynchronous)."""
+        groups = collections.defaultdict(list)
+        for src in keep:
+            buf = getattr(src, "_flame_payload", None) if not src.is_cuda else None
+            if buf is not None:
+                groups[id(buf)].append((buf, src.data_ptr(), src.numel() * src.element_size()))
+        out = []
+        for items in groups.values():
+            if len(items) < 2:
+                continue
+            buf = items[0][0]
+            whole = torch.frombuffer(buf, dtype=torch.uint8)        # zero-copy: the payload's address range
+            base, end = whole.data_ptr(), whole.data_ptr() + whole.numel()
+            lo = min(p for _, p, _ in items)
+            hi = max(p + n for _, p, n in items)
+            if lo < base or hi > end:
+                continue
+            span = whole[lo - base:hi - base]
+            ring_slot = None
+            if not span.is_pinned() and span.numel() >= PINNED_STAGE_MIN:
+                # pageable payload: torch's multi-threaded host copy into a pinned ring slot,
+                # then an ASYNCHRONOUS DMA (a pageable H2D blocks the caller for its duration)
+                span, ring_slot = self._pinned_stage(span)
+            with torch.cuda.stream(st):
+                dev = span.to(self.device, non_blocking=True)
+            dev.record_stream(st)
+            if ring_slot is not None:             # the ring slot is free again once this DMA has run
+                self._ring_events[ring_slot] = torch.cuda.Event()
+                self._ring_events[ring_slot].record(st)
+            keep.append(dev)
+            staged.append(whole)
+            ptrs = {p for _, p, _ in items}
+            moved = [r for r in host_rows if r[0] in ptrs]
+            for r in moved:
+                host_rows.remove(r)
+                out.append((dev.data_ptr() + (r[0] - lo), r[1], r[2], r[3]))
+        return out
+
+    def _pinned_stage(self, span: torch.Tensor):
+        """``span`` copied into a pinned host buffer: (the copy, its ring slot).  The ring holds
+        PINNED_RING buffers per slab; a slot is reused once the DMA that read it has run (the
+        caller records ``_ring_events[slot]`` behind that transfer)."""
+        i = self._ring_next
+        self._ring_next = (i + 1) % PINNED_RING
+        ev = self._ring_events[i]
+        if ev is not None:
+            ev.synchronize()
+        buf = self._ring_bufs[i]
+        if buf is None or buf.numel() < span.numel():
+            buf = self._ring_bufs[i] = torch.empty(max(span.numel(), 1 << 20), dtype=torch.uint8, pin_memory=True)
+        out = buf[:span.numel()]
+        out.copy_(span)
+        return out, i
 
     def put(self, weights: Dict[str, torch.Tensor], stream=None) -> SlotWeights:
         """Acquire a slot, write ``weights`` into it, return its tiled views."""

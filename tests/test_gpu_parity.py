@@ -718,6 +718,51 @@ def test_feddyn_vs_oracle_partial_participation(placement, order, history):
             S.assert_bitwise(f"feddyn/{placement}/hist/{e}", S.to_cpu(amd.local_param_dict[e]), h)
 
 
+@pytest.mark.parametrize("history", ["pingpong", "pingpong_rows"])
+def test_feddyn_pingpong_key_leaves_and_returns(history):
+    """under history="pingpong" a key whose arrival comes in another dtype takes the
+    reference path for that round; the arriving ends' updated histories must land back in the
+    stores (a new end included), so the next fused round reads them -- and a history torch
+    promoted to a wider dtype (f32 + f64 -> f64) keeps the key off the fused path while any
+    end holds it.  5 rounds vs the oracle, bitwise: average, cld_model, every history."""
+    O = _oracle()
+    g = torch.Generator().manual_seed(61)
+    tmpl = _dyn_model(g, 300_007)
+    ends0 = [f"e{i}" for i in range(6)]
+    rounds = [
+        (ends0, {}),                                              # all fused
+        (ends0[:4] + ["n1"], {"e1": ("w", torch.bfloat16)}),      # w -> reference path; n1 new
+        (["e0", "e1", "n1", "e5"], {}),                           # w fused again: reads the stores
+        (["e2", "e3", "n2"], {"e2": ("w", torch.float64)}),       # e2's history of w becomes f64
+        (ends0 + ["n1", "n2"], {}),                               # w stays on the reference path
+    ]
+    amd = make_amd("feddyn", alpha=0.01, history=history)
+    ora = O.OracleFedDyn(alpha=0.01)
+    wa, wo = {k: v.to(DEV) for k, v in tmpl.items()}, {k: v.clone() for k, v in tmpl.items()}
+    every = ends0 + ["n1", "n2"]
+    for r, (ends, odd) in enumerate(rounds):
+        amd.save_state(S._PRE, active_ends=every)
+        ora.save_state(S._PRE, active_ends=every)
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i, e in enumerate(ends):
+            u = _dyn_update(g, tmpl, 10 * r + i)
+            if e in odd:
+                k, dt = odd[e]
+                u[k] = u[k].to(dt)
+            ca[e] = S.TR({k: v.to(DEV) for k, v in u.items()}, 5 + i)
+            co[e] = S.TR({k: v.clone() for k, v in u.items()}, 5 + i)
+        total = sum(5 + i for i in range(len(ends)))
+        a = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=total)
+        o = ora.do({k: v.clone() for k, v in wo.items()}, co, total=total)
+        S.assert_bitwise(f"pp/{history}/r{r}/avg", S.to_cpu(a), o)
+        S.assert_bitwise(f"pp/{history}/r{r}/cld", S.to_cpu(amd.cld_model), ora.cld_model)
+        for e, h in ora.local_param_dict.items():
+            if h is not None:
+                got = {k: amd.local_param_dict[e][k] for k in h}
+                S.assert_bitwise(f"pp/{history}/r{r}/hist/{e}", S.to_cpu(got), h)
+        wa, wo = amd.cld_model, ora.cld_model
+
+
 def test_scaffold_vs_oracle_rounds():
     """SCAFFOLD drop-in == oracle bitwise: c_glob (HBM-resident, updated in place) and the
     model over 3 rounds, including an int buffer whose control variate arrives as fp32, and
@@ -914,6 +959,78 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
     tw = {k: v.clone() for k, v in top_w0.items()}
     top_o.scale_add_agg_weights(tw, top_agg_o, 7)
     S.assert_bitwise("oracle top w", fused[3], tw)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("placement", ["slab", "tensors"])
+@pytest.mark.parametrize("start", ["none", "existing"])
+def test_fedbuff_do_arrivals_equals_per_do(dtype, placement, start):
+    """FedBuff.do_arrivals (a middle's round of arrivals in one call) == do() per arrival (the
+    async roles, asyncfl/middle_aggregator.py:190-203) == the oracle, bitwise: the aggregate
+    read back, and the fused scale_add + delta applied from the queued arrivals."""
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(77)
+    shapes = {"w": (4099,), "m": (33, 65), "b": (3,)}
+    n, rnd = 13, 20
+    ups = [{k: (torch.randn(sh, generator=g) * 1e-2).to(dtype) for k, sh in shapes.items()} for _ in range(n)]
+    vers = [rnd - (i * 3) % 5 for i in range(n)]
+    base0 = {k: torch.randn(sh, generator=g).to(dtype) for k, sh in shapes.items()}
+    prev = {k: (torch.randn(sh, generator=g) * 1e-3).to(dtype) for k, sh in shapes.items()}
+    slab = UpdateSlab({k: torch.empty(sh, dtype=dtype) for k, sh in shapes.items()}, capacity=2 * n, device=DEV) \
+        if placement == "slab" else None
+
+    def dev(w):
+        w = {k: v.to(DEV) for k, v in w.items()}
+        return slab.put(w) if slab is not None else w
+
+    def start_agg():
+        return {k: v.to(DEV) for k, v in prev.items()} if start == "existing" else None
+
+    per, agg_p = make_amd("fedbuff"), start_agg()
+    for i in range(n):
+        c = S.SortedCache()
+        c[f"{i}"] = S.TR(dev(ups[i]), 1, vers[i])
+        agg_p = per.do(agg_p, c, total=1, version=rnd)
+    bat = make_amd("fedbuff")
+    agg_b = bat.do_arrivals(start_agg(), [S.TR(dev(ups[i]), 1, vers[i]) for i in range(n)], version=rnd)
+    ora, agg_o = O.OracleFedBuff(), ({k: v.clone() for k, v in prev.items()} if start == "existing" else None)
+    for i in range(n):
+        c = S.SortedCache()
+        c[f"{i}"] = S.TR({k: v.clone() for k, v in ups[i].items()}, 1, vers[i])
+        agg_o = ora.do(agg_o, c, total=1, version=rnd)
+    # the fused scale_add + delta straight from the queued arrivals (before any read)
+    wb = {k: v.to(DEV) for k, v in base0.items()}
+    _, db = bat.scale_add_agg_weights_with_delta(wb, agg_b, n)
+    wp = {k: v.to(DEV) for k, v in base0.items()}
+    _, dp = per.scale_add_agg_weights_with_delta(wp, agg_p, n)
+    wo = {k: v.clone() for k, v in base0.items()}
+    do_ = {k: O.scale_add_tensor(wo[k], agg_o[k], n, want_delta=True) for k in wo}
+    for lbl, a, b in (("agg", S.to_cpu(dict(agg_b)), S.to_cpu(dict(agg_p))), ("agg/oracle", S.to_cpu(dict(agg_b)), agg_o),
+                      ("w", S.to_cpu(wb), S.to_cpu(wp)), ("w/oracle", S.to_cpu(wb), wo),
+                      ("delta", S.to_cpu(db), S.to_cpu(dp)), ("delta/oracle", S.to_cpu(db), do_)):
+        S.assert_bitwise(f"do_arrivals/{lbl}", a, b)
+
+
+def test_hierarchy_round_from_batched_arrivals_vs_fixture(golden):
+    """The reference-generated 2 x 3 hierarchy (hier_fedbuff_small.npz) with each middle's
+    arrivals handed over in ONE FedBuff.do_arrivals call, then one hierarchy_round launch:
+    top model and middle deltas bitwise == the reference's."""
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    fx = golden("hier_fedbuff_small.npz")
+    rnd = fx.meta["round"]
+    top_w0 = fx.weights("top_w0")
+    mids = []
+    for mid in range(2):
+        arr = [S.TR({k: v.to(DEV) for k, v in fx.weights(f"m{mid}/update{t}").items()}, 10 + t, rnd - t % 2)
+               for t in range(3)]
+        agg = make_amd("fedbuff").do_arrivals(None, arr, version=rnd)
+        mids.append(({k: v.to(DEV) for k, v in top_w0.items()}, agg, 3, rnd - mid))
+    top = {k: v.to(DEV) for k, v in top_w0.items()}
+    _, deltas = hierarchy_round(mids, None, version=rnd, top_weights=top, top_goal=2, with_delta=True)
+    S.assert_bitwise("hier/top", S.to_cpu(top), fx.weights("top_out"))
+    for mid in range(2):
+        S.assert_bitwise(f"hier/delta m{mid}", S.to_cpu(deltas[mid]), fx.weights(f"m{mid}/delta"))
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -520,7 +520,8 @@ def test_hier_wave_quantum_world1():
     """ShardedHierarchy(middles=M) on the GPU: the library's residency for the hierarchy
     launch (2 workgroups per CU with LDS-held store groups, more without) sizes the last
     wave to whole rounds of resident workgroups; the sharded round stays bitwise equal to
-    one hierarchy_round (world 1, no process group)."""
+    one hierarchy_round (world 1, no process group) -- half of its middles taking their
+    arrivals through ShardedOptimizer.do_arrivals."""
     from flame_amd import engine, shard
     from flame_amd.optimizer.fedbuff import FedBuff, hierarchy_round
     from flame_amd.slab import UpdateSlab
@@ -545,7 +546,10 @@ def test_hier_wave_quantum_world1():
         mids = []
         for m in range(M):
             opt, agg = (hier.middle_optimizer() if sharded else FedBuff()), None
-            for t in range(C):
+            if sharded and m % 2 == 0:     # the batched arrival API on half of the sharded middles
+                agg = opt.do_arrivals(None, [S.TR(slab.put({k: v.to(DEV) for k, v in ups[m][t].items()}), 1,
+                                                  rnd - (m + t) % 3) for t in range(C)], version=rnd)
+            for t in range(C if agg is None else 0):
                 c = S.SortedCache()
                 c[f"m{m}t{t}"] = S.TR(slab.put({k: v.to(DEV) for k, v in ups[m][t].items()}), 1, rnd - (m + t) % 3)
                 agg = opt.do(agg, c, total=1, version=rnd)

@@ -108,7 +108,8 @@ def test_slab_write_one_launch_per_update():
 
 
 def test_slab_write_entry_points_direct():
-    """The C entry points on a raw table: >89 entries split over launches, 2D copies from host."""
+    """The C entry points on a raw table: >89 entries split over launches, device sources at every
+    16-byte misalignment, 2D copies from host."""
     from flame_amd import _native as N
     L = N.lib()
     n_ent, stride = 200, 3 * N.FLAME_TILE_BYTES
@@ -116,7 +117,13 @@ def test_slab_write_entry_points_direct():
     sizes = [int(x) for x in torch.randint(0, 3 * N.FLAME_TILE_BYTES, (n_ent,), generator=g)]
     dst = torch.zeros(n_ent, 3, 3, N.FLAME_TILE_BYTES, dtype=torch.uint8, device=DEV)   # [entry][tile][slot][bytes]
     srcs = [torch.randint(0, 256, (s,), generator=g, dtype=torch.uint8) for s in sizes]
-    dsrc = [s.to(DEV) for s in srcs]
+    # device sources at every misalignment 0..15 (the kernel's funnel-shift path)
+    dsrc = []
+    for i, s in enumerate(srcs):
+        o = i % 16
+        buf = torch.zeros(s.numel() + 16, dtype=torch.uint8, device=DEV)
+        buf[o:o + s.numel()] = s.to(DEV)
+        dsrc.append(buf[o:o + s.numel()])
     tab = np.zeros((n_ent, 4), dtype=np.int64)
     for i, s in enumerate(dsrc):
         tab[i] = (s.data_ptr(), dst[i, 0, 1].data_ptr(), sizes[i], stride)
@@ -139,3 +146,40 @@ def test_slab_write_entry_points_direct():
     bad[0, 1], bad[0, 2], bad[0, 3] = dst.data_ptr(), 2 * N.FLAME_TILE_BYTES, 100
     assert L.flame_slab_write(bad.ctypes.data, 1, None) == N.FLAME_EINVAL
     assert b"dst_tile_stride" in L.flame_last_error()
+
+
+def test_decoded_payloads_one_transfer_each_and_pinned_ring():
+    """Channel payloads decoded zero-copy (ingest.decode) into a slab-placed DeviceUpdateCache:
+    each update's tensors -- views into one pageable payload -- cross PCIe as ONE span, staged
+    through the slab's pinned ring (more payloads than ring slots); the payload buffers are
+    overwritten right after each insert (the receiver reuses them), and the FedAvg over the
+    cache still equals the oracle on the original bytes, bitwise."""
+    import cloudpickle
+    import scenarios as S
+    from flame_amd import ingest
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.slab import PINNED_RING, PINNED_STAGE_MIN
+    from oracle import oracle as O
+    g = torch.Generator().manual_seed(12)
+    shapes = {"conv.w": (32, 1, 3, 3), "conv.b": (32,), "fc.w": (128, 2304), "fc.b": (128,), "out.w": (10, 128),
+              "bn": (64,)}
+    n = PINNED_RING + 3
+    ups = [{k: torch.randn(s, generator=g) * 1e-2 for k, s in shapes.items()} for _ in range(n)]
+    base = {k: torch.randn(s, generator=g) for k, s in shapes.items()}
+    counts = [100 + 7 * i for i in range(n)]
+    cache = ingest.DeviceUpdateCache(device=DEV, placement="slab", capacity=n)
+    for i, u in enumerate(ups):
+        buf = bytearray(cloudpickle.dumps({"weights": u, "dataset_size": counts[i]}))
+        assert len(buf) > PINNED_STAGE_MIN
+        msg = ingest.decode(buf)
+        assert all(getattr(v, "_flame_payload", None) is buf for v in msg["weights"].values())
+        cache[f"t{i}"] = S.TR(msg["weights"], counts[i])
+        assert getattr(cache[f"t{i}"].weights, "slab", None) is not None
+        buf[:] = b"\xff" * len(buf)            # the receive buffer is reused for the next message
+    got = optimizer_provider.get("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache, total=sum(counts))
+    exp = {k: v.clone() for k, v in base.items()}
+    co = S.SortedCache()
+    for i, u in enumerate(ups):
+        co[f"t{i}"] = S.TR({k: v.clone() for k, v in u.items()}, counts[i])
+    O.OracleFedAvg().do(exp, co, total=sum(counts))
+    S.assert_bitwise("payload-staged fedavg", S.to_cpu(got), exp)

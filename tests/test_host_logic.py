@@ -125,6 +125,98 @@ def test_fedbuff_defers_arrivals_without_launch():
     assert plain.defer is False
 
 
+def test_fedbuff_do_arrivals_matches_per_do_queue():
+    """FedBuff.do_arrivals == the role's do() per arrival, before any launch: the same queued
+    (weights, rate) pairs in the same order (rates bit-equal to 1 / math.sqrt(...)), the same
+    None-start, the same aggregate object when one exists."""
+    import math
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.optimizer.fedbuff import DeferredAggregate
+    ws = [{"w": torch.full((3,), float(i)), "b": torch.ones(1)} for i in range(9)]
+    vers = [17 - (i * 7) % 5 for i in range(9)]
+    ref, agg = optimizer_provider.get("fedbuff"), None
+    for i in range(9):
+        c = S.SortedCache()
+        c[f"{i}"] = S.TR(ws[i], 2, vers[i])
+        agg = ref.do(agg, c, total=2, version=17)
+    opt = optimizer_provider.get("fedbuff")
+    got = opt.do_arrivals(None, [S.TR(ws[i], 2, vers[i]) for i in range(9)], version=17)
+    assert isinstance(got, DeferredAggregate) and opt.agg_goal_weights is got
+    assert [(id(w), r) for w, r in got._pending] == [(id(w), r) for w, r in agg._pending]
+    assert [r for _, r in got._pending] == [1 / math.sqrt(1 + 17 - v) for v in vers]
+    assert opt.is_agg_weights_none is False and ref.is_agg_weights_none is False
+    # onto an existing aggregate: one queue extension, same object
+    more = [S.TR(ws[i], 3, 16) for i in range(4)]
+    again = opt.do_arrivals(got, more, version=17)
+    assert again is got and len(got._pending) == 13
+    # a single arrival onto None: a None-start, as one do()
+    one = optimizer_provider.get("fedbuff")
+    a1 = one.do_arrivals(None, [S.TR(ws[0], 1, 17)], version=17)
+    assert one.is_agg_weights_none is True and len(a1._pending) == 1 and a1._pending[0][1] == 1.0
+    assert one.do_arrivals(a1, [], version=17) is a1
+
+
+def test_deferred_aggregate_tracks_one_slab_queue():
+    """DeferredAggregate notes when every queued arrival is a whole slot of one slab (pointer
+    rows then come from the slot numbers): the slab and the slots in queue order; a plain dict
+    or a second slab turns it off; a rejected arrival leaves it as it was; a flush resets it."""
+    from flame_amd.optimizers import optimizer_provider
+
+    class FakeSlab:
+        def __init__(self):
+            self.keys = ["w"]
+            self.meta = {"w": (torch.float32, (4,), 4, 0, 1)}
+
+    class Slot(dict):
+        __slots__ = ("__weakref__", "slab", "slot", "shapes")
+
+    def slot(slab, i):
+        w = Slot(w=torch.empty(0))
+        w.slab, w.slot, w.shapes = slab, i, {"w": (4,)}
+        return w
+
+    a, b = FakeSlab(), FakeSlab()
+    opt = optimizer_provider.get("fedbuff")
+    agg = opt.do_arrivals(None, [S.TR(slot(a, i), 1, 3) for i in (5, 2, 9)], version=3)
+    assert agg._pend_slab is a and agg._pend_slots == [5, 2, 9]
+    with pytest.raises(KeyError):
+        bad = Slot(zz=torch.empty(0))
+        opt.do_arrivals(agg, [S.TR(slot(a, 1), 1, 3), S.TR({"zz": torch.ones(4)}, 1, 3)], version=3)
+    assert agg._pend_slab is a and agg._pend_slots == [5, 2, 9] and len(agg._pending) == 3
+    opt.do_arrivals(agg, [S.TR(slot(a, 7), 1, 3)], version=3)
+    assert agg._pend_slots == [5, 2, 9, 7]
+    opt.do_arrivals(agg, [S.TR(slot(b, 0), 1, 3)], version=3)
+    assert agg._pend_slab is False
+    agg2 = optimizer_provider.get("fedbuff").do_arrivals(None, [S.TR(slot(a, 0), 1, 3), S.TR({"w": torch.ones(4)}, 1, 3)],
+                                                         version=3)
+    assert agg2._pend_slab is False
+    agg2._clear_pending()
+    assert agg2._pend_slab is None and agg2._pend_slots == [] and agg2._pending == []
+    del bad
+
+
+def test_fedbuff_do_arrivals_raises_at_the_stale_arrival():
+    """A stale version raises as math does, at its position: earlier arrivals are queued."""
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedbuff")
+    arr = [S.TR({"w": torch.ones(2)}, 1, 5), S.TR({"w": torch.ones(2)}, 1, 4), S.TR({"w": torch.ones(2)}, 1, 6),
+           S.TR({"w": torch.ones(2)}, 1, 1)]
+    with pytest.raises(ZeroDivisionError):
+        opt.do_arrivals(None, arr, version=5)          # 1 + 5 - 6 == 0 at the third arrival
+    assert len(opt.agg_goal_weights._pending) == 2
+    arr[2] = S.TR({"w": torch.ones(2)}, 1, 9)
+    opt2 = optimizer_provider.get("fedbuff")
+    with pytest.raises(ValueError):
+        opt2.do_arrivals(None, arr, version=5)         # negative: math domain error
+    assert len(opt2.agg_goal_weights._pending) == 2
+    with pytest.raises(ValueError):
+        optimizer_provider.get("fedbuff").do_arrivals(None, [S.TR({"w": torch.ones(2)}, 0, 5)], version=5)
+    opt3 = optimizer_provider.get("fedbuff")
+    with pytest.raises(ZeroDivisionError):
+        opt3.do_arrivals(None, [S.TR({"w": torch.ones(2)}, 1, 6)], version=5)
+    assert opt3.agg_goal_weights is None
+
+
 def test_fedprox_is_fedavg_with_regularizer():
     from flame_amd.optimizers import optimizer_provider
     from flame_amd.optimizer.fedavg import FedAvg

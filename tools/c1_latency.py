@@ -39,7 +39,7 @@ def main():
     pls = [cloudpickle.dumps({"weights": {k: v + 0.01 * (i + 1) for k, v in hw.items()}, "dataset_size": 2000})
            for i in range(2)]
     for placement in ["hbm", "slab", "host", "to_device"]:
-        T = {"decode": [], "cache": [], "do": [], "sync": [], "total": []}
+        T = {"decode": [], "cache": [], "deepcopy": [], "do": [], "sync": [], "total": []}
         cache = _SortedCache() if placement == "to_device" else \
             ingest.DeviceUpdateCache(device=dev, placement=placement, capacity=4)
         for _ in range(30):
@@ -52,25 +52,28 @@ def main():
                 else:
                     cache[f"t{i}"] = TrainResult(m["weights"], 2000)
             t2 = time.perf_counter()
-            opt.do(deepcopy(w), cache, total=4000)
+            base = deepcopy(w)           # the role's do(deepcopy(self.weights), ...) (syncfl/top_aggregator.py:161-166)
+            t2b = time.perf_counter()
+            opt.do(base, cache, total=4000)
             t3 = time.perf_counter()
             torch.cuda.synchronize()
             t4 = time.perf_counter()
-            for k, v in zip(T, [t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0]):
+            for k, v in zip(T, [t1 - t0, t2 - t1, t2b - t2, t3 - t2b, t4 - t3, t4 - t0]):
                 T[k].append(v * 1e3)
         print(placement, {k: round(statistics.median(v[5:]), 3) for k, v in T.items()}, flush=True)
     t0 = time.perf_counter()
     for _ in range(10):
         [cloudpickle.loads(p) for p in pls]
     print(f"reference cloudpickle.loads of the 2 payloads: {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
-    if "--profile" in sys.argv:     # where do()'s host time goes (HBM placement)
+    if "--profile" in sys.argv:     # where a round's host time goes (slab placement)
         import cProfile
         import pstats
-        cache = ingest.DeviceUpdateCache(device=dev, placement="hbm", capacity=4)
+        cache = ingest.DeviceUpdateCache(device=dev, placement="slab", capacity=4)
         msgs = [ingest.decode(p) for p in pls]
 
         def rounds(n):
             for _ in range(n):
+                msgs = [ingest.decode(p) for p in pls]
                 for i, m in enumerate(msgs):
                     cache[f"t{i}"] = TrainResult(m["weights"], 2000)
                 opt.do(deepcopy(w), cache, total=4000)
@@ -80,7 +83,7 @@ def main():
         pr.enable()
         rounds(200)
         pr.disable()
-        pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
 
 
 if __name__ == "__main__":
