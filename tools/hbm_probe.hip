@@ -172,3 +172,38 @@ extern "C" int probe_mix_burst(const void* p, void* dst, int64_t wgs, int R, int
                        (const uint8_t*)p, (uint8_t*)dst, R, B, inplace);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Sub-row region probe (round 3): the hierarchy kernel's region question.  The C5 slab gives a
+// workgroup one 16 MiB region (4096 arrivals x one 4 KiB tile row each).  Here workgroup w
+// reads region r = w / S, but only sub-row q = w % S (4096 / S bytes) of each 4 KiB row, with
+// BLK lanes (BLK x 16 B = 4096 / S bytes, one row per step, UN rows in flight).  S = 1, BLK = 256
+// is the current pattern; S = 4, BLK = 64 is a one-wave workgroup on a quarter of every row
+// (the four quarters' workgroups are dispatched back to back); compare with contiguous R / S regions.
+template <int BLK, int UN>
+__global__ __launch_bounds__(BLK) void read_subrow_kernel(const uint8_t* __restrict__ p, int64_t region, int S,
+                                                          int64_t rows, uint32_t* out) {
+    const int64_t r = blockIdx.x / S, q = blockIdx.x % S;
+    const uint8_t* base = p + r * region + q * (4096 / S) + threadIdx.x * 16;
+    uint32_t acc = 0;
+    int64_t i = 0;
+    for (; i + UN <= rows; i += UN) {
+        u4 v[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(base + (i + u) * 4096));
+#pragma unroll
+        for (int u = 0; u < UN; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+extern "C" int probe_read_subrow(const void* p, int64_t bytes, void* out, int64_t region, int S, void* stream) {
+    if (region % 4096 || (S != 1 && S != 2 && S != 4)) return 2;
+    const int64_t regions = bytes / region, rows = region / 4096;
+    const dim3 grid((unsigned)(regions * S));
+    hipStream_t st = (hipStream_t)stream;
+    if (S == 1) hipLaunchKernelGGL((read_subrow_kernel<256, 16>), grid, dim3(256), 0, st, (const uint8_t*)p, region, S, rows, (uint32_t*)out);
+    else if (S == 2) hipLaunchKernelGGL((read_subrow_kernel<128, 16>), grid, dim3(128), 0, st, (const uint8_t*)p, region, S, rows, (uint32_t*)out);
+    else hipLaunchKernelGGL((read_subrow_kernel<64, 16>), grid, dim3(64), 0, st, (const uint8_t*)p, region, S, rows, (uint32_t*)out);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
