@@ -284,9 +284,17 @@ class PayloadDecoder:
             _sysinfo, q = self.load(q)
             if len(_STORAGE_HEADERS) < 8:
                 _STORAGE_HEADERS.append(bytes(self.mv[span.start:q]))
-        # the storage record (object pickle + key-list pickle + numel) of a given tensor repeats
-        # byte for byte in every payload of the same model: parse results are kept by their
-        # exact bytes (the VM is a pure function of them), grouped by record length
+        # torch's own record layout (legacy _save, protocol 2): parsed field by field, every byte
+        # checked; the storage key inside it is the storage's address, new in every message
+        rec = _parse_storage_record(self.mv, q)
+        if rec is not None:
+            dtype, numel, q = rec
+            nbytes = numel * dtype.itemsize
+            if q + nbytes > span.start + span.n:
+                raise pickle.UnpicklingError("storage runs past its bytes")
+            return _StorageRef(self.buf, q, numel, dtype)
+        # any other encoding of the record: parse results kept by the record's exact bytes (the
+        # VM is a pure function of them), grouped by record length
         for n_rec, seen in _STORAGE_RECORDS.items():
             hit = seen.get(bytes(self.mv[q:q + n_rec]))
             if hit is not None:
@@ -320,6 +328,69 @@ class PayloadDecoder:
         if len(seen) < 4096:
             seen[bytes(self.mv[rec0:q])] = (obj.dtype, numel, nbytes)
         return _StorageRef(self.buf, q, numel, obj.dtype)
+
+
+def _parse_storage_record(mv, q):
+    """The storage record torch's legacy ``_save`` writes (protocol 2) -- the persistent-id
+    pickle ``('storage', torch.<T>Storage, key, location, numel, None)``, the key-list pickle
+    ``[key]`` and the u64 element count -- parsed without the VM.  Returns ``(dtype, numel,
+    position after the count)``, or None if ANY byte departs from that layout (the caller then
+    runs the restricted VM)."""
+    n = len(mv)
+
+    def unicode_at(p):        # BINUNICODE: 'X' u32 length, utf-8 bytes
+        if p + 5 > n or mv[p] != 0x58:
+            return None, p
+        ln = int.from_bytes(mv[p + 1:p + 5], "little")
+        if p + 5 + ln > n:
+            return None, p
+        return bytes(mv[p + 5:p + 5 + ln]), p + 5 + ln
+
+    def binput(p, i):
+        return p + 2 if p + 2 <= n and mv[p] == 0x71 and mv[p + 1] == i else -1
+
+    if bytes(mv[q:q + 3]) != b"\x80\x02(":
+        return None
+    tag, p = unicode_at(q + 3)
+    if tag != b"storage" or (p := binput(p, 0)) < 0:
+        return None
+    if p >= n or mv[p] != 0x63:                       # GLOBAL 'torch\n<T>Storage\n'
+        return None
+    e1 = bytes(mv[p + 1:p + 64]).find(b"\n")
+    e2 = bytes(mv[p + 1:p + 64]).find(b"\n", e1 + 1) if e1 >= 0 else -1
+    if e1 < 0 or e2 < 0 or bytes(mv[p + 1:p + 1 + e1]) != b"torch":
+        return None
+    dtype = _STORAGE_DTYPES.get(bytes(mv[p + 2 + e1:p + 1 + e2]).decode("ascii", "replace"))
+    if dtype is None or (p := binput(p + 2 + e2, 1)) < 0:
+        return None
+    key, p = unicode_at(p)
+    if key is None or (p := binput(p, 2)) < 0:
+        return None
+    loc, p = unicode_at(p)
+    if loc is None or (p := binput(p, 3)) < 0 or p >= n:
+        return None
+    op = mv[p]
+    if op == 0x4B:                                    # BININT1
+        numel, p = mv[p + 1], p + 2
+    elif op == 0x4D:                                  # BININT2
+        numel, p = int.from_bytes(mv[p + 1:p + 3], "little"), p + 3
+    elif op == 0x4A:                                  # BININT
+        numel, p = int.from_bytes(mv[p + 1:p + 5], "little", signed=True), p + 5
+    elif op == 0x8A:                                  # LONG1
+        ln = mv[p + 1]
+        numel, p = int.from_bytes(mv[p + 2:p + 2 + ln], "little", signed=True), p + 2 + ln
+    else:
+        return None
+    if numel < 0 or bytes(mv[p:p + 2]) != b"Nt" or (p := binput(p + 2, 4)) < 0 or bytes(mv[p:p + 2]) != b"Q.":
+        return None
+    p += 2
+    keys = b"\x80\x02]q\x00X" + len(key).to_bytes(4, "little") + key + b"q\x01a."
+    if bytes(mv[p:p + len(keys)]) != keys:
+        return None
+    p += len(keys)
+    if p + 8 > n or int.from_bytes(mv[p:p + 8], "little") != numel:
+        return None
+    return dtype, numel, p + 8
 
 
 _STORAGE_HEADERS = []   # validated legacy-stream headers (bytes)

@@ -192,3 +192,31 @@ def test_shm_lease_registry_and_generations():
     finally:
         seg.close()
         seg.unlink()
+
+
+def test_storage_records_parsed_without_the_vm():
+    """Every storage record torch's legacy save writes -- its key is the trainer's storage
+    ADDRESS, new in every message -- is parsed by the strict field-by-field parser
+    (ingest._parse_storage_record), for every dtype and numel encoding (BININT1 / BININT2 /
+    BININT / LONG1); a record that departs from the layout in any byte goes to the restricted
+    VM, which still refuses what it does not allow."""
+    import pickle
+    import cloudpickle
+    from flame_amd import ingest
+    g = torch.Generator().manual_seed(4)
+    for dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32, torch.int16,
+               torch.int8, torch.uint8, torch.bool):
+        for n in (1, 200, 300, 70_000, 3_000_001):
+            t = (torch.randn(n, generator=g) * 50).to(dt)
+            payload = cloudpickle.dumps({"weights": {"w": t, "v": t[1:]}, "dataset_size": 7})
+            ingest._STORAGE_RECORDS.clear()
+            got = ingest.decode(payload)["weights"]
+            assert torch.equal(got["w"], t) and torch.equal(got["v"], t[1:]), (dt, n)
+            assert not ingest._STORAGE_RECORDS, (dt, n)        # the fast parser took every record
+    # a record naming a storage type outside the allowlist: fast parser declines, the VM refuses
+    t = torch.ones(4)
+    payload = bytearray(cloudpickle.dumps({"w": t}))
+    i = payload.find(b"torch\nFloatStorage\n")
+    payload[i:i + len(b"torch\nFloatStorage\n")] = b"torch\nFloatXtorage\n"
+    with pytest.raises(pickle.UnpicklingError):
+        ingest.decode(bytes(payload))

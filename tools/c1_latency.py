@@ -36,15 +36,19 @@ def main():
     hw = {k: torch.randn(s, generator=g) * 0.05 for k, s in MNIST_SHAPES}
     w = {k: v.to(dev) for k, v in hw.items()}
     opt = optimizer_provider.get("fedavg")
-    pls = [cloudpickle.dumps({"weights": {k: v + 0.01 * (i + 1) for k, v in hw.items()}, "dataset_size": 2000})
-           for i in range(2)]
+    # every round decodes FRESH payloads, as the channel delivers them: new tensors each round, so
+    # the storage keys inside (the trainer's storage addresses) differ between messages
+    R = 30
+    rounds_pls = [[cloudpickle.dumps({"weights": {k: v + 0.01 * (i + 1) + 1e-4 * r for k, v in hw.items()},
+                                      "dataset_size": 2000}) for i in range(2)] for r in range(R)]
+    pls = rounds_pls[0]
     for placement in ["hbm", "slab", "host", "to_device"]:
         T = {"decode": [], "cache": [], "deepcopy": [], "do": [], "sync": [], "total": []}
         cache = _SortedCache() if placement == "to_device" else \
             ingest.DeviceUpdateCache(device=dev, placement=placement, capacity=4)
-        for _ in range(30):
+        for r in range(R):
             t0 = time.perf_counter()
-            msgs = [ingest.decode(p) for p in pls]
+            msgs = [ingest.decode(p) for p in rounds_pls[r]]
             t1 = time.perf_counter()
             for i, m in enumerate(msgs):
                 if placement == "to_device":     # weights_to_model_device (common/util.py:198-208)
@@ -72,8 +76,8 @@ def main():
         msgs = [ingest.decode(p) for p in pls]
 
         def rounds(n):
-            for _ in range(n):
-                msgs = [ingest.decode(p) for p in pls]
+            for r in range(n):
+                msgs = [ingest.decode(p) for p in rounds_pls[r % R]]
                 for i, m in enumerate(msgs):
                     cache[f"t{i}"] = TrainResult(m["weights"], 2000)
                 opt.do(deepcopy(w), cache, total=4000)
