@@ -31,6 +31,7 @@ import collections
 import enum
 import functools
 import pickle
+import re
 import struct
 import warnings
 from typing import Any, Dict
@@ -102,6 +103,7 @@ class PayloadDecoder:
         """Run one pickle starting at ``pos``; return (object, end position)."""
         mv = self.mv
         stack, memo, marks = [], {}, []
+        push, pop, call = stack.append, stack.pop, self._call     # (hot loop: locals, not attributes)
         p = pos
         while True:
             op = mv[p]
@@ -110,18 +112,17 @@ class PayloadDecoder:
             if op == 0x94:    # MEMOIZE
                 memo[len(memo)] = stack[-1]
             elif op == 0x4B:    # BININT1
-                stack.append(mv[p])
+                push(mv[p])
                 p += 1
             elif op == 0x52:    # REDUCE
-                args = stack.pop()
-                fn = stack.pop()
-                stack.append(self._call(fn, args))
+                args = pop()
+                stack[-1] = call(stack[-1], args)
             elif op == 0x68:    # BINGET
-                stack.append(memo[mv[p]])
+                push(memo[mv[p]])
                 p += 1
             elif op == 0x8C:    # SHORT_BINUNICODE
                 n = mv[p]
-                stack.append(bytes(mv[p + 1:p + 1 + n]).decode("utf-8"))
+                push(str(mv[p + 1:p + 1 + n], "utf-8"))
                 p += 1 + n
             elif op == 0x85:    # TUPLE1
                 stack[-1] = (stack[-1],)
@@ -130,10 +131,22 @@ class PayloadDecoder:
             elif op == 0x74:    # TUPLE
                 k = marks.pop()
                 stack[k:] = [tuple(stack[k:])]
+            elif op in (0x43, 0x42, 0x8E):  # SHORT_BINBYTES, BINBYTES, BINBYTES8: keep a SPAN, no copy
+                if op == 0x43:
+                    n = mv[p]
+                    p += 1
+                elif op == 0x42:
+                    n = int.from_bytes(mv[p:p + 4], "little")
+                    p += 4
+                else:
+                    n = int.from_bytes(mv[p:p + 8], "little")
+                    p += 8
+                push(_Span(p, n))
+                p += n
             elif op == 0x29:    # EMPTY_TUPLE
-                stack.append(())
+                push(())
             elif op == 0x89:    # NEWFALSE
-                stack.append(False)
+                push(False)
             elif op == 0x80:      # PROTO
                 p += 1
             elif op == 0x95:    # FRAME
@@ -162,16 +175,6 @@ class PayloadDecoder:
             elif op == 0x8D:    # BINUNICODE8
                 n, p = self._unpack("<Q", p)
                 stack.append(bytes(mv[p:p + n]).decode("utf-8"))
-                p += n
-            elif op in (0x43, 0x42, 0x8E):  # SHORT_BINBYTES, BINBYTES, BINBYTES8: keep a SPAN, no copy
-                if op == 0x43:
-                    n = mv[p]
-                    p += 1
-                elif op == 0x42:
-                    n, p = self._unpack("<I", p)
-                else:
-                    n, p = self._unpack("<Q", p)
-                stack.append(_Span(p, n))
                 p += n
             elif op == 0x4D:    # BININT2
                 v, p = self._unpack("<H", p)
@@ -330,12 +333,36 @@ class PayloadDecoder:
         return _StorageRef(self.buf, q, numel, obj.dtype)
 
 
+# torch's storage record in one match (C speed): type name, key length + key, location length +
+# location, a BININT1 / BININT2 / BININT element count, the key list repeating the key exactly
+# (backreferences), the u64 count.  Length fields are verified after the match.
+_RECORD_RE = re.compile(
+    rb"\x80\x02\(X\x07\x00\x00\x00storageq\x00ctorch\n(\w+)\nq\x01X(.{4})([^q]*)q\x02X(.{4})([^q]*)q\x03"
+    rb"(K.|M..|J.{4})Ntq\x04Q\.\x80\x02\]q\x00X\2\3q\x01a\.(.{8})", re.S)
+
+
 def _parse_storage_record(mv, q):
     """The storage record torch's legacy ``_save`` writes (protocol 2) -- the persistent-id
     pickle ``('storage', torch.<T>Storage, key, location, numel, None)``, the key-list pickle
     ``[key]`` and the u64 element count -- parsed without the VM.  Returns ``(dtype, numel,
     position after the count)``, or None if ANY byte departs from that layout (the caller then
     runs the restricted VM)."""
+    m = _RECORD_RE.match(mv, q)
+    if m is not None:
+        name, klen, key, llen, loc, nop, cnt = m.groups()
+        dtype = _STORAGE_DTYPES.get(name.decode("ascii"))
+        if (dtype is not None and int.from_bytes(klen, "little") == len(key)
+                and int.from_bytes(llen, "little") == len(loc)):
+            op = nop[0]
+            numel = (nop[1] if op == 0x4B else int.from_bytes(nop[1:], "little", signed=(op == 0x4A)))
+            if numel >= 0 and int.from_bytes(cnt, "little") == numel:
+                return dtype, numel, m.end()
+    return _parse_storage_record_slow(mv, q)
+
+
+def _parse_storage_record_slow(mv, q):
+    """Field-by-field form of :func:`_parse_storage_record` (LONG1 counts, keys containing
+    'q', ...)."""
     n = len(mv)
 
     def unicode_at(p):        # BINUNICODE: 'X' u32 length, utf-8 bytes

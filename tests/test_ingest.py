@@ -194,7 +194,7 @@ def test_shm_lease_registry_and_generations():
         seg.unlink()
 
 
-def test_storage_records_parsed_without_the_vm():
+def test_storage_records_parsed_without_the_vm(monkeypatch):
     """Every storage record torch's legacy save writes -- its key is the trainer's storage
     ADDRESS, new in every message -- is parsed by the strict field-by-field parser
     (ingest._parse_storage_record), for every dtype and numel encoding (BININT1 / BININT2 /
@@ -203,6 +203,10 @@ def test_storage_records_parsed_without_the_vm():
     import pickle
     import cloudpickle
     from flame_amd import ingest
+
+    def no_slow(mv, q):
+        raise AssertionError("the one-match record parser should have taken this record")
+    monkeypatch.setattr(ingest, "_parse_storage_record_slow", no_slow)
     g = torch.Generator().manual_seed(4)
     for dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32, torch.int16,
                torch.int8, torch.uint8, torch.bool):
@@ -213,6 +217,14 @@ def test_storage_records_parsed_without_the_vm():
             got = ingest.decode(payload)["weights"]
             assert torch.equal(got["w"], t) and torch.equal(got["v"], t[1:]), (dt, n)
             assert not ingest._STORAGE_RECORDS, (dt, n)        # the fast parser took every record
+    monkeypatch.undo()
+    # the field-by-field parser agrees with the one-match parser on every record above
+    for dt in (torch.float32, torch.bfloat16, torch.int64, torch.bool):
+        t = torch.ones(300_001, dtype=dt)
+        payload = cloudpickle.dumps({"w": t})
+        mv = memoryview(payload)
+        q = payload.find(b"\x80\x02(X\x07\x00\x00\x00storage")
+        assert ingest._parse_storage_record(mv, q) == ingest._parse_storage_record_slow(mv, q) != None
     # a record naming a storage type outside the allowlist: fast parser declines, the VM refuses
     t = torch.ones(4)
     payload = bytearray(cloudpickle.dumps({"w": t}))
