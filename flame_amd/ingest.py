@@ -633,6 +633,9 @@ class ShmReceiver:
 
 
 # ------------------------------------------------------------------ device-resident cache
+from .slab import SlotWeights  # noqa: E402  (slab imports nothing from this module)
+
+
 class DeviceUpdateCache:
     """``diskcache.Cache`` stand-in that keeps received updates resident on the GPU.
 
@@ -749,6 +752,9 @@ class DeviceUpdateCache:
     def _split_narrow(w):
         """(kernel-dtype keys, bool / uint8 / int8 / int16 keys) of an update that has both."""
         from . import engine
+        codes = engine.DTYPE_CODE
+        if all(not isinstance(v, torch.Tensor) or v.dtype in codes for v in w.values()):
+            return None                       # (the common case, checked without building dicts)
         main = collections.OrderedDict((k, v) for k, v in w.items()
                                        if isinstance(v, torch.Tensor) and v.dtype in engine.DTYPE_CODE)
         if not main or len(main) == len(w):
@@ -782,7 +788,11 @@ class DeviceUpdateCache:
         if ev is not None:
             cur = torch.cuda.current_stream(self._dev())
             cur.wait_event(ev)
-            for v in tres.weights.values():
+            w = tres.weights
+            if isinstance(w, SlotWeights):
+                return      # views of a slab slot: the slab owns the memory; the slot is recycled
+                            # behind an event recorded when these views are dropped (slab.py)
+            for v in w.values():
                 if isinstance(v, torch.Tensor) and v.is_cuda:
                     v.record_stream(cur)
 

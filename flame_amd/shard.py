@@ -651,10 +651,17 @@ class ShardedOptimizer:
         if self.plan is None:
             raise RuntimeError("ShardedOptimizer(accumulate_only): call set_layout(model_weights) first")
         plan, local = self.plan, []
+        local_slab = None         # a slab already known to hold only this rank's slices
         for tres in arrivals:
-            lw = plan.local(tres.weights)
-            local.append(tres if lw is tres.weights else
-                         _SlicedResult(lw, getattr(tres, "count", 0), getattr(tres, "version", 0)))
+            w = tres.weights
+            slab = getattr(w, "slab", None)
+            if slab is not None and slab is local_slab and getattr(w, "ranges", None) is None:
+                local.append(tres)
+                continue
+            lw = plan.local(w)
+            if lw is w and slab is not None and getattr(w, "ranges", None) is None:
+                local_slab = slab
+            local.append(tres if lw is w else _SlicedResult(lw, getattr(tres, "count", 0), getattr(tres, "version", 0)))
         return self.inner.do_arrivals(agg, local, version=version)
 
     def scale_add_agg_weights(self, base_weights, agg_goal_weights, agg_goal: int):

@@ -127,6 +127,7 @@ class UpdateSlab:
         self._ready = {}         # slot -> event the next writer must wait for
         self._stream = None
         self._wt = None          # per-key insert table (see _write_table)
+        self._slot_views = {}    # slot -> [(key, tiled view)] (see views)
         self._ring_bufs = [None] * PINNED_RING      # pinned staging of pageable payloads (_pinned_stage)
         self._ring_events = [None] * PINNED_RING
         self._ring_next = 0
@@ -148,11 +149,13 @@ class UpdateSlab:
         self._free.append(slot)
 
     def views(self, slot: int) -> SlotWeights:
-        """Tiled views of ``slot`` (what the optimizers receive as ``TrainResult.weights``)."""
-        w = SlotWeights()
-        for k in self.keys:
-            dt, _, _, tile0, tiles = self.meta[k]
-            w[k] = self.storage[dt][tile0:tile0 + tiles, slot, :]
+        """Tiled views of ``slot`` (what the optimizers receive as ``TrainResult.weights``).
+        A slot's view tensors are made once and shared by every SlotWeights of that slot (the
+        storage never moves; only the dict and its release hook are per insert)."""
+        cached = self._slot_views.get(slot)
+        if cached is None:
+            cached = self._slot_views[slot] = [(k, self.slot_view(slot, k)) for k in self.keys]
+        w = SlotWeights(cached)
         w._release = lambda s=slot: self._release(s)
         w.shapes = {k: self.meta[k][1] for k in self.keys}
         w.slab, w.slot = self, slot     # lets the engine compute pointer rows without touching views
