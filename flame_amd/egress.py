@@ -196,7 +196,7 @@ class MessageEncoder:
         buf = self._buffer(total)
         out = buf.numpy()
         off = 0
-        copies = False
+        copies = set()          # devices whose streams carry D2H copies into the buffer
         for pc in pieces:
             if isinstance(pc, bytes):
                 out[off:off + len(pc)] = np.frombuffer(pc, dtype=np.uint8)
@@ -208,12 +208,12 @@ class MessageEncoder:
                 src = pc.detach()
                 if src.is_cuda:
                     dst.copy_(src, non_blocking=True)      # D2H straight into the payload
-                    copies = True
+                    copies.add(src.device)
                 else:
                     dst.copy_(src)
             off += nb
-        if copies:
-            torch.cuda.current_stream().synchronize()
+        for d in copies:        # the payload is complete when encode returns
+            torch.cuda.current_stream(d).synchronize()
         assert off == total
         return memoryview(out[:total]).toreadonly()
 

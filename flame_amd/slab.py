@@ -39,6 +39,9 @@ from . import engine
 # pageable payload spans of at least this many bytes are staged through pinned memory
 PINNED_STAGE_MIN = 256 << 10
 PINNED_RING = 4
+# a payload span is staged as one transfer only if it is at most this much larger than the
+# tensor bytes it carries (pickle framing and storage headers are a few hundred bytes per key)
+STAGE_SPAN_SLACK = 1.25
 
 
 class SlotWeights(dict):
@@ -290,8 +293,8 @@ class UpdateSlab:
             base, end = whole.data_ptr(), whole.data_ptr() + whole.numel()
             lo = min(p for _, p, _ in items)
             hi = max(p + n for _, p, n in items)
-            if lo < base or hi > end:
-                continue
+            if lo < base or hi > end or hi - lo > STAGE_SPAN_SLACK * sum(n for _, _, n in items) + (64 << 10):
+                continue      # outside the buffer, or mostly other bytes (e.g. a big non-weight blob)
             span = whole[lo - base:hi - base]
             ring_slot = None
             if not span.is_pinned() and span.numel() >= PINNED_STAGE_MIN:
