@@ -3,7 +3,7 @@
 hierarchy): the middles' arrivals (batched ``FedBuff.do_arrivals`` or one ``do()`` per arrival)
 and the ``hierarchy_round`` launch.  Small P -- only the host side matters here.
 
-    python tools/hier_host_profile.py [batched|per-do] [rounds]
+    python tools/hier_host_profile.py [batched|per-do] [rounds] [--sharded]
 """
 import cProfile
 import os
@@ -33,17 +33,25 @@ def main():
     from flame_amd.slab import UpdateSlab
     mode = sys.argv[1] if len(sys.argv) > 1 else "batched"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    sharded = "--sharded" in sys.argv       # ShardedHierarchy at world 1 (the N > 1 bench's code path)
     M, C, P, rnd = 64, 64, 1 << 20, 10
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16
-    store = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M * C, device=dev)
-    src = {"model": torch.zeros(P, dtype=dt, device=dev)}
+    if sharded:
+        from flame_amd import shard
+        hier = shard.ShardedHierarchy({"model": torch.empty(P, dtype=dt, device="meta")}, device=dev, middles=M)
+        tmpl = hier.plan.local_template()
+        src = {k: torch.zeros(v.shape, dtype=dt, device=dev) for k, v in tmpl.items()}
+    else:
+        tmpl = {"model": torch.empty(P, dtype=dt)}
+        src = {"model": torch.zeros(P, dtype=dt, device=dev)}
+    store = UpdateSlab(tmpl, capacity=M * C, device=dev)
     client_w = [store.put(src) for _ in range(M * C)]
-    mid_store = UpdateSlab({"model": torch.empty(P, dtype=dt)}, capacity=M, device=dev)
+    mid_store = UpdateSlab(tmpl, capacity=M, device=dev)
     mid_w = [mid_store.put(src) for _ in range(M)]
     gw = torch.zeros(P, dtype=dt, device=dev)
     stale = [i % 4 for i in range(M * C)]
-    opts = [optimizer_provider.get("fedbuff") for _ in range(M)]
+    opts = [hier.middle_optimizer() if sharded else optimizer_provider.get("fedbuff") for _ in range(M)]
 
     def arrivals():
         if mode == "batched":
@@ -62,8 +70,9 @@ def main():
         t0 = time.perf_counter()
         aggs = arrivals()
         t1 = time.perf_counter()
-        hierarchy_round([(mid_w[m], aggs[m], C, rnd - (m % 2)) for m in range(M)], None, version=rnd,
-                        top_weights={"model": gw}, top_goal=M)
+        rnd_fn = hier.round if sharded else hierarchy_round
+        rnd_fn([(mid_w[m], aggs[m], C, rnd - (m % 2)) for m in range(M)], None, version=rnd,
+               top_weights={"model": gw}, top_goal=M)
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1
 
@@ -78,7 +87,7 @@ def main():
         torch.cuda.synchronize()
     ta.sort()
     tb.sort()
-    print(f"{mode}: arrivals {ta[len(ta) // 2] * 1e3:.3f} ms, hierarchy_round issue {tb[len(tb) // 2] * 1e3:.3f} ms "
+    print(f"{mode}{' sharded' if sharded else ''}: arrivals {ta[len(ta) // 2] * 1e3:.3f} ms, hierarchy_round issue {tb[len(tb) // 2] * 1e3:.3f} ms "
           f"(medians of {rounds})", flush=True)
     pr = cProfile.Profile()
     pr.enable()
