@@ -962,7 +962,8 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("placement", ["slab", "tensors"])
 @pytest.mark.parametrize("start", ["none", "existing"])
-def test_fedbuff_do_arrivals_equals_per_do(dtype, placement, start):
+@pytest.mark.parametrize("defer", [True, False])
+def test_fedbuff_do_arrivals_equals_per_do(dtype, placement, start, defer):
     """FedBuff.do_arrivals (a middle's round of arrivals in one call) == do() per arrival (the
     async roles, asyncfl/middle_aggregator.py:190-203) == the oracle, bitwise: the aggregate
     read back, and the fused scale_add + delta applied from the queued arrivals."""
@@ -990,7 +991,7 @@ def test_fedbuff_do_arrivals_equals_per_do(dtype, placement, start):
         c = S.SortedCache()
         c[f"{i}"] = S.TR(dev(ups[i]), 1, vers[i])
         agg_p = per.do(agg_p, c, total=1, version=rnd)
-    bat = make_amd("fedbuff")
+    bat = make_amd("fedbuff", defer=defer)       # defer=False: one launch, a plain dict
     agg_b = bat.do_arrivals(start_agg(), [S.TR(dev(ups[i]), 1, vers[i]) for i in range(n)], version=rnd)
     ora, agg_o = O.OracleFedBuff(), ({k: v.clone() for k, v in prev.items()} if start == "existing" else None)
     for i in range(n):
