@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+import sysconfig
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -18,6 +19,9 @@ SRC = os.path.join(PKG, "csrc", "fedagg.hip")
 HDR = os.path.join(ROOT, "include", "flame_amd.h")
 LIB = os.path.join(PKG, "libflame_amd.so")
 ARCH = os.environ.get("FLAME_AMD_ARCH", "gfx950")
+# host side: the restricted pickle VM of flame_amd.ingest (a CPython extension, plain gcc)
+VM_SRC = os.path.join(PKG, "csrc", "pickle_vm.c")
+VM_LIB = os.path.join(PKG, "_pickle_vm" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 HIPCC_FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -40,7 +44,20 @@ def stale() -> bool:
     return any(os.path.getmtime(p) > t for p in (SRC, HDR))
 
 
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """The pickle VM extension (gcc, CPython headers)."""
+    if not force and os.path.exists(VM_LIB) and os.path.getmtime(VM_LIB) >= os.path.getmtime(VM_SRC):
+        return VM_LIB
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-std=c11", "-shared", "-fPIC", "-Wall", "-Wextra", "-Werror",
+           "-Wno-missing-field-initializers", f"-I{sysconfig.get_paths()['include']}", "-o", VM_LIB, VM_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return VM_LIB
+
+
 def build(force: bool = False, verbose: bool = False, extra=None) -> str:
+    build_host(force=force, verbose=verbose)
     if not force and not stale():
         return LIB
     cmd = [hipcc(), *HIPCC_FLAGS, *(extra or []), "-o", LIB, SRC]

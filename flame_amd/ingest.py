@@ -30,6 +30,7 @@ from __future__ import annotations
 import collections
 import enum
 import functools
+import os
 import pickle
 import re
 import struct
@@ -100,7 +101,15 @@ class PayloadDecoder:
         return struct.unpack_from(fmt, self.mv, p)[0], p + n
 
     def load(self, pos=0, persistent_load=None):
-        """Run one pickle starting at ``pos``; return (object, end position)."""
+        """Run one pickle starting at ``pos``; return (object, end position).  The opcode loop
+        is the C one (``csrc/pickle_vm.c``, same opcodes, same allowlist calls) unless
+        ``FLAME_AMD_PICKLE_VM=py`` selects :meth:`load_py`."""
+        if _VM is None:
+            return self.load_py(pos, persistent_load)
+        return _VM.load(self.mv, pos, self._find, self._call, _Span, persistent_load, _load_from_bytes_marker)
+
+    def load_py(self, pos=0, persistent_load=None):
+        """The opcode loop in Python (the C loop's specification; differential-tested)."""
         mv = self.mv
         stack, memo, marks = [], {}, []
         push, pop, call = stack.append, stack.pop, self._call     # (hot loop: locals, not attributes)
@@ -130,6 +139,8 @@ class PayloadDecoder:
                 marks.append(len(stack))
             elif op == 0x74:    # TUPLE
                 k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
                 stack[k:] = [tuple(stack[k:])]
             elif op in (0x43, 0x42, 0x8E):  # SHORT_BINBYTES, BINBYTES, BINBYTES8: keep a SPAN, no copy
                 if op == 0x43:
@@ -141,7 +152,9 @@ class PayloadDecoder:
                 else:
                     n = int.from_bytes(mv[p:p + 8], "little")
                     p += 8
-                push(_Span(p, n))
+                # the argument of torch.storage._load_from_bytes (on top of the stack): a span
+                # of the payload, no copy; any other bytes value is a bytes object
+                push(_Span(p, n) if stack and stack[-1] is _load_from_bytes_marker else bytes(mv[p:p + n]))
                 p += n
             elif op == 0x29:    # EMPTY_TUPLE
                 push(())
@@ -193,15 +206,25 @@ class PayloadDecoder:
                 stack.append(None)
             elif op == 0x88:    # NEWTRUE
                 stack.append(True)
-            elif op == 0x86:    # TUPLE2
-                stack[-2:] = [tuple(stack[-2:])]
-            elif op == 0x87:    # TUPLE3
-                stack[-3:] = [tuple(stack[-3:])]
+            elif op == 0x86 or op == 0x87:    # TUPLE2, TUPLE3
+                k = len(stack) - (op - 0x84)
+                if k < 0:
+                    raise IndexError("stack underflow")
+                stack[k:] = [tuple(stack[k:])]
+            elif op == 0x91:    # FROZENSET
+                k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
+                stack[k:] = [frozenset(stack[k:])]
             elif op == 0x6C:    # LIST
                 k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
                 stack[k:] = [list(stack[k:])]
             elif op == 0x65:    # APPENDS
                 k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
                 items = stack[k:]
                 del stack[k:]
                 stack[-1].extend(items)
@@ -210,6 +233,8 @@ class PayloadDecoder:
                 stack[-1].append(v)
             elif op == 0x75:    # SETITEMS
                 k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
                 items = stack[k:]
                 del stack[k:]
                 d = stack[-1]
@@ -221,6 +246,8 @@ class PayloadDecoder:
                 stack[-1][key] = v
             elif op == 0x90:    # ADDITEMS
                 k = marks.pop()
+                if k > len(stack):
+                    raise IndexError("stack underflow below MARK")
                 items = stack[k:]
                 del stack[k:]
                 stack[-1].update(items)
@@ -273,6 +300,17 @@ class PayloadDecoder:
         if not isinstance(span, _Span):
             raise pickle.UnpicklingError("storage bytes expected")
         q = span.start
+        if _VM is not None and _STORAGE_HEADERS:
+            # the common case in C: a validated header, then torch's record layout (the same
+            # checks as below; None = anything else, parsed the long way)
+            hit = _VM.storage_head(self.mv, q, span.start + span.n, _STORAGE_HEADERS)
+            if hit is not None:
+                dtype = _STORAGE_DTYPES.get(hit[0])
+                if dtype is not None:
+                    numel, q = hit[1], hit[2]
+                    if q + numel * dtype.itemsize > span.start + span.n:
+                        raise pickle.UnpicklingError("storage runs past its bytes")
+                    return _StorageRef(self.buf, q, numel, dtype)
         # magic, protocol and sys-info pickles: the same bytes before every storage of a
         # payload, so a header already parsed and checked is skipped by a byte compare
         for h in _STORAGE_HEADERS:
@@ -434,10 +472,35 @@ class _Span:
 _load_from_bytes_marker = object()
 
 
+def _pickle_vm():
+    """The C opcode loop (built in-tree by ``flame_amd.build``); ``FLAME_AMD_PICKLE_VM=py``
+    selects the Python loop instead.  Missing while not opted out: an ImportError naming the
+    build step, not a silent slow path."""
+    if os.environ.get("FLAME_AMD_PICKLE_VM", "c") == "py":
+        return None
+    try:
+        from . import _pickle_vm
+    except ImportError as e:
+        raise ImportError("flame_amd._pickle_vm is not built: run `python -m flame_amd.build` "
+                          "(or set FLAME_AMD_PICKLE_VM=py)") from e
+    return _pickle_vm
+
+
+_VM = _pickle_vm()
+
+
 def _codecs_encode(text, encoding="latin1"):
     if encoding != "latin1":
         raise pickle.UnpicklingError("only latin1-encoded bytes are allowed")
     return text.encode("latin1")
+
+
+def _bytes_like(cls, *args):
+    """bytes / bytearray as pickles rebuild them (``cls()``, ``cls(data[, encoding])``); never
+    ``cls(n)``, which would allocate n zero bytes on the sender's say-so."""
+    if args and not isinstance(args[0], (bytes, bytearray, str)):
+        raise pickle.UnpicklingError(f"{cls.__name__}() from {type(args[0]).__name__} is not allowed")
+    return cls(*args)
 
 
 def _allow(fn):
@@ -456,10 +519,14 @@ def _default_globals():
         ("collections", "OrderedDict"): collections.OrderedDict,
         ("builtins", "set"): set,
         ("builtins", "frozenset"): frozenset,
-        ("builtins", "bytearray"): bytearray,
+        ("builtins", "bytearray"): _allow(functools.partial(_bytes_like, bytearray)),
+        ("builtins", "bytes"): _allow(functools.partial(_bytes_like, bytes)),
         ("builtins", "complex"): complex,
         ("_codecs", "encode"): _allow(_codecs_encode),
     }
+    for (mod, name), v in list(g.items()):     # protocols <= 2 name builtins the Python-2 way
+        if mod == "builtins":
+            g[("__builtin__", name)] = v
     for name, dt in _STORAGE_DTYPES.items():
         g[("torch", name)] = dt
     try:  # flame's message keys (lib/python/flame/common/constants.py MessageType)
