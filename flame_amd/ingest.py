@@ -77,8 +77,9 @@ def _rebuild_tensor_v2(storage, storage_offset, size, stride, requires_grad=Fals
                        metadata=None):
     if not isinstance(storage, _StorageRef):
         raise pickle.UnpicklingError("tensor rebuild without a storage")
-    base = storage.tensor()
-    t = base.as_strided(tuple(size), tuple(stride), storage_offset)
+    t = storage.tensor()
+    if not (storage_offset == 0 and len(size) == 1 and size[0] == storage.numel and tuple(stride) == (1,)):
+        t = t.as_strided(tuple(size), tuple(stride), storage_offset)     # (a whole 1-D storage is `t` itself)
     # the payload buffer the view reads: UpdateSlab.write copies one update's tensors that
     # share a payload with ONE host->device transfer (flame_amd/slab.py)
     t._flame_payload = storage.buf
