@@ -34,6 +34,13 @@ def guarded(data: bytes) -> memoryview:
 
 
 def main():
+    if "--lib" in sys.argv:          # another build of the C loop (e.g. the UBSan one)
+        import importlib.util
+        path = sys.argv[sys.argv.index("--lib") + 1]
+        spec = importlib.util.spec_from_file_location("flame_amd._pickle_vm", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        ingest._VM = mod
     assert ingest._VM is not None
     g = torch.Generator().manual_seed(0)
     msgs = [{"weights": {"a": torch.randn(3, 4, generator=g), "b": torch.arange(5).to(torch.int16),

@@ -175,6 +175,20 @@ def test_no_read_past_the_buffer_guard_page():
     assert "guard ok" in r.stdout
 
 
+def test_guard_page_run_under_ubsan(tmp_path):
+    """The same run with the C loop built with -fsanitize=undefined (no recovery): any
+    undefined behaviour (overflowing shifts, misaligned or null access) aborts the child."""
+    import sysconfig
+    from flame_amd import build as B
+    lib = str(tmp_path / ("_pickle_vm" + sysconfig.get_config_var("EXT_SUFFIX")))
+    subprocess.check_call(["gcc", "-O1", "-g", "-std=c11", "-shared", "-fPIC", "-fsanitize=undefined",
+                           "-fno-sanitize-recover=all", f"-I{sysconfig.get_paths()['include']}", "-o", lib, B.VM_SRC])
+    r = subprocess.run([sys.executable, os.path.join(HERE, "pickle_vm_guard.py"), "--lib", lib], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "runtime error" not in r.stderr, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    assert "guard ok" in r.stdout
+
+
 def test_refusals_are_identical():
     """Globals outside the allowlist, BUILD with state, persistent ids: refused by both loops
     with the same error (nothing executed)."""
