@@ -207,3 +207,36 @@ extern "C" int probe_read_subrow(const void* p, int64_t bytes, void* out, int64_
     else hipLaunchKernelGGL((read_subrow_kernel<64, 16>), grid, dim3(64), 0, st, (const uint8_t*)p, region, S, rows, (uint32_t*)out);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Group-major ("blocked") layout probe: the buffer is G groups, each holding one B-byte block
+// per workgroup; workgroup w reads block w of group 0, then of group 1, ... (B contiguous bytes,
+// UN 4 KiB steps in flight).  Concurrent workgroups then stream ONE group's neighbouring blocks
+// (a contiguous window) instead of each its own far-apart region -- the question of a
+// group-major update slab.
+template <int UN>
+__global__ __launch_bounds__(256) void read_blocked_kernel(const uint8_t* __restrict__ p, int64_t B, int G,
+                                                           uint32_t* out) {
+    const int64_t nwg = gridDim.x;
+    uint32_t acc = 0;
+    for (int g = 0; g < G; ++g) {
+        const uint8_t* base = p + ((int64_t)g * nwg + blockIdx.x) * B + threadIdx.x * 16;
+        for (int64_t off = 0; off + UN * 4096 <= B; off += UN * 4096) {
+            u4 v[UN];
+#pragma unroll
+            for (int u = 0; u < UN; ++u)
+                v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(base + off + u * 4096));
+#pragma unroll
+            for (int u = 0; u < UN; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+extern "C" int probe_read_blocked(const void* p, int64_t bytes, void* out, int64_t B, int G, void* stream) {
+    if (B < 16 * 4096 || B % (16 * 4096) || G < 1) return 2;
+    const int64_t nwg = bytes / (B * G);
+    if (nwg < 1 || nwg > 0x7FFFFFFF) return 2;
+    hipLaunchKernelGGL((read_blocked_kernel<16>), dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)p, B, G, (uint32_t*)out);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
