@@ -22,6 +22,7 @@ reference.  ``d_t`` is not materialised by the fused path; it is computed
 lazily from ``agg_weights`` and the previous ``current_weights`` on access.
 """
 import logging
+import os
 from abc import abstractmethod
 from collections import OrderedDict
 
@@ -41,6 +42,10 @@ class FedOPT(FedAvg):
     """FedOPT class."""
 
     variant = None  # "fedadam" | "fedyogi" | "fedadagrad"
+    # two launches per dtype instead of one: the FedAvg reduction (flame_agg_reduce, avg written
+    # into base) and then the adaptive step over avg/cur/m/v alone (flame_fedopt_reduce_adapt
+    # with no clients) -- bit-identical; which is faster is measured in DESIGN.md §4
+    split_launch = os.environ.get("FLAME_AMD_FEDOPT_SPLIT", "0") == "1"
 
     def __init__(self, beta_1, beta_2, eta, tau):
         super().__init__()
@@ -149,9 +154,16 @@ class FedOPT(FedAvg):
                 self.v_t[k] = engine._as_device(self.v_t[k], device)
             ms.append(self.m_t[k])
             vs.append(self.v_t[k])
-        engine.fedopt_reduce_adapt_(self.variant, [t.dev for t in targets], [t.dev for t in targets], curs,
-                                    outs, ms, vs, [[w[k] for w, _ in entries] for k in ks],
-                                    [r for _, r in entries], hyper, state_zero)
+        avgs = [t.dev for t in targets]
+        clients = [[w[k] for w, _ in entries] for k in ks]
+        rates = [r for _, r in entries]
+        if self.split_launch:
+            engine.reduce_(avgs, avgs, clients, rates)
+            engine.fedopt_reduce_adapt_(self.variant, [None] * len(ks), avgs, curs, outs, ms, vs,
+                                        [[] for _ in ks], [], hyper, state_zero)
+        else:
+            engine.fedopt_reduce_adapt_(self.variant, avgs, avgs, curs, outs, ms, vs, clients, rates, hyper,
+                                        state_zero)
         for t in targets:
             t.writeback()
         new_cur.update(zip(ks, outs))

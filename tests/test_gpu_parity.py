@@ -1712,6 +1712,47 @@ def test_fedopt_argmeta_equals_device_table(sort, dtype):
         S.assert_bitwise(f"{sort}/{dtype}/round{r}", a, b)
 
 
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
+@pytest.mark.parametrize("case", ["f32_slab", "bf16_slab", "f16_tensors", "f32_big"])
+def test_fedopt_split_launch_equals_fused(sort, case):
+    """FedOPT.split_launch (the FedAvg reduction, then the adaptive step as a no-client
+    flame_fedopt_reduce_adapt) == the one fused launch, bitwise: avg, cur, m, v over three
+    rounds (passthrough, zero state, running state).  f32_big takes the multi-chunk workgroup
+    path (FLAME_OPT_WGC) of the fused kernel."""
+    from flame_amd.optimizer.fedopt import FedOPT
+    from flame_amd.slab import UpdateSlab
+    dtype = {"f32_slab": torch.float32, "bf16_slab": torch.bfloat16, "f16_tensors": torch.float16,
+             "f32_big": torch.float32}[case]
+    g = torch.Generator().manual_seed(23)
+    shapes = {"w": (20_000_000,)} if case == "f32_big" else {"w": (300, 7), "b": (7,), "t": (4099,)}
+    n = 3 if case == "f32_big" else 6
+    w0 = {k: torch.randn(sh, generator=g).to(dtype) for k, sh in shapes.items()}
+    rounds = [[({k: (torch.randn(sh, generator=g) * 1e-2).to(dtype) for k, sh in shapes.items()}, 10 + 7 * i)
+               for i in range(n)] for _ in range(3)]
+    results = {}
+    for split in (False, True):
+        FedOPT.split_launch = split
+        try:
+            opt = make_amd(sort)
+            slab = UpdateSlab({k: torch.empty(sh, dtype=dtype) for k, sh in shapes.items()}, capacity=n, device=DEV) \
+                if case.endswith("slab") else None
+            w = {k: v.to(DEV) for k, v in w0.items()}
+            outs = []
+            for arrivals in rounds:
+                cache = S.SortedCache()
+                for i, (u, c) in enumerate(arrivals):
+                    ud = {k: v.to(DEV) for k, v in u.items()}
+                    cache[f"{i:03d}"] = S.TR(slab.put(ud) if slab is not None else ud, c)
+                w = opt.do({k: v.clone() for k, v in w.items()}, cache, total=sum(c for _, c in arrivals))
+                outs.append([S.to_cpu(dict(x)) for x in (w, opt.agg_weights, opt.m_t or {}, opt.v_t or {})])
+            results[split] = outs
+        finally:
+            FedOPT.split_launch = False
+    for r, (a, b) in enumerate(zip(results[False], results[True])):
+        for lbl, x, y in zip(("cur", "avg", "m", "v"), a, b):
+            S.assert_bitwise(f"{sort}/{case}/round{r}/{lbl}", x, y)
+
+
 def test_key_subset_arrivals():
     """Updates carrying a SUBSET of the model's keys (fedavg.py:93 / fedbuff.py:143 add
     ``for k, v in tres.weights.items()``: a key a client did not send keeps its value).
