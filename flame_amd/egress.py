@@ -32,7 +32,7 @@ import torch
 from .ingest import LEGACY_MAGIC, _STORAGE_DTYPES
 
 _STORAGE_NAME = {dt: name for name, dt in _STORAGE_DTYPES.items()}
-_MARK = b"\xfa\x1aFLAMEAMD"                 # 10 bytes + 6-byte index: a tensor's placeholder
+_MARK_LEN = 10                               # random mark (per encode) + 6-byte index: a tensor's placeholder
 _HEADER = None                               # torch's legacy stream header (magic, protocol, sys info)
 
 
@@ -126,9 +126,10 @@ class _SkeletonPickler(_pickler_base()):
     """cloudpickle (protocol 3: no frames) with every tensor replaced by torch's reduce over a
     16-byte placeholder storage; the tensors are collected in pickling order."""
 
-    def __init__(self, f, tensors: List[torch.Tensor]):
+    def __init__(self, f, tensors: List[torch.Tensor], mark: bytes):
         super().__init__(f, protocol=3)
         self._tensors = tensors
+        self._mark = mark
 
     def reducer_override(self, obj):
         if isinstance(obj, torch.Tensor):
@@ -142,7 +143,7 @@ class _SkeletonPickler(_pickler_base()):
                 stride.append(acc)
                 acc *= d
             return (torch._utils._rebuild_tensor_v2,
-                    (_StoragePlaceholder(_MARK + i.to_bytes(6, "little")), 0, shape, tuple(reversed(stride)), False,
+                    (_StoragePlaceholder(self._mark + i.to_bytes(6, "little")), 0, shape, tuple(reversed(stride)), False,
                      collections.OrderedDict()))
         sup = getattr(super(), "reducer_override", None)
         return sup(obj) if sup is not None else NotImplemented
@@ -172,13 +173,15 @@ class MessageEncoder:
     def encode(self, message: Any) -> memoryview:
         tensors: List[torch.Tensor] = []
         f = io.BytesIO()
-        _SkeletonPickler(f, tensors).dump(message)
+        # a fresh random mark per message: no bytes of the message itself can pass for a placeholder
+        mark = os.urandom(_MARK_LEN)
+        _SkeletonPickler(f, tensors, mark).dump(message)
         skel = f.getvalue()
         # the placeholders, in order: SHORT_BINBYTES 16 <mark i> -> the storage's whole stream,
         # its raw bytes 64-byte aligned in the payload (so a device tensor lands by one aligned DMA)
         pieces, pos, off = [], 0, 0
         for i, t in enumerate(tensors):
-            ph = b"C\x10" + _MARK + i.to_bytes(6, "little")
+            ph = b"C\x10" + mark + i.to_bytes(6, "little")
             j = skel.find(ph, pos)
             if j < 0:
                 raise RuntimeError("flame_amd.egress: placeholder not found in the skeleton")
