@@ -189,6 +189,31 @@ def test_guard_page_run_under_ubsan(tmp_path):
     assert "guard ok" in r.stdout
 
 
+def test_under_asan(tmp_path):
+    """The guard-page fuzz and the differential tests with the C loop built with
+    -fsanitize=address,undefined, inside an ASan-linked embedded CPython (tests/asan/py_embed.c)
+    with PYTHONMALLOC=malloc, so the loop's own stack / mark arrays and every object it makes
+    are ASan-checked heap."""
+    import sysconfig
+    from flame_amd import build as B
+    inc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR")
+    ver = sysconfig.get_config_var("LDVERSION")
+    san = ["-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"]
+    exe = str(tmp_path / "py_embed")
+    lib = str(tmp_path / ("_pickle_vm" + sysconfig.get_config_var("EXT_SUFFIX")))
+    subprocess.check_call(["gcc", *san, os.path.join(HERE, "asan", "py_embed.c"), f"-I{inc}", f"-L{libdir}",
+                           f"-lpython{ver}", "-lcrypt", "-ldl", "-lm", "-o", exe])
+    subprocess.check_call(["gcc", *san, "-std=c11", "-shared", "-fPIC", f"-I{inc}", "-o", lib, B.VM_SRC])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:detect_odr_violation=0:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", PYTHONMALLOC="malloc")
+    r = subprocess.run([exe, os.path.join(HERE, "asan", "run_pickle_vm.py"), lib], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, \
+        (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert "asan run ok" in r.stdout
+
+
 def test_refusals_are_identical():
     """Globals outside the allowlist, BUILD with state, persistent ids: refused by both loops
     with the same error (nothing executed)."""
