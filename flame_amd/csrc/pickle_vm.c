@@ -248,6 +248,18 @@ static PyObject *vm_load(PyObject *self, PyObject *args) {
             p += (Py_ssize_t)len;
             break;
         }
+        case 0x96: {                                   /* BYTEARRAY8 (protocol 5) */
+            NEED(8);
+            const uint64_t len = le(b + p, 8);
+            p += 8;
+            if (len > (uint64_t)(n - p)) {
+                malformed("truncated");
+                goto fail;
+            }
+            PUSH(PyByteArray_FromStringAndSize((const char *)b + p, (Py_ssize_t)len));
+            p += (Py_ssize_t)len;
+            break;
+        }
         case 0x85: {                                   /* TUPLE1 */
             TOP_OR_FAIL();
             PyObject *t = PyTuple_New(1);

@@ -157,6 +157,13 @@ class PayloadDecoder:
                 # of the payload, no copy; any other bytes value is a bytes object
                 push(_Span(p, n) if stack and stack[-1] is _load_from_bytes_marker else bytes(mv[p:p + n]))
                 p += n
+            elif op == 0x96:    # BYTEARRAY8 (protocol 5)
+                n = int.from_bytes(mv[p:p + 8], "little")
+                p += 8
+                if p + n > len(mv):
+                    raise IndexError("truncated")
+                push(bytearray(mv[p:p + n]))
+                p += n
             elif op == 0x29:    # EMPTY_TUPLE
                 push(())
             elif op == 0x89:    # NEWFALSE

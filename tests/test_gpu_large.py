@@ -141,3 +141,64 @@ def test_fedadam_past_2_31_elements():
             S.assert_close_fedopt("fedadam/r1/v", {"w": _at(opt.v_t["w"], idx)}, ora.v_t)
     del cur, opt
     _free()
+
+
+@pytest.mark.parametrize("placement", ["slab", "tensors"])
+def test_bf16_hierarchy_round_past_2_31_elements(placement):
+    """Config 5's kernel (flame_hier_fedbuff, middles + top in one pass) on one bf16 key of
+    2^31 + 4099 elements: 2 middles x 2 arrivals, middle weights, deltas, top aggregate and
+    top weights against the oracle's op sequence at the sampled elements, bitwise."""
+    from oracle import oracle as O
+    from flame_amd import engine
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    from flame_amd.slab import UpdateSlab
+    M, C, rnd, goals, mid_ver, top_goal = 2, 2, 9, [2, 3], [9, 8], 2
+    vers = [[9, 7], [8, 9]]
+    _need(12 * P * 2 / 1e9 + 2)
+    idx = _index()
+
+    def bf(seed, stream, sigma):
+        t = torch.empty(P, dtype=torch.bfloat16, device=DEV)
+        engine.synth_fill_(t, seed, stream, 0, sigma)
+        return t
+    ups = [[bf(12, 1 + m * C + t, 1e-2) for t in range(C)] for m in range(M)]
+    mids = [bf(12, 100 + m, 1.0) for m in range(M)]
+    top_w = bf(12, 200, 1.0)
+    u_s = [[_at(u, idx) for u in row] for row in ups]
+    mid_s, top_s = [_at(x, idx) for x in mids], _at(top_w, idx)
+    slab = UpdateSlab({"w": torch.empty(P, dtype=torch.bfloat16, device="meta")}, capacity=M * C, device=DEV) \
+        if placement == "slab" else None
+    aggs = []
+    for m in range(M):
+        opt, agg = _make("fedbuff"), None
+        for t in range(C):
+            c = S.SortedCache()
+            c["a"] = S.TR(slab.put({"w": ups[m][t]}) if slab is not None else {"w": ups[m][t]}, 1, vers[m][t])
+            agg = opt.do(agg, c, total=1, version=rnd)
+        aggs.append(agg)
+    if slab is not None:
+        del ups
+        _free()
+    mids_w = [{"w": x} for x in mids]
+    top_agg, deltas = hierarchy_round([(mids_w[m], aggs[m], goals[m], mid_ver[m]) for m in range(M)], None,
+                                      version=rnd, top_weights={"w": top_w}, top_goal=top_goal, with_delta=True)
+    top_o, top_agg_o = O.OracleFedBuff(), None
+    for m in range(M):
+        mo, agg_o = O.OracleFedBuff(), None
+        for t in range(C):
+            c = S.SortedCache()
+            c["a"] = S.TR({"w": u_s[m][t]}, 1, vers[m][t])
+            agg_o = mo.do(agg_o, c, total=1, version=rnd)
+        w = {"w": mid_s[m].clone()}
+        d = {"w": O.scale_add_tensor(w["w"], agg_o["w"], goals[m], want_delta=True)}
+        S.assert_bitwise(f"hier/{placement}/mid{m}", {"w": _at(mids[m], idx)}, w)
+        S.assert_bitwise(f"hier/{placement}/delta{m}", {"w": _at(deltas[m]["w"], idx)}, d)
+        c = S.SortedCache()
+        c["d"] = S.TR(d, 1, mid_ver[m])
+        top_agg_o = top_o.do(top_agg_o, c, total=1, version=rnd)
+    S.assert_bitwise(f"hier/{placement}/top agg", {"w": _at(top_agg["w"], idx)}, top_agg_o)
+    tw = {"w": top_s.clone()}
+    top_o.scale_add_agg_weights(tw, top_agg_o, top_goal)
+    S.assert_bitwise(f"hier/{placement}/top w", {"w": _at(top_w, idx)}, tw)
+    del mids, top_w, aggs, deltas, top_agg
+    _free()

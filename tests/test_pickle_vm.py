@@ -223,6 +223,16 @@ def test_refusals_are_identical():
     bad = [pickle.dumps(Evil(), protocol=p) for p in (2, 4, 5)]
     bad.append(pickle.dumps(collections.Counter(a=1), protocol=4))        # BUILD / non-allowlisted
     bad.append(b"\x80\x04\x95\x05\x00\x00\x00\x00\x00\x00\x00N\x51.")         # BINPERSID
+    # bytes / bytearray rebuilt from a size (n zero bytes allocated on the sender's say-so)
+    bad.append(b"\x80\x02c__builtin__\nbytearray\nJ\x00\x00\x00\x40\x85R.")
+    bad.append(b"\x80\x03cbuiltins\nbytes\nJ\x00\x00\x00\x40\x85R.")
     for pl in bad:
         a, b = _decode(pl, ingest._VM), _decode(pl, None)
         assert a == b == ("err", pickle.UnpicklingError), (pl, a, b)
+    # ... while the forms pickles actually use still decode
+    for v in (b"", bytearray(b"xyz"), b"\x00\xff" * 5):
+        for proto in (2, 3, 5):
+            pl = pickle.dumps({"v": v}, protocol=proto)
+            for vm in (ingest._VM, None):
+                got = _decode(pl, vm)
+                assert got[0] == "ok" and got[1]["v"] == v and type(got[1]["v"]) is type(v), (v, proto, got)
