@@ -167,7 +167,7 @@ class _Staging:
             host = host.pin_memory()
         except RuntimeError:
             pass
-        cur = torch.cuda.current_stream(device)
+        cur = current_stream(device)
         side = self._streams.get(device)
         if side is None:
             side = self._streams[device] = torch.cuda.Stream(device)
@@ -201,7 +201,7 @@ class _Staging:
         A view into a sender's shared-memory segment is instead waited for here: the sender
         may rewrite the segment once the launching call has returned (shm_lease)."""
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
+        ev.record(current_stream(device))
         if shm_lease.aliases(host_tensor):
             ev.synchronize()
             return
@@ -227,13 +227,13 @@ class _timed:
         self.on = kernel_events is not None or bool(_recorders)
         if self.on:
             self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e0.record(torch.cuda.current_stream(self.device))
+            self.e0.record(current_stream(self.device))
         return self
 
     def __exit__(self, *exc):
         if self.on and exc[0] is None:
             e1 = torch.cuda.Event(enable_timing=True)
-            e1.record(torch.cuda.current_stream(self.device))
+            e1.record(current_stream(self.device))
             ev = (self.name, self.e0, e1, self.nbytes)
             if kernel_events is not None:
                 kernel_events.append(ev)
@@ -242,14 +242,35 @@ class _timed:
         return False
 
 
+def _dev_index(device) -> int:
+    device = torch.device(device) if not isinstance(device, torch.device) else device
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
 def _stream_ptr(device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """The raw HIP stream torch's current stream is on ``device`` (no Stream object made)."""
+    return torch._C._cuda_getCurrentRawStream(_dev_index(device))
+
+
+_STREAMS = {}
+
+
+def current_stream(device) -> torch.cuda.Stream:
+    """``torch.cuda.current_stream(device)``, the Stream object kept per (device, raw stream):
+    torch's own call builds a new one each time, several per launch on the small-round path.
+    (torch's pooled streams are never destroyed, so a raw pointer names one stream for good.)"""
+    idx = _dev_index(device)
+    key = (idx, torch._C._cuda_getCurrentRawStream(idx))
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.current_stream(idx)
+    return st
 
 
 def _keepalive(tensors, device):
     """Call AFTER the launch: device tensors join the stream's allocator bookkeeping,
     zero-copy host tensors are held until an event recorded behind the kernel fires."""
-    st = torch.cuda.current_stream(device)
+    st = current_stream(device)
     for t in tensors:
         if t.is_cuda:
             t.record_stream(st)

@@ -861,8 +861,8 @@ class DeviceUpdateCache:
 
     def _order(self, ev, tres):
         if ev is not None:
-            cur = torch.cuda.current_stream(self._dev())
-            cur.wait_event(ev)
+            from . import engine
+            engine.current_stream(self._dev()).wait_event(ev)
             w = tres.weights
             if isinstance(w, SlotWeights):
                 return      # views of a slab slot: the slab owns the memory; the slot is recycled

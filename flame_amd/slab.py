@@ -147,7 +147,7 @@ class UpdateSlab:
     def _release(self, slot: int) -> None:
         if torch.cuda.is_available():
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
+            ev.record(engine.current_stream(self.device))
             self._ready[slot] = ev
         self._free.append(slot)
 
@@ -201,7 +201,8 @@ class UpdateSlab:
         registered or pageable): ``flame_slab_write_2d``, one pitched copy-engine transfer per
         key, no staging tensor.
         """
-        st = stream or torch.cuda.current_stream(self.device)
+        cur = engine.current_stream(self.device)
+        st = stream or cur
         ev = self._ready.pop(slot, None)
         if ev is not None:
             st.wait_event(ev)
@@ -243,7 +244,7 @@ class UpdateSlab:
         if dev_rows:
             tab = np.asarray(dev_rows, dtype=np.uint64).view(np.int64)
             N.check(L.flame_slab_write(tab.ctypes.data, len(dev_rows), st.cuda_stream))
-            if st != torch.cuda.current_stream(self.device):
+            if st != cur:
                 for t in keep:
                     if t.is_cuda:
                         t.record_stream(st)       # read on `st`: keep the caching allocator off it
@@ -270,7 +271,7 @@ class UpdateSlab:
         wt = self._write_table()
         tab = np.asarray([(src.data_ptr(), int(wt[i, 0]) + slot * N.FLAME_TILE_BYTES, int(wt[i, 1]), int(wt[i, 2]))],
                          dtype=np.uint64).view(np.int64)
-        N.check(N.lib().flame_slab_write(tab.ctypes.data, 1, torch.cuda.current_stream(self.device).cuda_stream))
+        N.check(N.lib().flame_slab_write(tab.ctypes.data, 1, engine._stream_ptr(self.device)))
 
     def _stage_payloads(self, host_rows, keep, st, staged):
         """Host rows whose tensors are views into ONE decoded channel payload
