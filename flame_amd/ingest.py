@@ -862,7 +862,8 @@ class DeviceUpdateCache:
     def _order(self, ev, tres):
         if ev is not None:
             from . import engine
-            engine.current_stream(self._dev()).wait_event(ev)
+            cur = engine.current_stream(self._dev())
+            cur.wait_event(ev)
             w = tres.weights
             if isinstance(w, SlotWeights):
                 return      # views of a slab slot: the slab owns the memory; the slot is recycled
