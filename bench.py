@@ -326,12 +326,13 @@ def kernel_stats(events, name):
             "achieved_GBps": total_b / total_t / 1e9}
 
 
-def read_ceiling(buf: torch.Tensor, reps: int = 5):
+def read_ceiling(buf: torch.Tensor, reps: int = 5, regions=()):
     """Same-device HBM streaming-read ceiling over an existing buffer (tools/hbm_probe.hip):
     the best of a grid-stride read (16,384 workgroups, 16 nt dwordx4 loads in flight per
     lane) and a region-streaming read (each workgroup one contiguous 1 MiB region, 16 loads
     per lane -- the product kernel's access pattern with the fastest region size measured).
-    Returns (best GB/s, {probe: GB/s})."""
+    ``regions``: further region sizes (bytes) to probe the same way, e.g. a kernel's own
+    per-workgroup region when it differs from 1 MiB.  Returns (best GB/s, {probe: GB/s})."""
     import ctypes
     import subprocess
     so = os.path.join(ROOT, "build", "hbm_probe.so")
@@ -355,6 +356,9 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5):
         "region_1MiB_16ld": lambda: L.probe_read_region(buf.data_ptr(), nbytes, out.data_ptr(), 1 << 20, 1 << 20,
                                                         16, st),
     }
+    for r in regions:
+        probes[f"region_{r >> 20}MiB_16ld"] = (lambda r=r: L.probe_read_region(buf.data_ptr(), nbytes, out.data_ptr(),
+                                                                             r, r, 16, st))
     res = {}
     for name, launch in probes.items():
         ts = []
@@ -1012,6 +1016,11 @@ def bench_hier(args, world, rank, dev):
     step = {"fused": step_fused, "group": step_group, "serial": step_serial, "sync": step_sync,
             "sync_serial": step_sync_serial}[args.hier_mode]
     elapsed, events = timed(world, args.steps, args.warmup, step)
+    ceiling, probes = None, {}
+    if rank == 0 and world == 1:
+        # the same-process read ceiling over the slab, with the kernel's own per-workgroup region
+        # (every arrival's tile of one chunk: M x C x 4 KiB) beside the fastest (1 MiB) one
+        ceiling, probes = read_ceiling(store.storage[dt], regions=(M * C * 4096,))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_clients > 0 and not args.hier_mode.startswith("sync"):
         cpu = cpu_baseline_hier([store.read(i, "model").cpu() for i in range(C)], P, stale[:C], rnd,
@@ -1046,7 +1055,12 @@ def bench_hier(args, world, rank, dev):
                                         "arrivals": args.hier_arrivals},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,
-                         "kernel": names[0]},
+                         "kernel": names[0], "kernel_ms": red["avg_s"] * 1e3,
+                         "algorithmic_bytes": red["bytes_per_launch"],
+                         "measured_read_ceiling_GBps": ceiling, "read_probes_GBps": probes,
+                         "frac_of_measured_ceiling": red["achieved_GBps"] / ceiling if ceiling else None,
+                         "frac_of_own_region_probe": (red["achieved_GBps"] / probes[f"region_{(M * C * 4096) >> 20}MiB_16ld"]
+                                                      if f"region_{(M * C * 4096) >> 20}MiB_16ld" in probes else None)},
             "kernels": {**kst, "kernel_ms_per_step": per_step_kernel * 1e3,
                         "kernel_client_params_per_s": M * C * P / per_step_kernel},
             "cpu_baseline": cpu,

@@ -240,3 +240,42 @@ extern "C" int probe_read_blocked(const void* p, int64_t bytes, void* out, int64
                        (const uint8_t*)p, B, G, (uint32_t*)out);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Per-wave regions: each 64-lane wave streams ONE contiguous region [g*R, (g+1)*R) in 1 KiB
+// steps (64 lanes x 16 B), UN steps in flight; g = blockIdx.x * waves_per_block + wave.  With
+// 256-lane blocks the four waves of a block stream four neighbouring regions -- what a slab
+// with 1 KiB tiles ([tile][slot][1 KiB]) would hand the hierarchy kernel's workgroup (one
+// tile row per wave); with 64-lane blocks each block streams its own region.
+template <int UN>
+__global__ __launch_bounds__(256) void read_wave_region_kernel(const uint8_t* __restrict__ p, int64_t region,
+                                                               int64_t bytes, uint32_t* out) {
+    const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t b0 = g * region;
+    const int64_t b1 = b0 + region < bytes ? b0 + region : bytes;
+    uint32_t acc = 0;
+    int64_t off = b0 + (threadIdx.x & 63) * 16;
+    for (; off + (UN - 1) * 1024 + 16 <= b1; off += UN * 1024) {
+        u4 v[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            v[u] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u4*)(p + off + u * 1024));
+#pragma unroll
+        for (int u = 0; u < UN; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    for (; off + 16 <= b1; off += 1024) {
+        u4 v = *(const u4*)(p + off);
+        acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+extern "C" int probe_read_wave_region(const void* p, int64_t bytes, void* out, int64_t region, int block, int un,
+                                      void* stream) {
+    if (region < 1024 || region % 1024 || (block != 64 && block != 128 && block != 256)) return 2;
+    const int64_t blocks = bytes / region / (block / 64);
+    if (blocks < 1 || blocks > 0x7FFFFFFF) return 2;
+    if (un == 16) hipLaunchKernelGGL((read_wave_region_kernel<16>), dim3((unsigned)blocks), dim3(block), 0, (hipStream_t)stream, (const uint8_t*)p, region, bytes, (uint32_t*)out);
+    else if (un == 8) hipLaunchKernelGGL((read_wave_region_kernel<8>), dim3((unsigned)blocks), dim3(block), 0, (hipStream_t)stream, (const uint8_t*)p, region, bytes, (uint32_t*)out);
+    else hipLaunchKernelGGL((read_wave_region_kernel<6>), dim3((unsigned)blocks), dim3(block), 0, (hipStream_t)stream, (const uint8_t*)p, region, bytes, (uint32_t*)out);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
