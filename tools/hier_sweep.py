@@ -62,6 +62,26 @@ VARIANTS = {
     "lds20cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 6},
     "lds18cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 18, "FLAME_HLDS_CU16": 6},
     "lds14cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 14, "FLAME_HLDS_CU16": 6},
+    # round 3: the next client batch's loads issued before the current one is combined (a
+    # wave's loads in flight stay between CU and 2 CU instead of dropping to 0 while it computes)
+    "pipe3": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 3},
+    "pipe4": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 4},
+    "pipe6": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 6},
+    "pipe2": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 2},
+    # round 3: whole batches only (the init-first arrival with the first batch, the remainder together)
+    "tailb": {"FLAME_TAILB": 1},
+    "tailbpf": {"FLAME_TAILB": 1, "FLAME_HPF": 1},
+    "tailbcu5": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 5},
+    "tailbcu7": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 7},
+    "tailbcu8": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 8},
+    "tailbcu4": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 4},
+    "tailbcu3": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 3},
+    "tailbcu2": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 2},
+    "hcu3": {"FLAME_HLDS_CU16": 3},
+    "lds12cu3": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 3},
+    "lds12cu4": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 4},
+    "lds8cu3": {"FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 3},
+    "lds8cu2": {"FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 2},
     "hdiag1": {"FLAME_HDIAG": 1},   # diagnostic: middle weights not stored (output not checked)
     "hdiag2": {"FLAME_HDIAG": 2},   # diagnostic: middle weights neither loaded nor stored
 }
@@ -101,7 +121,7 @@ def main():
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
-        build_variants(sorted({n.split(":")[0] for n in names if n != "probe"}))
+        build_variants(sorted({n.split(":")[0] for n in names if n not in ("probe", "rprobe")}))
         return
 
     import torch
@@ -150,7 +170,7 @@ def main():
         dmt = torch.from_numpy(pt.meta).to(dev)
         bt = dmt.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    libs = {nm: load(nm.split(":")[0]) for nm in names if nm != "probe"}
+    libs = {nm: load(nm.split(":")[0]) for nm in names if nm not in ("probe", "rprobe")}
     # "<variant>:sync" = the same build in FLAME_HIER_SYNC mode (FedAvg middles + top FedAvg, same bytes)
     sseg = engine.HierSeg(P, mid_w=seg.mid_w, clients=seg.clients, top_in=gw.data_ptr(), top_out=top.data_ptr(),
                           tile_stride=seg.tile_stride, mid_tile_stride=mts)
@@ -161,6 +181,10 @@ def main():
     def launch(nm):
         if nm == "probe":
             assert PL.probe_read(slab.data_ptr(), pbytes, pout.data_ptr(), 16384, 2, stream) == 0
+            return
+        if nm == "rprobe":    # the kernel's own per-workgroup region at its residency and loads in flight
+            assert PL.probe_read_region_persist(slab.data_ptr(), pbytes, pout.data_ptr(), M * C * T * isz, 6, 0,
+                                                65536, None, stream) == 0
             return
         if nm.endswith(":sync"):
             rc = libs[nm].flame_hier_fedbuff(code, N.FLAME_HIER_TOP_ACCUM | N.FLAME_HIER_SYNC, bs + ps.offs["segs"],
@@ -178,15 +202,18 @@ def main():
         if rc:
             raise RuntimeError(libs[nm].flame_last_error())
 
-    if "probe" in names:
+    if "probe" in names or "rprobe" in names:
         PL = ctypes.CDLL(os.path.join(ROOT, "build", "hbm_probe.so"))
+        PL.probe_read_region_persist.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                 ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
         PL.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p]
         pout = torch.zeros(4, dtype=torch.int32, device=dev)
         pbytes = slab.numel() * isz // 4096 * 4096
     refs = {}       # per mode (FedBuff / sync): every variant bitwise-equal to the first one of its mode
     for nm in names:
-        if nm == "probe":
+        if nm in ("probe", "rprobe"):
             continue
         mids.copy_(mids0)
         gw.copy_(gw0)
@@ -223,7 +250,7 @@ def main():
     nbytes = isz * P * (M * C + 2 * M + 1 + 2)
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
-        nb = pbytes if nm == "probe" else nbytes
+        nb = pbytes if nm in ("probe", "rprobe") else nbytes
         print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nb / med / 1e6:8.1f} GB/s  "
               f"{VARIANTS.get(nm.split(':')[0], {})}", flush=True)
 

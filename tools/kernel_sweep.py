@@ -85,6 +85,41 @@ VARIANTS = {
     "occ5": {"FLAME_OCC_LDS": 32768},
     "occ6": {"FLAME_OCC_LDS": 27136},
     "xcd": {"FLAME_XCD_SWIZZLE": 1},
+    # round 3: fewer loads in flight per CU (tools/occ_probe.py: reads peak at 2 workgroups per CU
+    # with 6 x 16-B loads per lane, above the full-occupancy configurations)
+    "occ2cu6": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 6},
+    "occ2cu8": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 8},
+    "occ2cu4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4},
+    "occ2cu12": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 12},
+    "occ3cu4": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 4},
+    "occ3cu6": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 6},
+    "occ4cu4": {"FLAME_OCC_LDS": 40960, "FLAME_CU": 4},
+    "occ2pipe3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3, "FLAME_PIPE": 1},
+    "occ2pipe4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_PIPE": 1},
+    "occ2cu3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3},
+    "occ2cu2": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 2},
+    "occ2cu5": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 5},
+    "occ3cu3": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 3},
+    "occ3cu2": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 2},
+    "tailb": {"FLAME_TAILB": 1},
+    "occ2cu4tb": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_TAILB": 1},
+    "occ2cu6tb": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 6, "FLAME_TAILB": 1},
+    "optwgc4cu6": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 6},
+    "optwgc8cu12": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 12},
+    "lo0": {"FLAME_LO_CU": 0},        # flame_agg_reduce before the low-occupancy path (full occupancy, unroll 8)
+    "lo4": {"FLAME_LO_CU": 4},
+    "lo2occ3": {"FLAME_LO_CU": 2, "FLAME_LO_LDS": 53248},
+    "lo3occ3": {"FLAME_LO_CU": 3, "FLAME_LO_LDS": 53248},
+    "optwgc4cu3": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 3},
+    "optwgc4cu4": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 4},
+    "lo16_3": {"FLAME_LO_CU16": 3},
+    "lo16_6": {"FLAME_LO_CU16": 6},
+    "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
+    "optwgc8cu3": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 3},
+    "optwgc8cu4": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 4},
+    "optwgc6cu3": {"FLAME_OPT_WGC": 6, "FLAME_OPT_CU": 3},
+    "optwgc3cu3": {"FLAME_OPT_WGC": 3, "FLAME_OPT_CU": 3},
+    "optwgc2cu3": {"FLAME_OPT_WGC": 2, "FLAME_OPT_CU": 3},
     # client loads as buffer loads with an explicit cache policy (sc0 1, nt 2, sc1 16; value - 1)
     "bl_none": {"FLAME_BUFLD": 1},
     "bl_nt": {"FLAME_BUFLD": 3},
@@ -154,8 +189,8 @@ def main():
     counts = synth.counts(2, n)
     rates = [int(c) / int(counts.sum()) for c in counts]
     probe = "probe" in names
-    if probe:
-        names = [x for x in names if x != "probe"]
+    rprobe = "rprobe" in names
+    names = [x for x in names if x not in ("probe", "rprobe")]
     # "<variant>:tiled" = same build, client data in the tiled [chunks][N][chunk] layout
     libs = {nm: load(nm.split(":")[0]) for nm in names}
     tiled_slab = None
@@ -201,6 +236,11 @@ def main():
         if nm == "probe":
             assert PL.probe_read(slab.data_ptr(), pbytes, pout.data_ptr(), 16384, 2, stream) == 0
             return
+        if nm == "rprobe":    # the kernel's own per-workgroup region, 2 workgroups per CU, 6 loads per lane
+            src = tiled_slab if tiled_slab is not None else slab
+            assert PL.probe_read_region_persist(src.data_ptr(), pbytes, pout.data_ptr(), rregion, 6, 0, 65536,
+                                                None, stream) == 0
+            return
         p, dm = plans[nm]
         b = dm.data_ptr()
         if args.kernel == "agg":
@@ -225,17 +265,27 @@ def main():
         libs["probe"] = _P()
         plans["probe"] = None
         names = names + ["probe"]
+    if rprobe:
+        PL = ctypes.CDLL(os.path.join(ROOT, "build", "hbm_probe.so"))
+        PL.probe_read_region_persist.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                 ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
+        pout = torch.zeros(4, dtype=torch.int32, device=dev)
+        src = tiled_slab if tiled_slab is not None else slab
+        rregion = n * 4096 if tiled_slab is not None else 4 << 20
+        pbytes = src.numel() * src.element_size() // rregion * rregion
+        names = names + ["rprobe"]
 
     # correctness: every variant bitwise equal to the first of its layout (FedOPT: from the same
     # cur / m / v state, all four outputs compared)
     refs = {}
     for nm in names:
-        if args.kernel != "agg" and nm != "probe":
+        if args.kernel != "agg" and nm not in ("probe", "rprobe"):
             for t, t0 in zip((cur, m, v), state0):
                 t.copy_(t0)
         launch(nm)
         torch.cuda.synchronize()
-        if nm == "probe" or nm.startswith("nostore"):
+        if nm in ("probe", "rprobe") or nm.startswith("nostore"):
             continue
         got = [out.clone()] if args.kernel == "agg" else [out.clone(), m.clone(), v.clone(), cur_out.clone()]
         lay = "tiled" if nm.endswith(":tiled") else "rows"
@@ -262,7 +312,7 @@ def main():
     res = {}
     for nm in names:
         med, mn = statistics.median(times[nm]), min(times[nm])
-        nb = pbytes if nm == "probe" else nbytes
+        nb = pbytes if nm in ("probe", "rprobe") else nbytes
         res[nm] = {"median_ms": med, "min_ms": mn, "GBps_median": nb / med / 1e6,
                    "defs": VARIANTS.get(nm.split(":")[0], {})}
         print(f"{nm:10s} median {med:8.3f} ms  min {mn:8.3f} ms  {nb / med / 1e6:8.1f} GB/s", flush=True)
