@@ -329,8 +329,9 @@ def kernel_stats(events, name):
 def read_ceiling(buf: torch.Tensor, reps: int = 5, regions=()):
     """Same-device HBM streaming-read ceiling over an existing buffer (tools/hbm_probe.hip):
     the best of a grid-stride read (16,384 workgroups, 16 nt dwordx4 loads in flight per
-    lane) and a region-streaming read (each workgroup one contiguous 1 MiB region, 16 loads
-    per lane -- the product kernel's access pattern with the fastest region size measured).
+    lane) and region-streaming reads (each workgroup one contiguous 1 MiB region -- the product
+    kernel's access pattern with the fastest region size measured -- at full residency with 16
+    loads per lane, and at 2 workgroups per CU with 6, the faster of the two since round 3).
     ``regions``: further region sizes (bytes) to probe the same way, e.g. a kernel's own
     per-workgroup region when it differs from 1 MiB.  Returns (best GB/s, {probe: GB/s})."""
     import ctypes
@@ -359,6 +360,17 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5, regions=()):
     for r in regions:
         probes[f"region_{r >> 20}MiB_16ld"] = (lambda r=r: L.probe_read_region(buf.data_ptr(), nbytes, out.data_ptr(),
                                                                              r, r, 16, st))
+    # the same region streams at 2 workgroups per CU (64 KiB of dynamic LDS each) with 6 loads in
+    # flight per lane: the residency HBM reads fastest at (tools/occ_probe.py), the one the product
+    # kernels now run at (flame_agg_reduce's FLAME_LO_CU path, FedOPT, the hierarchy kernel)
+    if hasattr(L, "probe_read_region_persist"):
+        L.probe_read_region_persist.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
+        for r in (1 << 20, *regions):
+            probes[f"region_{r >> 20}MiB_2perCU_6ld"] = (
+                lambda r=r: L.probe_read_region_persist(buf.data_ptr(), nbytes // r * r, out.data_ptr(), r, 6, 0,
+                                                        65536, None, st))
     res = {}
     for name, launch in probes.items():
         ts = []
@@ -569,7 +581,9 @@ def main():
         elif world == 1 and args.cpu_clients > 0:
             cpu = cpu_baseline_fedopt(args.workload, host_row, n, P, base0, counts, args.cpu_clients,
                                       args.cpu_rounds)
-        ceiling, probes = read_ceiling(slab_buf) if world == 1 else (None, {})
+        # (the kernel's own per-workgroup region too: n x 4 KiB of the tiled slab)
+        ceiling, probes = (read_ceiling(slab_buf, regions=(n * 4096,) if args.layout == "slab" and n * 4096 != 1 << 20
+                                        else ()) if world == 1 else (None, {}))
         # a piece-pipelined step has several launches: price the step's kernels as one
         launches_per_step = ks["launches"] / args.steps
         k_time = ks["avg_s"] * launches_per_step
@@ -1059,8 +1073,9 @@ def bench_hier(args, world, rank, dev):
                          "algorithmic_bytes": red["bytes_per_launch"],
                          "measured_read_ceiling_GBps": ceiling, "read_probes_GBps": probes,
                          "frac_of_measured_ceiling": red["achieved_GBps"] / ceiling if ceiling else None,
-                         "frac_of_own_region_probe": (red["achieved_GBps"] / probes[f"region_{(M * C * 4096) >> 20}MiB_16ld"]
-                                                      if f"region_{(M * C * 4096) >> 20}MiB_16ld" in probes else None)},
+                         # against the kernel's own region read at its own residency (2 per CU, 6 loads per lane)
+                         "frac_of_own_region_probe": (red["achieved_GBps"] / probes[own] if (
+                             own := f"region_{(M * C * 4096) >> 20}MiB_2perCU_6ld") in probes else None)},
             "kernels": {**kst, "kernel_ms_per_step": per_step_kernel * 1e3,
                         "kernel_client_params_per_s": M * C * P / per_step_kernel},
             "cpu_baseline": cpu,

@@ -48,6 +48,14 @@ namespace {
 #ifndef FLAME_PIPE
 #define FLAME_PIPE 0      // 1: prefetch the next client batch before combining the current one
 #endif
+#ifndef FLAME_SPF
+#define FLAME_SPF 0       // 1: prefetch the next client batch's pointers (scalar loads) behind the current
+                          // batch's vector loads (reduce_clients, vector path)
+#endif
+#ifndef FLAME_TAILB
+#define FLAME_TAILB 0     // 1: the init-first client joins the first batch and the last n % CU clients
+                          // load together (reduce_clients, vector path)
+#endif
 #ifndef FLAME_NT
 #define FLAME_NT 1        // non-temporal client loads (read once)
 #endif
@@ -121,6 +129,26 @@ namespace {
 #define FLAME_OCC_LDS 0   // sweep variants: dynamic LDS bytes per reduction / hierarchy workgroup (caps
                           // resident workgroups per CU at 160 KiB / FLAME_OCC_LDS; the kernels use no LDS)
 #endif
+#ifndef FLAME_LO_CU
+#define FLAME_LO_CU 3     // flame_agg_reduce, launches of >= FLAME_LO_MIN_CLIENTS clients and >= FLAME_LO_MIN_CHUNKS
+                          // chunks: 2 workgroups per CU (FLAME_LO_LDS of dynamic LDS, unused) with this client
+                          // unroll -- fewer loads in flight reads HBM faster (C3: 14.90 -> 14.18 ms, 7.24 TB/s =
+                          // 99 % of a region probe at that residency; tools/kernel_sweep.py occ2cu3 / lo0,
+                          // profiles/r03ze_c3_sweep.log, r03zf_c3_sweep.log); 0 = off
+#endif
+#ifndef FLAME_LO_CU16
+#define FLAME_LO_CU16 4   // the same for 16-bit dtypes (8 elements per load: unroll 3 reads 6.49 TB/s, 4 6.99;
+                          // bf16 1024 x 25M, profiles/r03zf_c3_bf16_sweep.log)
+#endif
+#ifndef FLAME_LO_LDS
+#define FLAME_LO_LDS 65536
+#endif
+#ifndef FLAME_LO_MIN_CLIENTS
+#define FLAME_LO_MIN_CLIENTS 128
+#endif
+#ifndef FLAME_LO_MIN_CHUNKS
+#define FLAME_LO_MIN_CHUNKS 4096
+#endif
 #ifndef FLAME_XCD_SWIZZLE
 #define FLAME_XCD_SWIZZLE 0  // sweep variant: each XCD (workgroups are dispatched to XCDs round-robin)
                              // streams one contiguous eighth of the chunks
@@ -129,13 +157,16 @@ namespace {
 #define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
 #endif
 #ifndef FLAME_OPT_WGC
-#define FLAME_OPT_WGC 8   // FedOPT (fp32, >= 8 x 256 x WGC chunks): chunks per workgroup; > 1 holds their
-                          // avg/m/v/cur blocks in LDS (16 KiB per chunk, 128 KiB at 8 -> one workgroup
+#define FLAME_OPT_WGC 4   // FedOPT (fp32, >= 8 x 256 x WGC chunks): chunks per workgroup; > 1 holds their
+                          // avg/m/v/cur blocks in LDS (16 KiB per chunk; 64 KiB at 4 -> two workgroups
                           // per CU) and stores them in one burst at the end.  C4 FedAdam, tiled slab:
-                          // 15.18 -> 14.62 ms (tools/kernel_sweep.py, profiles/r02_fedopt_wgc_sweep.log)
+                          // 1 chunk 15.18, 8 chunks (one workgroup per CU, unroll 8) 14.62 ms (round 2,
+                          // profiles/r02_fedopt_wgc_sweep.log); 4 chunks with unroll 3 (fewer loads in
+                          // flight, as flame_agg_reduce's FLAME_LO_CU) 1.8-2.0 % under 8 chunks / unroll 8
+                          // (profiles/r03zf_c4_sweep.log, r03zg_c4_sweep.log)
 #endif
 #ifndef FLAME_OPT_CU
-#define FLAME_OPT_CU FLAME_CU  // FedOPT fp32 client unroll with FLAME_OPT_WGC > 1
+#define FLAME_OPT_CU 3    // FedOPT fp32 client unroll with FLAME_OPT_WGC > 1
 #endif
 
 constexpr int kBlock = FLAME_BLOCK;
@@ -400,6 +431,94 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
 #pragma unroll
             for (int j = 0; j < EPT; ++j) acc[v][j] = X::add(acc[v][j], X::tmp(x[v][j], r, rd));
     };
+#if FLAME_SPF
+    if constexpr (VEC && CU > 1) {
+        // the next batch's client pointers are read (scalar loads) while the current batch's
+        // vector loads are in flight, so a batch never waits on its pointer row before issuing
+        if (init_first && n > 0) {
+            T x[kVPT][EPT];
+            load_client(0, x);
+            const float r = rate32(0);
+            const double rd = rate64(0);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[v][j], r, rd);
+            i = 1;
+        }
+        if (i + CU <= n) {
+            uint64_t pa[CU];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) pa[u] = cp[i + u];
+            while (true) {
+                T x[CU][kVPT][EPT];
+#pragma unroll
+                for (int u = 0; u < CU; ++u) {
+                    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(pa[u]) + coff);
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) unpack<T, EPT>(ld_nt(p + v * VS), x[u][v]);
+                }
+                const bool more = i + 2 * CU <= n;
+                if (more) {
+#pragma unroll
+                    for (int u = 0; u < CU; ++u) pa[u] = cp[i + CU + u];
+                }
+#pragma unroll
+                for (int u = 0; u < CU; ++u) combine(i + u, x[u]);
+                i += CU;
+                if (!more) break;
+            }
+        }
+        for (; i < n; ++i) {
+            T x[kVPT][EPT];
+            load_client(i, x);
+            combine(i, x);
+        }
+        return;
+    }
+#endif
+#if FLAME_TAILB
+    if constexpr (VEC && CU > 1) {
+        // whole batches only: the init-first client's load goes out with the first batch and the
+        // last n % CU clients' loads go out together (one wait each, not one round trip per
+        // client); the arithmetic is the same sequence, in client order
+        if (init_first && n > 0) {
+            const int r = n < CU ? n : CU;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(u, x[u]);
+            const float r0 = rate32(0);
+            const double rd0 = rate64(0);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[0][v][j], r0, rd0);
+#pragma unroll
+            for (int u = 1; u < CU; ++u)
+                if (u < r) combine(u, x[u]);
+            i = r;
+        }
+        for (; i + CU <= n; i += CU) {
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, x[u]);
+        }
+        if (i < n) {
+            const int r = n - i;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) combine(i + u, x[u]);
+        }
+        return;
+    }
+#endif
     if (init_first && n > 0) {
         T x[kVPT][EPT];
         load_client(0, x);
@@ -1479,6 +1598,24 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>((n_chunks + kWGC - 1) / kWGC)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
+#if FLAME_LO_CU > 0
+    // long-lived workgroups over many chunks: two per CU, FLAME_LO_CU loads in flight per lane
+    if (n_clients >= FLAME_LO_MIN_CLIENTS && n_chunks >= FLAME_LO_MIN_CHUNKS && kWGC == 1 && FLAME_OCC_LDS == 0) {
+        switch (dtype) {
+        case FLAME_F32:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, FLAME_LO_CU>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        case FLAME_BF16:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, FLAME_LO_CU16>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        case FLAME_F16:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, FLAME_LO_CU16>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        default:
+            break;      // f64 / integers: the general launch below
+        }
+    }
+#endif
     switch (dtype) {
     case FLAME_F32:
         hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
