@@ -77,6 +77,10 @@ VARIANTS = {
     "tailbcu4": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 4},
     "tailbcu3": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 3},
     "tailbcu2": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 2},
+    "spf": {"FLAME_SPF": 1},
+    "spfcu5": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 5},
+    "spfcu8": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 8},
+    "spfcu4": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 4},
     "hcu3": {"FLAME_HLDS_CU16": 3},
     "lds12cu3": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 3},
     "lds12cu4": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 4},

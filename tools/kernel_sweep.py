@@ -112,6 +112,8 @@ VARIANTS = {
     "lo3occ3": {"FLAME_LO_CU": 3, "FLAME_LO_LDS": 53248},
     "optwgc4cu3": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 3},
     "optwgc4cu4": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 4},
+    "spf": {"FLAME_SPF": 1},          # next batch's client pointers prefetched behind the current loads
+    "spflo4": {"FLAME_SPF": 1, "FLAME_LO_CU": 4},
     "lo16_3": {"FLAME_LO_CU16": 3},
     "lo16_6": {"FLAME_LO_CU16": 6},
     "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
