@@ -48,6 +48,12 @@ namespace {
 #ifndef FLAME_PIPE
 #define FLAME_PIPE 0      // 1: prefetch the next client batch before combining the current one
 #endif
+#ifndef FLAME_BF16_HI
+#define FLAME_BF16_HI 0   // 1: bf16 rounding as one v_cvt_pk_bf16_f32 into the high half (bf16_round)
+#endif
+#ifndef FLAME_BF16_PK
+#define FLAME_BF16_PK 0   // 1: bf16 client combine on packed fp32 pairs (reduce_clients)
+#endif
 #ifndef FLAME_SPF
 #define FLAME_SPF 0       // 1: prefetch the next client batch's pointers (scalar loads) behind the current
                           // batch's vector loads (reduce_clients, vector path)
@@ -194,8 +200,17 @@ int check_launch(const char* what) {
 
 // ---------------------------------------------------------------- rounding helpers
 __device__ __forceinline__ float bf16_round(float x) {
+#if FLAME_BF16_HI
+    // RNE fp32 -> bf16 -> fp32 in ONE instruction: v_cvt_pk_bf16_f32 packs (lo, hi) = (bf16(0),
+    // bf16(x)), and that dword IS the fp32 value of bf16(x) (the compiler's lowering of the cast
+    // puts x in the low half and shifts it back up: two instructions per rounding)
+    float r;
+    asm("v_cvt_pk_bf16_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
     // RNE fp32 -> bf16 -> fp32 (v_cvt_pk_bf16_f32 on gfx950)
     return static_cast<float>(static_cast<__bf16>(x));
+#endif
 }
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
     return __uint_as_float(static_cast<uint32_t>(b) << 16);
@@ -423,33 +438,65 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
             }
         }
     };
-    auto combine = [&](int c, const T (&x)[kVPT][EPT]) {
-        const float r = rate32(c);
-        const double rd = rate64(c);
+    auto combine_r = [&](const float r, const double rd, const T (&x)[kVPT][EPT]) {
+#if FLAME_BF16_PK
+        if constexpr (DT == FLAME_BF16) {
+            // the same two roundings per element, two elements per packed-fp32 multiply and add
+            // (v_pk_mul_f32 / v_pk_add_f32: each lane's result is the IEEE fp32 op's)
+            using f2 = __attribute__((ext_vector_type(2))) float;
+            const f2 r2 = {r, r};
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; j += 2) {
+                    const f2 x2 = {X::ld(x[v][j]), X::ld(x[v][j + 1])};
+                    f2 t2 = x2 * r2;
+                    t2 = f2{bf16_round(t2.x), bf16_round(t2.y)};
+                    f2 a2 = f2{acc[v][j], acc[v][j + 1]} + t2;
+                    acc[v][j] = bf16_round(a2.x);
+                    acc[v][j + 1] = bf16_round(a2.y);
+                }
+            return;
+        }
+#endif
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
             for (int j = 0; j < EPT; ++j) acc[v][j] = X::add(acc[v][j], X::tmp(x[v][j], r, rd));
     };
+    auto combine = [&](int c, const T (&x)[kVPT][EPT]) { combine_r(rate32(c), rate64(c), x); };
 #if FLAME_SPF
-    if constexpr (VEC && CU > 1) {
-        // the next batch's client pointers are read (scalar loads) while the current batch's
-        // vector loads are in flight, so a batch never waits on its pointer row before issuing
-        if (init_first && n > 0) {
-            T x[kVPT][EPT];
-            load_client(0, x);
-            const float r = rate32(0);
-            const double rd = rate64(0);
+    if constexpr (VEC && CU > 1 && DT != FLAME_F64) {
+        // the next batch's client pointers AND rates are read (scalar loads) while the current
+        // batch's vector loads are in flight: a batch never waits on its pointer row before
+        // issuing, nor its combine on a rate load (a rate loaded in the combine, as the plain
+        // loop does, makes the combine's lgkmcnt(0) wait for every scalar load in flight, the
+        // prefetched pointers included).  Scalar-cache misses matter once a launch's pointer
+        // and rate rows outgrow the scalar cache (4,096 arrivals: 48 KiB per workgroup)
+        if (init_first && n > 0) {    // the init-first client's load goes out with the first batch
+            const int r = n < CU ? n : CU;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(u, x[u]);
+            const float r0 = rate32(0);
 #pragma unroll
             for (int v = 0; v < kVPT; ++v)
 #pragma unroll
-                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[v][j], r, rd);
-            i = 1;
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[0][v][j], r0, 0.0);
+#pragma unroll
+            for (int u = 1; u < CU; ++u)
+                if (u < r) combine(u, x[u]);
+            i = r;
         }
         if (i + CU <= n) {
             uint64_t pa[CU];
+            float ra[CU];
 #pragma unroll
-            for (int u = 0; u < CU; ++u) pa[u] = cp[i + u];
+            for (int u = 0; u < CU; ++u) {
+                pa[u] = cp[i + u];
+                ra[u] = r32[i + u];
+            }
             while (true) {
                 T x[CU][kVPT][EPT];
 #pragma unroll
@@ -458,21 +505,32 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
 #pragma unroll
                     for (int v = 0; v < kVPT; ++v) unpack<T, EPT>(ld_nt(p + v * VS), x[u][v]);
                 }
+                float rc[CU];
+#pragma unroll
+                for (int u = 0; u < CU; ++u) rc[u] = ra[u];
                 const bool more = i + 2 * CU <= n;
                 if (more) {
 #pragma unroll
-                    for (int u = 0; u < CU; ++u) pa[u] = cp[i + CU + u];
+                    for (int u = 0; u < CU; ++u) {
+                        pa[u] = cp[i + CU + u];
+                        ra[u] = r32[i + CU + u];
+                    }
                 }
 #pragma unroll
-                for (int u = 0; u < CU; ++u) combine(i + u, x[u]);
+                for (int u = 0; u < CU; ++u) combine_r(rc[u], 0.0, x[u]);
                 i += CU;
                 if (!more) break;
             }
         }
-        for (; i < n; ++i) {
-            T x[kVPT][EPT];
-            load_client(i, x);
-            combine(i, x);
+        if (i < n) {                  // the last n % CU clients' loads go out together
+            const int r = n - i;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) combine(i + u, x[u]);
         }
         return;
     }

@@ -77,7 +77,18 @@ VARIANTS = {
     "tailbcu4": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 4},
     "tailbcu3": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 3},
     "tailbcu2": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 2},
+    # round 3: cheaper bf16 arithmetic (the kernel issues ~13x the VALU instructions of C3's per
+    # launch, SQ counters r03zj): one-instruction rounding, packed-fp32 multiply / add
+    "bhi": {"FLAME_BF16_HI": 1},
+    "bpk": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1},
+    "bpkcu4": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 4},
+    "bpkcu5": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 5},
+    "bpkcu8": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 8},
     "spf": {"FLAME_SPF": 1},
+    "spf2": {"FLAME_SPF": 2},          # pointers AND rates prefetched one batch ahead, whole batches
+    "spf2cu5": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 5},
+    "spf2cu4": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 4},
+    "spf2cu8": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 8},
     "spfcu5": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 5},
     "spfcu8": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 8},
     "spfcu4": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 4},

@@ -112,8 +112,11 @@ VARIANTS = {
     "lo3occ3": {"FLAME_LO_CU": 3, "FLAME_LO_LDS": 53248},
     "optwgc4cu3": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 3},
     "optwgc4cu4": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 4},
+    "bpk": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1},   # cheaper bf16 arithmetic (hier_sweep.py)
+    "bpklo3": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_LO_CU16": 3},
     "spf": {"FLAME_SPF": 1},          # next batch's client pointers prefetched behind the current loads
     "spflo4": {"FLAME_SPF": 1, "FLAME_LO_CU": 4},
+    "spf2": {"FLAME_SPF": 2},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
     "lo16_3": {"FLAME_LO_CU16": 3},
     "lo16_6": {"FLAME_LO_CU16": 6},
     "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
