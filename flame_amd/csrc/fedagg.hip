@@ -54,6 +54,9 @@ namespace {
 #ifndef FLAME_BF16_PK
 #define FLAME_BF16_PK 0   // 1: bf16 client combine on packed fp32 pairs (reduce_clients)
 #endif
+#ifndef FLAME_DYN_OCC_LDS
+#define FLAME_DYN_OCC_LDS 0  // sweep: dynamic LDS bytes per FedDyn workgroup (caps its residency; unused)
+#endif
 #ifndef FLAME_SPF
 #define FLAME_SPF 0       // 1: prefetch the next client batch's pointers (scalar loads) behind the current
                           // batch's vector loads (reduce_clients, vector path)
@@ -150,7 +153,8 @@ namespace {
 #define FLAME_LO_LDS 65536
 #endif
 #ifndef FLAME_LO_MIN_CLIENTS
-#define FLAME_LO_MIN_CLIENTS 128
+#define FLAME_LO_MIN_CLIENTS 64  // 64 x 100M fp32: 4.04 -> 3.90 ms, bf16 64 x 200M: 4.09 -> 4.00 ms
+                                 // (profiles/r03zn_c64_lomin.log, r03zn_b64_lomin.log)
 #endif
 #ifndef FLAME_LO_MIN_CHUNKS
 #define FLAME_LO_MIN_CHUNKS 4096
@@ -1995,19 +1999,19 @@ int flame_feddyn_round(int dtype, const flame_dyn_segment* segs, int32_t n_segs,
     const float ra32 = static_cast<float>(rate_avg), rm32 = static_cast<float>(rate_mean);
     switch (dtype) {
     case FLAME_F32:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F32, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F32, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_BF16:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_BF16, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_BF16, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_F16:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F16, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F16, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_F64:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F64, FLAME_DYN_CU>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F64, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     default:

@@ -116,7 +116,14 @@ VARIANTS = {
     "bpklo3": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_LO_CU16": 3},
     "spf": {"FLAME_SPF": 1},          # next batch's client pointers prefetched behind the current loads
     "spflo4": {"FLAME_SPF": 1, "FLAME_LO_CU": 4},
-    "spf2": {"FLAME_SPF": 2},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
+    "spf2": {"FLAME_SPF": 2},
+    # FedDyn (2 reads : 1 write) and mid-size reductions at lower residency (tools/feddyn_sweep.py)
+    "dynocc2": {"FLAME_DYN_OCC_LDS": 65536},
+    "dynocc2cu2": {"FLAME_DYN_OCC_LDS": 65536, "FLAME_DYN_CU": 2},
+    "dynocc2cu3": {"FLAME_DYN_OCC_LDS": 65536, "FLAME_DYN_CU": 3},
+    "dynocc3cu2": {"FLAME_DYN_OCC_LDS": 53248, "FLAME_DYN_CU": 2},
+    "dynocc4cu2": {"FLAME_DYN_OCC_LDS": 40960, "FLAME_DYN_CU": 2},
+    "lomin32": {"FLAME_LO_MIN_CLIENTS": 32},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
     "lo16_3": {"FLAME_LO_CU16": 3},
     "lo16_6": {"FLAME_LO_CU16": 6},
     "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
