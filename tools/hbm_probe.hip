@@ -331,3 +331,19 @@ extern "C" int probe_read_region_persist(const void* p, int64_t bytes, void* out
     if (hipLaunchKernel(fn, dim3((unsigned)grid), dim3(256), args, lds, (hipStream_t)stream) != hipSuccess) return 1;
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// The blocked (grouped-slab) read at a chosen residency: read_blocked_kernel with UN loads per lane and
+// `lds` bytes of dynamic LDS capping the workgroups per CU.
+extern "C" int probe_read_blocked_lds(const void* p, int64_t bytes, void* out, int64_t B, int G, int un, int lds,
+                                      void* stream) {
+    if (B < 16 * 4096 || B % (16 * 4096) || G < 1 || lds < 0 || lds > 160 * 1024) return 2;
+    const int64_t nwg = bytes / (B * G);
+    if (nwg < 1 || nwg > 0x7FFFFFFF) return 2;
+    const void* fn = un == 16 ? (const void*)read_blocked_kernel<16> : (const void*)read_blocked_kernel<6>;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return 3;
+    const uint8_t* pp = (const uint8_t*)p;
+    uint32_t* po = (uint32_t*)out;
+    void* args[] = {(void*)&pp, (void*)&B, (void*)&G, (void*)&po};
+    if (hipLaunchKernel(fn, dim3((unsigned)nwg), dim3(256), args, lds, (hipStream_t)stream) != hipSuccess) return 1;
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
