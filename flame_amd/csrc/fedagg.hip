@@ -57,6 +57,10 @@ namespace {
 #ifndef FLAME_DYN_OCC_LDS
 #define FLAME_DYN_OCC_LDS 0  // sweep: dynamic LDS bytes per FedDyn workgroup (caps its residency; unused)
 #endif
+#ifndef FLAME_HXP
+#define FLAME_HXP 0       // hierarchy kernel (LDS store groups, FedBuff mode): > 0 = one double-buffered stream
+                          // of that many arrivals per batch across the middles (must divide the arrivals)
+#endif
 #ifndef FLAME_SPF
 #define FLAME_SPF 0       // 1: prefetch the next client batch's pointers (scalar loads) behind the current
                           // batch's vector loads (reduce_clients, vector path)
@@ -1145,6 +1149,87 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
         // weights wait in LDS (lane-private slots, no barrier) rather than in registers -- long
         // store bursts at 2 workgroups per CU
         __shared__ V16 held[HL ? HB * kVPT * kBlock : 1];
+#if FLAME_HXP
+        // ONE double-buffered stream of arrival batches across the middles (FLAME_HXP arrivals per
+        // batch, dividing n_clients): the next batch -- the next middle's first one included -- is in
+        // flight while the current batch is combined and while a finished middle's epilogue runs, so
+        // a wave's loads never drain at a middle boundary.  A middle's weights are loaded one middle
+        // ahead (with the previous middle's first batch): loads complete in issue order, so a
+        // weights load issued behind the current batches would hold the epilogue until they land.
+        // Same per-element operation order as the loop below (bitwise).
+        constexpr int XB = FLAME_HXP;
+        if (HL && !SYNC && kVPT == 1 && n_clients % XB == 0 && n_clients >= XB) {
+            const int bpm = n_clients / XB;
+            const int nbt = n_mids * bpm;
+            T xa[XB][kVPT][EPT], xb[XB][kVPT][EPT];
+            V16 wc, wn;
+            wc = ld_v(mid_ptr(0));
+            if (n_mids > 1) wn = ld_v(mid_ptr(1));
+            A acc[kVPT][EPT];
+            auto issue = [&](int b, T (&x)[XB][kVPT][EPT]) {
+                const int m = b / bpm;
+                const int c0 = (b - m * bpm) * XB;
+                const uint64_t* cp = crow + static_cast<int64_t>(m) * n_clients + c0;
+#pragma unroll
+                for (int u = 0; u < XB; ++u) {
+                    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[u]) + coff);
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) unpack<T, EPT>(ld_nt(p + v * VS), x[u][v]);
+                }
+            };
+            auto combine_batch = [&](int b, const T (&x)[XB][kVPT][EPT]) {
+                const int m = b / bpm;
+                const int c0 = (b - m * bpm) * XB;
+                const float* r = mid_rates + static_cast<int64_t>(m) * n_clients + c0;
+#pragma unroll
+                for (int u = 0; u < XB; ++u) {
+                    const float ru = r[u];
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                        for (int j = 0; j < EPT; ++j) {
+                            const A t = X::tmp(x[u][v][j], ru, 0.0);
+                            acc[v][j] = (u == 0 && c0 == 0) ? t : X::add(acc[v][j], t);   // init-first
+                        }
+                }
+                if (c0 + XB < n_clients) return;
+                // middle m complete: scale_add from its weights, the delta into the top, the new
+                // weights into the LDS-held store group (stored as a burst when the group is full)
+                T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+                const float g = mid_goal[m], rt = top_rates[m];
+                const int u = m % HB;
+                T w[EPT], d[EPT];
+                unpack<T, EPT>(wc, w);
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) {
+                    S::op(w[j], X::st(acc[0][j]), g, static_cast<double>(g), &d[j]);
+                    const A t = X::tmp(d[j], rt, 0.0);
+                    top[0][j] = have_top ? X::add(top[0][j], t) : t;
+                }
+                have_top = true;
+                held[u * kBlock + threadIdx.x] = pack<T, EPT>(w);
+                if (dp) st_v(dp, pack<T, EPT>(d));
+                wc = wn;                           // loaded a whole middle ago
+                if (m + 2 < n_mids) wn = ld_v(mid_ptr(m + 2));
+                if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {
+                    const int mg = m - u;
+#pragma unroll 1
+                    for (int q = 0; q <= u; ++q) st_pol<FLAME_HST>(mid_ptr(mg + q), held[q * kBlock + threadIdx.x]);
+                }
+            };
+            issue(0, xa);
+            int b = 0;
+#pragma unroll 1
+            while (true) {
+                if (b + 1 < nbt) issue(b + 1, xb);
+                combine_batch(b, xa);
+                if (++b >= nbt) break;
+                if (b + 1 < nbt) issue(b + 1, xa);
+                combine_batch(b, xb);
+                if (++b >= nbt) break;
+            }
+        } else
+#endif
 #pragma unroll 1
         for (int m0 = 0; m0 < n_mids; m0 += HB) {
             V16 pend[HL ? 1 : HB][kVPT];

@@ -84,6 +84,11 @@ VARIANTS = {
     "bpkcu4": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 4},
     "bpkcu5": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 5},
     "bpkcu8": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 8},
+    # round 3: one double-buffered arrival stream across the middles (no drain at middle boundaries)
+    "hxp2": {"FLAME_HXP": 2},
+    "hxp4": {"FLAME_HXP": 4},
+    "hxp8": {"FLAME_HXP": 8},
+    "hxp16": {"FLAME_HXP": 16},
     "spf": {"FLAME_SPF": 1},
     "spf2": {"FLAME_SPF": 2},          # pointers AND rates prefetched one batch ahead, whole batches
     "spf2cu5": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 5},
