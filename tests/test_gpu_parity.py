@@ -192,6 +192,32 @@ def test_reduce_vs_oracle_dtypes(dtype, numel):
     S.assert_bitwise(f"{dtype}/{numel}", out, {"x": exp})
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_low_residency_reduction_vs_oracle(dtype):
+    """flame_agg_reduce's 2-workgroups-per-CU instantiation (FLAME_LO_CU / FLAME_LO_CU16: launches of
+    >= 64 clients over >= 4,096 chunks) on every element against the oracle: 64 clients
+    as separate tensors (the row layout, so the XCD chunk map is on too) over 4,096 chunks + a ragged
+    4,099-element key, every float dtype the path instantiates."""
+    from flame_amd import engine
+    O = _oracle()
+    n = 64
+    chunk = engine.chunk_elems(engine.dtype_code(dtype))
+    shapes = [("w", 4096 * chunk), ("t", 4_099)]
+    g = torch.Generator().manual_seed(11)
+    counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+    total = sum(counts)
+    base = {k: _synth_dev(12, 0 + j, s, 1.0, dtype) for j, (k, s) in enumerate(shapes)}
+    cl = [{k: _synth_dev(12, 10 + 2 * i + j, s, 1e-2, dtype) for j, (k, s) in enumerate(shapes)} for i in range(n)]
+    exp = {k: v.cpu() for k, v in base.items()}
+    for k in exp:
+        O.reduce_tensor(exp[k], [c[k].cpu() for c in cl], [c / total for c in counts])
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i:04d}"] = S.TR(cl[i], counts[i])
+    out = make_amd("fedavg").do({k: v.clone() for k, v in base.items()}, cache, total=total)
+    S.assert_bitwise(f"low-residency {dtype}", out, exp)
+
+
 def test_c2_256x1M_bitwise():
     """Config 2: 256 clients x (1,000,000 + 4,099) fp32, counts U{1..1000}, seed 1."""
     from flame_amd import synth
