@@ -57,6 +57,9 @@ namespace {
 #ifndef FLAME_DYN_OCC_LDS
 #define FLAME_DYN_OCC_LDS 0  // sweep: dynamic LDS bytes per FedDyn workgroup (caps its residency; unused)
 #endif
+#ifndef FLAME_HLO
+#define FLAME_HLO 1       // flame_hier_fedbuff, one middle over >= 64 arrivals and >= 4,096 chunks: low residency
+#endif
 #ifndef FLAME_HXP
 #define FLAME_HXP 0       // hierarchy kernel (LDS store groups, FedBuff mode): > 0 = one double-buffered stream
                           // of that many arrivals per batch across the middles (must divide the arrivals)
@@ -1980,9 +1983,18 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
                            n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
     // many middles (config 5: 64 per GPU): LDS-held store groups; a few (a single FedBuff's fused
     // scale_add, small hierarchies): register groups, no LDS, full occupancy
+    // one middle over a long launch (a FedBuff aggregator's fused scale_add / a middle's scale_add +
+    // delta over >= 64 queued arrivals): fewer workgroups per CU, fewer loads in flight -- fp32 2 per
+    // CU unroll 3, 16-bit 3 per CU unroll 3 (64 x 25M: 1.058 -> 0.989 ms fp32, 0.533 -> 0.509 ms bf16;
+    // tools/fedbuff_sweep.py, profiles/r03zv_fedbuff_*.log); FLAME_HLO=0 turns it off
+#define FLAME_HIER_LO(DT, LDS)                                                                                   \
+    hipLaunchKernelGGL((hier_fedbuff_kernel<DT, 3, false, kHB, false>), grid, block, LDS, st, segs, n_segs,     \
+                       n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
 #define FLAME_HIER_LAUNCH(DT, CUV, CUL)                                                                        \
     if (FLAME_HLDS && n_mids >= FLAME_HLDS_MIN_MIDS) { FLAME_HIER_LAUNCH1(DT, CUL, kHBL, true) }             \
-    else { FLAME_HIER_LAUNCH1(DT, CUV, kHB, false) }
+    else if (FLAME_HLO && !sync && n_mids == 1 && n_clients >= 64 && n_chunks >= 4096 && FLAME_OCC_LDS == 0) {  \
+        FLAME_HIER_LO(DT, (DT == FLAME_F32 ? 65536 : 53248))                                                    \
+    } else { FLAME_HIER_LAUNCH1(DT, CUV, kHB, false) }
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
     switch (dtype) {
     case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll, kClientUnroll) break;
@@ -1990,6 +2002,7 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16, kHierLdsUnroll16) break;
 #undef FLAME_HIER_LAUNCH1
 #undef FLAME_HIER_LAUNCH
+#undef FLAME_HIER_LO
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
     }

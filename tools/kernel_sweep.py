@@ -123,7 +123,12 @@ VARIANTS = {
     "dynocc2cu3": {"FLAME_DYN_OCC_LDS": 65536, "FLAME_DYN_CU": 3},
     "dynocc3cu2": {"FLAME_DYN_OCC_LDS": 53248, "FLAME_DYN_CU": 2},
     "dynocc4cu2": {"FLAME_DYN_OCC_LDS": 40960, "FLAME_DYN_CU": 2},
-    "lomin32": {"FLAME_LO_MIN_CLIENTS": 32},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
+    "lomin32": {"FLAME_LO_MIN_CLIENTS": 32},
+    # the single-middle hierarchy launch (FedBuff's fused scale_add, tools/fedbuff_sweep.py) capped at
+    # 2 / 3 workgroups per CU with fewer loads in flight (FLAME_CU: fp32 unroll of every full-residency path)
+    "hocc2cu3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3, "FLAME_HCU16": 4},
+    "hocc2cu4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_HCU16": 4},
+    "hocc3cu3": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 3, "FLAME_HCU16": 3},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
     "lo16_3": {"FLAME_LO_CU16": 3},
     "lo16_6": {"FLAME_LO_CU16": 6},
     "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
