@@ -139,11 +139,23 @@ def setup_dist(force_group=False):
             os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=str(sk.getsockname()[1]))
             sk.close()
+        # bounded: a rank that never joins (or a hung collective, RCCL aborts on it) fails the run in
+        # minutes instead of the default ten
+        import datetime
+        tmo = datetime.timedelta(seconds=int(os.environ.get("FLAME_BENCH_PG_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     return world, rank, local
+
+
+def process_group_info():
+    """The process group the line was measured over (None without one)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return {"backend": dist.get_backend(), "world": dist.get_world_size()}
 
 
 def barrier(world):
@@ -666,6 +678,168 @@ def _collective_note(plan, world, itemsize):
             "replicated_tail_elements": sum(s.hi - s.lo for s in plan.subs if s.tail)}
 
 
+# ------------------------------------------------------------------ N>1 self-check (untimed)
+# Run after the timed steps of every parameter-sharded line: each rank digests the full model
+# it holds (every rank must end with the whole model, syncfl/top_aggregator.py:161-173), the
+# digests are all-gathered and compared, and sampled global elements of every wave (plus
+# every rank boundary and the replicated tails) are recomputed on the host from the counter
+# generator with the reference's per-op roundings (numpy fp32 ops round once each, no FMA;
+# bf16 through flame_amd.synth's RNE) and compared bitwise on every rank.
+def _bf16(x):
+    from flame_amd import synth
+    return synth.bf16_bits_to_f32(synth.f32_to_bf16_bits(np.asarray(x, dtype=np.float32)))
+
+
+def _rate32(r):
+    return np.float32(r)
+
+
+def sample_indices(plan, key, per_wave=64, seed=0):
+    """~per_wave global element indices of ``key`` per wave, every rank boundary of every
+    piece, and the key's tail (replicated on every rank)."""
+    rng = np.random.default_rng(seed)
+    world = plan.world
+    picks = []
+    for w in range(plan.n_waves):
+        pieces = [(s.g0, s.g1) for s in plan.subs if s.key == key and s.wave == w and not s.tail]
+        if not pieces:
+            continue
+        sizes = np.array([b - a for a, b in pieces], dtype=np.int64)
+        pos = rng.integers(0, int(sizes.sum()), size=per_wave)
+        ends = np.cumsum(sizes)
+        for p in pos:
+            j = int(np.searchsorted(ends, p, side="right"))
+            picks.append(pieces[j][0] + int(p - (ends[j] - sizes[j])))
+        for a, b in pieces:
+            per = (b - a) // world
+            for r in range(world):
+                picks += [a + r * per, a + (r + 1) * per - 1]
+    for s in plan.subs:
+        if s.key == key and s.tail and s.g1 > s.g0:
+            picks += list(range(s.g0, min(s.g1, s.g0 + per_wave)))
+    return np.unique(np.asarray(picks, dtype=np.int64))
+
+
+def host_fedavg_rounds(seed, counts, idx, rounds, base=None):
+    """FedAvg.do (fedavg.py:79-104) ``rounds`` times in place over the n synthetic clients."""
+    from flame_amd import synth
+    total = int(np.asarray(counts).sum())
+    r32 = [_rate32(int(c) / total) for c in counts]
+    acc = synth.synth_f32(seed, 0, idx, 1.0) if base is None else base
+    cl = [synth.synth_f32(seed, 1 + i, idx, 1e-2) for i in range(len(counts))]
+    for _ in range(rounds):
+        for v, r in zip(cl, r32):
+            acc = acc + v * r
+    return acc
+
+
+def host_fedopt_rounds(sort, hyper, seed, counts, idx, rounds):
+    """FedOPT.do (fedopt.py:58-129) from the synthetic base: round 1 the FedAvg passthrough,
+    then FedAvg of (a copy of) current + the adaptive step, every op rounded in fp32."""
+    from flame_amd import synth
+    b1, omb1, b2, omb2, eta, tau = [np.float32(x) for x in hyper]
+    cur = synth.synth_f32(seed, 0, idx, 1.0)
+    m = v = None
+    for r in range(rounds):
+        avg = host_fedavg_rounds(seed, counts, idx, 1, base=cur.copy())
+        if r == 0:
+            cur = avg
+            continue
+        if m is None:
+            m, v = np.zeros_like(avg), np.zeros_like(avg)
+        d = avg - cur
+        m = b1 * m + omb1 * d
+        d2 = d * d
+        if sort == "fedadam":
+            v = b2 * v + omb2 * d2
+        elif sort == "fedyogi":
+            v = v - (omb2 * d2) * np.sign(v - d2).astype(np.float32)
+        else:
+            v = v + d2
+        cur = cur + (eta * m) / (np.sqrt(v) + tau)
+    return cur
+
+
+def host_hier_rounds(seed, M, C, idx, rounds, rnd, fetched, sync):
+    """Config 5's round ``rounds`` times in bf16: every middle's FedBuff over its C arrivals
+    (fedbuff.py:94-96,136-157) + scale_add + delta (asyncfl/middle_aggregator.py:221-226,246),
+    the top's FedBuff over the deltas (rate 1/sqrt(1 + m % 2)) + scale_add (top_goal M); sync:
+    every middle's FedAvg from its weights, delta, the top's FedAvg of the deltas
+    (syncfl/middle_aggregator.py:163-229, syncfl/top_aggregator.py:122-176)."""
+    import math
+    from flame_amd import synth
+    cnt = synth.counts(seed, M * C)
+    stale = [int(x) % 4 for x in cnt]
+    gw = _bf16(synth.synth_f32(seed, 0, idx, 1.0))
+    mids = [gw.copy() for _ in range(M)]
+    shared = gw.copy()
+    arr = [_bf16(synth.synth_f32(seed, 1 + i, idx, 1e-2)) for i in range(M * C)]
+    for _ in range(rounds):
+        if sync:
+            totals = [int(cnt[m * C:(m + 1) * C].sum()) for m in range(M)]
+            top_total = sum(totals)
+            for m in range(M):
+                w = shared if fetched else mids[m]
+                a = w
+                for t in range(C):
+                    i = m * C + t
+                    a = _bf16(a + _bf16(arr[i] * _rate32(int(cnt[i]) / totals[m])))
+                d = _bf16(a - w)
+                if not fetched:
+                    mids[m] = a
+                gw = _bf16(gw + _bf16(d * _rate32(totals[m] / top_total)))
+            continue
+        top = None
+        for m in range(M):
+            w = shared if fetched else mids[m]
+            a = None
+            for t in range(C):
+                i = m * C + t
+                tmp = _bf16(arr[i] * _rate32(1 / math.sqrt(1 + stale[i])))
+                a = tmp if a is None else _bf16(a + tmp)
+            nw = _bf16(w + _bf16(a / np.float32(C)))
+            d = _bf16(nw - w)
+            if not fetched:
+                mids[m] = nw
+            tmp = _bf16(d * _rate32(1 / math.sqrt(1 + rnd - (rnd - m % 2))))
+            top = tmp if top is None else _bf16(top + tmp)
+        gw = _bf16(gw + _bf16(top / np.float32(M)))
+    return gw
+
+
+def verify_sharded(model: torch.Tensor, idx, expected) -> dict:
+    """Digest of this rank's full model, all-gathered; the sampled elements vs the host
+    restatement on every rank.  Returns the line's ``gather_check`` object."""
+    import hashlib
+    import torch.distributed as dist
+    t = model.detach().contiguous().view(-1)
+    h = hashlib.blake2b(t.view(torch.uint8).cpu().numpy().tobytes(), digest_size=16).hexdigest()
+    got = t[torch.as_tensor(idx, device=t.device)].cpu()
+    if got.dtype == torch.bfloat16:
+        gb = got.view(torch.int16).numpy().view(np.uint16)
+        eb = np.asarray(__import__("flame_amd.synth", fromlist=["x"]).f32_to_bf16_bits(expected))
+    else:
+        gb = got.numpy().view(np.uint32)
+        eb = np.asarray(expected, dtype=np.float32).view(np.uint32)
+    bad = int(np.count_nonzero(gb != eb))
+    digests, bads = [h], [bad]
+    if dist.is_available() and dist.is_initialized():
+        digests = [None] * dist.get_world_size()
+        bads = [None] * dist.get_world_size()
+        dist.all_gather_object(digests, h)
+        dist.all_gather_object(bads, bad)
+    return {"ranks_agree": len(set(digests)) == 1, "digest": digests[0], "rank_digests": digests,
+            "sampled_elements": int(len(idx)), "sample_mismatches_per_rank": bads,
+            "sample_parity": "bitwise" if not any(bads) else f"MISMATCH ({sum(bads)} sampled elements)"}
+
+
+def _checked(gc) -> None:
+    """A failed self-check fails the run (after the line is printed)."""
+    if not gc["ranks_agree"] or any(gc["sample_mismatches_per_rank"]):
+        raise SystemExit(f"bench.py: N>1 self-check failed: ranks_agree={gc['ranks_agree']}, "
+                         f"sample mismatches per rank {gc['sample_mismatches_per_rank']}")
+
+
 def bench_sharded(args, world, rank, dev, n, P):
     """Configs 3/4 at N GPUs through the product's ShardedOptimizer: weak scaling -- the
     model has P x world params; each rank owns P of them (plus the replicated key tails)
@@ -675,7 +849,8 @@ def bench_sharded(args, world, rank, dev, n, P):
     from flame_amd import engine, shard, synth
     from flame_amd.optimizers import optimizer_provider
     G = P * world
-    opt = shard.ShardedOptimizer(optimizer_provider.get(args.workload), device=dev, fracs=_fracs(args, shard))
+    inner = optimizer_provider.get(args.workload)
+    opt = shard.ShardedOptimizer(inner, device=dev, fracs=_fracs(args, shard))
     opt.set_layout({"model": torch.empty(G, dtype=torch.float32, device="meta")})
     plan = opt.plan
     store, client_w = _local_slab(plan, n, dev, args.seed, 1e-2)
@@ -695,8 +870,11 @@ def bench_sharded(args, world, rank, dev, n, P):
         return cache
     arrived = [received() for _ in range(args.warmup + args.steps + (0 if fedavg else 1))]
 
+    rounds = [0]
+
     def step():
         cache = arrived.pop()
+        rounds[0] += 1
         if fedavg:        # syncfl top: FedAvg mutates the base in place (fedavg.py:74,87)
             opt.do(state["weights"], cache, total=total, num_trainers=n)
         else:             # FedOPT caller convention: weights = do(deepcopy(weights), ...)
@@ -708,6 +886,16 @@ def bench_sharded(args, world, rank, dev, n, P):
     elapsed, events = timed(world, args.steps, args.warmup, step)
     name = "flame_agg_reduce" if fedavg else "flame_fedopt_reduce_adapt"
     ks = kernel_stats(events, name)
+    # untimed self-check: every rank holds the same full model, sampled elements == the host
+    idx = sample_indices(plan, "model", seed=args.seed)
+    if fedavg:
+        expected = host_fedavg_rounds(args.seed, counts, idx, rounds[0])
+    else:
+        expected = host_fedopt_rounds(args.workload, engine.fedopt_scalars(inner.beta_1, inner.beta_2, inner.eta,
+                                                                           inner.tau),
+                                      args.seed, counts, idx, rounds[0])
+    gc = verify_sharded(state["weights"]["model"], idx, expected)
+    gc["rounds_checked"] = rounds[0]
     if rank == 0:
         lps = ks["launches"] / args.steps
         k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
@@ -729,11 +917,14 @@ def bench_sharded(args, world, rank, dev, n, P):
                          "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": name,
                          "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes, "launches_per_step": lps},
             "collective": _collective_note(plan, world, 4),
+            "process_group": process_group_info(),
+            "gather_check": gc,
             "cpu_baseline": None,
         }), flush=True)
     import torch.distributed as dist
     if dist.is_initialized():
         dist.destroy_process_group()
+    _checked(gc)
 
 
 def _middle_arrivals(args, M, C, client_w, stale, rnd):
@@ -821,8 +1012,19 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
     def step_sync():
         hier.sync_round(arrived.pop(), {"model": gw}, update_middle_weights=not fetched)
 
-    elapsed, events = timed(world, args.steps, args.warmup, step_sync if args.hier_mode == "sync" else step_fused)
+    rounds = [0]
+    body = step_sync if args.hier_mode == "sync" else step_fused
+
+    def step():
+        rounds[0] += 1
+        body()
+
+    elapsed, events = timed(world, args.steps, args.warmup, step)
     ks = kernel_stats(events, "flame_hier_fedbuff")
+    idx = sample_indices(plan, "model", seed=args.seed)
+    gc = verify_sharded(gw, idx, host_hier_rounds(args.seed + 4, M, C, idx, rounds[0], rnd, fetched,
+                                                  args.hier_mode == "sync"))
+    gc["rounds_checked"] = rounds[0]
     if rank == 0:
         lps = ks["launches"] / args.steps
         k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
@@ -846,10 +1048,13 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                          "kernel": "flame_hier_fedbuff", "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
                          "launches_per_step": lps},
             "collective": _collective_note(plan, world, 2),
+            "process_group": process_group_info(),
+            "gather_check": gc,
         }), flush=True)
     import torch.distributed as dist
     if dist.is_initialized():
         dist.destroy_process_group()
+    _checked(gc)
 
 
 def bench_fedbuff(args, world, rank, dev):
@@ -1261,4 +1466,13 @@ def bench_e2e(args, n, P, dev):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 - name the rank, fail non-zero (no restart)
+        import traceback
+        traceback.print_exc()
+        print(f"bench.py: rank {os.environ.get('RANK', '0')} of {os.environ.get('WORLD_SIZE', '1')} failed: "
+              f"{type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)

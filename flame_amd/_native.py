@@ -21,6 +21,7 @@ FLAME_FEDADAM, FLAME_FEDYOGI, FLAME_FEDADAGRAD = 0, 1, 2
 FLAME_OPT_STATE_ZERO = 1
 FLAME_OPT_XCD_MAP = 2
 FLAME_SEG_UNALIGNED = 1
+FLAME_SEG_CUR_IS_AVG = 2
 FLAME_HIER_TOP_ACCUM = 1
 FLAME_HIER_TOP_APPLY = 2
 FLAME_HIER_MID_READONLY = 4
@@ -39,6 +40,7 @@ EXPORTS = (
     "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
     "flame_slab_write", "flame_slab_write_2d",
+    "flame_launch_branches", "flame_launch_branch_name", "flame_launch_branch_count",
 )
 
 
@@ -103,6 +105,12 @@ def lib() -> ctypes.CDLL:
     L.flame_slab_write.argtypes = [vp, i32, vp]
     L.flame_slab_write_2d.restype = ctypes.c_int
     L.flame_slab_write_2d.argtypes = [vp, i32, vp]
+    L.flame_launch_branches.restype = i32
+    L.flame_launch_branches.argtypes = []
+    L.flame_launch_branch_name.restype = ctypes.c_char_p
+    L.flame_launch_branch_name.argtypes = [i32]
+    L.flame_launch_branch_count.restype = i64
+    L.flame_launch_branch_count.argtypes = [i32]
     if L.flame_abi_version() != 1:
         raise ImportError(f"flame_amd ABI mismatch: library {L.flame_abi_version()} != 1")
     _lib = L
@@ -113,3 +121,11 @@ def check(rc: int) -> None:
     if rc != FLAME_OK:
         msg = lib().flame_last_error().decode(errors="replace")
         raise FlameError(f"flame_amd status {rc}: {msg}")
+
+
+def launch_branch_counts() -> dict:
+    """{branch name: successful launches so far} for every launch branch of the C ABI
+    (flame_launch_branches); which kernel instantiation each call took."""
+    L = lib()
+    return {L.flame_launch_branch_name(i).decode(): int(L.flame_launch_branch_count(i))
+            for i in range(L.flame_launch_branches())}

@@ -18,6 +18,9 @@ ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "fedagg.hip")
 HDR = os.path.join(ROOT, "include", "flame_amd.h")
 LIB = os.path.join(PKG, "libflame_amd.so")
+# The kernel source WITH its compile-time sweep switches (default-off variants, diagnostics that
+# skip work): tools/kernel_sweep.py / hier_sweep.py build it into build/variants, never into LIB.
+SWEEP_SRC = os.path.join(ROOT, "tools", "sweep", "fedagg_sweep.hip")
 ARCH = os.environ.get("FLAME_AMD_ARCH", "gfx950")
 # host side: the restricted pickle VM of flame_amd.ingest (a CPython extension, plain gcc)
 VM_SRC = os.path.join(PKG, "csrc", "pickle_vm.c")
@@ -56,11 +59,13 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return VM_LIB
 
 
-def build(force: bool = False, verbose: bool = False, extra=None) -> str:
+def build(force: bool = False, verbose: bool = False) -> str:
+    """The product library: the fixed source, the fixed flags -- no ``-D`` overrides (a sweep
+    build that forgot to restore a macro must never become the shipped kernel)."""
     build_host(force=force, verbose=verbose)
     if not force and not stale():
         return LIB
-    cmd = [hipcc(), *HIPCC_FLAGS, *(extra or []), "-o", LIB, SRC]
+    cmd = [hipcc(), *HIPCC_FLAGS, "-o", LIB, SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -79,6 +79,7 @@ class Seg:
     v: int = 0
     clients: List[int] = field(default_factory=list)
     tile_stride: int = 0   # bytes between consecutive chunks of one client (0 = contiguous)
+    flags: int = 0         # FLAME_SEG_* bits set by the caller (FLAME_SEG_UNALIGNED is computed)
 
     def pointers(self):
         return [self.out, self.inp, self.cur, self.cur_out, self.m, self.v, self.tile_stride] + list(self.clients)
@@ -124,7 +125,7 @@ def plan(code: int, segs: Sequence[Seg], rates: Sequence, chunk: Optional[int] =
         row[:] = s.clients
         fixed = (s.out, s.inp, s.cur, s.cur_out, s.m, s.v)
         unaligned = bool(np.any(row % VEC_BYTES)) or any(p % VEC_BYTES for p in fixed if p)
-        head[i] = (*fixed, s.numel, begin, N.FLAME_SEG_UNALIGNED if unaligned else 0, s.tile_stride)
+        head[i] = (*fixed, s.numel, begin, s.flags | (N.FLAME_SEG_UNALIGNED if unaligned else 0), s.tile_stride)
         begin += -(-s.numel // chunk) if s.numel > 0 else 0
     if begin == 0:
         begin = 1  # all segments empty: one (idle) chunk keeps the launch valid
@@ -463,9 +464,11 @@ FEDOPT_VARIANT = {"fedadam": N.FLAME_FEDADAM, "fedyogi": N.FLAME_FEDYOGI, "fedad
 def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], base: List[torch.Tensor],
                          cur: List[torch.Tensor], cur_out: List[torch.Tensor], m: List[torch.Tensor],
                          v: List[torch.Tensor], clients: List[List[torch.Tensor]], rates: Sequence[float],
-                         hyper, state_zero: bool) -> None:
+                         hyper, state_zero: bool, cur_is_avg: Optional[Sequence[bool]] = None) -> None:
     """Fused FedAvg + FedOPT step (kernel: flame_fedopt_reduce_adapt), one launch per dtype
-    (fp32 / bf16 / fp16; every tensor of a segment shares its dtype)."""
+    (fp32 / bf16 / fp16; every tensor of a segment shares its dtype).  ``cur_is_avg[s]``:
+    segment s's current weights ARE its FedAvg result (FLAME_SEG_CUR_IS_AVG: the caller's
+    current aliases base, so d = avg - avg); ``cur[s]`` is then not read."""
     if not base:
         return
     device = base[0].device
@@ -475,17 +478,21 @@ def fedopt_reduce_adapt_(variant: str, avg_out: List[Optional[torch.Tensor]], ba
         groups.setdefault(dtype_code(b.dtype), []).append(s_)
     for code, idx in groups.items():
         segs, keep = [], []
+        p_alias = 0
         for s_ in idx:
-            for t in (base[s_], cur[s_], cur_out[s_], m[s_], v[s_]):
+            alias = bool(cur_is_avg[s_]) if cur_is_avg is not None else False
+            for t in (base[s_], cur_out[s_], m[s_], v[s_]) + (() if alias else (cur[s_],)):
                 assert t.dtype == base[s_].dtype and t.is_contiguous() and t.device == device
             row, tstride = _client_row(clients[s_], base[s_], device, keep)
             segs.append(Seg(base[s_].numel(), out=avg_out[s_].data_ptr() if avg_out[s_] is not None else 0,
-                            inp=base[s_].data_ptr(), cur=cur[s_].data_ptr(), cur_out=cur_out[s_].data_ptr(),
-                            m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row, tile_stride=tstride))
+                            inp=base[s_].data_ptr(), cur=0 if alias else cur[s_].data_ptr(),
+                            cur_out=cur_out[s_].data_ptr(), m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row,
+                            tile_stride=tstride, flags=N.FLAME_SEG_CUR_IS_AVG if alias else 0))
+            p_alias += base[s_].numel() if alias else 0
         P = sum(sg.numel for sg in segs)
         isz = ITEMSIZE[code]
         # clients + base + cur (+ m, v unless zero state) read; avg, m, v, cur_out written
-        nbytes = isz * P * (len(rates) + 2 + (0 if state_zero else 2) + 4)
+        nbytes = isz * (P * (len(rates) + 2 + (0 if state_zero else 2) + 4) - p_alias)
         h = list(hyper)
         if code in (N.FLAME_BF16, N.FLAME_F16):  # torch-CPU rounds the scalar of `sqrt(v) + tau`
             h[5] = float(torch.tensor(float(h[5]), dtype=base[idx[0]].dtype))

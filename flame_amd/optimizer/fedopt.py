@@ -35,7 +35,21 @@ logger = logging.getLogger(__name__)
 
 
 def _same_storage(a, b) -> bool:
-    return a is b or (a.device == b.device and a.numel() > 0 and a.data_ptr() == b.data_ptr())
+    return a is b or (a.device == b.device and a.numel() > 0 and a.data_ptr() == b.data_ptr()
+                      and a.shape == b.shape and a.stride() == b.stride())
+
+
+def _byte_range(t):
+    end = t.data_ptr() + t.element_size() * (1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()) if n > 0))
+    return t.data_ptr(), end
+
+
+def _overlaps(a, b) -> bool:
+    """Do two tensors' byte ranges intersect?"""
+    if a.numel() == 0 or b.numel() == 0:
+        return False
+    (a0, a1), (b0, b1) = _byte_range(a), _byte_range(b)
+    return a0 < b1 and b0 < a1
 
 
 class FedOPT(FedAvg):
@@ -100,9 +114,12 @@ class FedOPT(FedAvg):
             dt = base_weights[k].dtype
             # the eager caller hands the same base dict to every do() of a round, so after the
             # round-1 passthrough current IS base (eager_syncfl/top_aggregator.py:42,75): the
-            # reference's d = avg - current is then 0; such keys take the op-sequence path
+            # reference's d = avg - current is then 0 -- the fused kernel takes cur = avg for such
+            # keys (FLAME_SEG_CUR_IS_AVG); only a partial overlap takes the op-sequence path
             aliased = k in current and _same_storage(current[k], base_weights[k])
-            ok = (dt in float_dts and k in current and not aliased
+            partial = (k in current and not aliased and current[k].device == base_weights[k].device
+                       and _overlaps(current[k], base_weights[k]))
+            ok = (dt in float_dts and k in current and not partial
                   and current[k].dtype == dt and current[k].shape == base_weights[k].shape
                   and all(k in w and w[k].dtype == dt for w, _ in entries)
                   and (self.m_t is None or (k in self.m_t and self.m_t[k].dtype == dt
@@ -141,7 +158,9 @@ class FedOPT(FedAvg):
     def _launch_fused(self, ks, base_weights, current, entries, device, hyper, state_zero, alloc, new_cur):
         """One flame_fedopt_reduce_adapt launch per dtype over keys ``ks``."""
         targets = [engine._Target(base_weights[k], device) for k in ks]
-        curs = [engine._as_device(current[k], device) for k in ks]
+        alias = [_same_storage(current[k], base_weights[k]) for k in ks]
+        # an aliased key's current is the FedAvg result itself: the kernel takes cur = avg
+        curs = [t.dev if a else engine._as_device(current[k], device) for t, a, k in zip(targets, alias, ks)]
         outs = [alloc(k, base_weights[k].dtype, base_weights[k].shape) if alloc is not None else
                 torch.empty(base_weights[k].shape, dtype=base_weights[k].dtype, device=device) for k in ks]
         ms, vs = [], []
@@ -160,10 +179,10 @@ class FedOPT(FedAvg):
         if self.split_launch:
             engine.reduce_(avgs, avgs, clients, rates)
             engine.fedopt_reduce_adapt_(self.variant, [None] * len(ks), avgs, curs, outs, ms, vs,
-                                        [[] for _ in ks], [], hyper, state_zero)
+                                        [[] for _ in ks], [], hyper, state_zero, cur_is_avg=alias)
         else:
             engine.fedopt_reduce_adapt_(self.variant, avgs, avgs, curs, outs, ms, vs, clients, rates, hyper,
-                                        state_zero)
+                                        state_zero, cur_is_avg=alias)
         for t in targets:
             t.writeback()
         new_cur.update(zip(ks, outs))

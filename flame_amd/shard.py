@@ -254,8 +254,13 @@ class _Comm:
         self.coalesce = COALESCE
         self._works = []
 
-    def all_gather_inplace(self, pairs) -> None:
+    def _fail(self, wave, what, e):
+        raise RuntimeError(f"flame_amd.shard: rank {self.rank} of {self.world} ({self.backend}): {what} of "
+                           f"wave {wave} failed: {e}") from e
+
+    def all_gather_inplace(self, pairs, wave=None) -> None:
         """``pairs``: [(piece, owned)] with ``owned`` this rank's range inside ``piece``.
+        A failing collective raises naming this rank and ``wave``.
 
         One body for RCCL and for gloo on CPU tensors (the world 2 / 3 / 8 CPU tests run it):
         async, in place (NCCL's in-place all-gather, ``sendbuff == recvbuff + rank * count``),
@@ -265,6 +270,12 @@ class _Comm:
         share one GPU; gloo has no device all-gather) stages through the host synchronously."""
         if not pairs or self.dist is None:
             return
+        try:
+            self._all_gather_inplace(pairs, wave)
+        except Exception as e:  # noqa: BLE001 - re-raised with the rank and wave
+            self._fail(wave, "all-gather", e)
+
+    def _all_gather_inplace(self, pairs, wave) -> None:
         d = self.dist
         if self.backend == "gloo" and pairs[0][0].is_cuda:
             for piece, owned in pairs:
@@ -283,20 +294,24 @@ class _Comm:
             # to bf16); RCCL would take mixed dtypes, the per-dtype split costs it nothing measurable
             if cm_factory is None or len(group) == 1:
                 for piece, owned in group:
-                    self._works.append(d.all_gather_into_tensor(piece, owned, group=self.group, async_op=True))
+                    self._works.append((wave, d.all_gather_into_tensor(piece, owned, group=self.group,
+                                                                       async_op=True)))
                 GATHER_STATS["async"] += len(group)
                 continue
             with cm_factory(group=self.group, async_ops=True) as cm:
                 for piece, owned in group:
                     d.all_gather_into_tensor(piece, owned, group=self.group)
-            self._works.append(cm)
+            self._works.append((wave, cm))
             GATHER_STATS["coalesced"] += 1
 
     def wait(self) -> None:
         """Order the launch stream after every gather issued so far (host does not block)."""
         works, self._works = self._works, []
-        for w in works:
-            w.wait()
+        for wave, w in works:
+            try:
+                w.wait()
+            except Exception as e:  # noqa: BLE001 - re-raised with the rank and wave
+                self._fail(wave, "wait on the all-gather", e)
 
 
 class _Work:
@@ -382,7 +397,7 @@ class _Gatherer:
             if not s.tail and n in self.target:
                 t = self.target[n]
                 pairs.append((t[s.g0:s.g1], t[s.lo:s.hi]))
-        self.comm.all_gather_inplace(pairs)
+        self.comm.all_gather_inplace(pairs, wave)
 
     def finish(self):
         """Issue what is left, wait for the gathers; the caller's dict (in place) or a new

@@ -84,6 +84,11 @@ extern "C" {
 
 /* per-segment flag (flame_segment.flags) */
 #define FLAME_SEG_UNALIGNED 1    /* some pointer of this segment is not 16-byte aligned */
+#define FLAME_SEG_CUR_IS_AVG 2   /* flame_fedopt_reduce_adapt: `cur` IS the FedAvg result (the eager
+                                    caller's current_weights alias base_weights after the round-1
+                                    passthrough, eager_syncfl/top_aggregator.py:42,75 +
+                                    fedopt.py:87-88): cur takes the reduced value, d = avg - avg;
+                                    seg.cur is not read */
 
 /*
  * One contiguous run of elements (typically one state_dict tensor, or one
@@ -163,6 +168,8 @@ int64_t flame_agg_argmeta_max_bytes(void);
  *   d = avg - cur; m = b1*m + omb1*d;
  *   Adam: v = b2*v + omb2*(d*d);  Yogi: v = v - omb2*(d*d)*sign(v - d*d);  AdaGrad: v = v + d*d
  *   cur_out = cur + (eta*m) / (sqrt(v) + tau)
+ * (a segment flagged FLAME_SEG_CUR_IS_AVG takes cur = avg, as the reference does when
+ * current_weights and base_weights are one object).
  * Scalars are the roundings torch applies to the Python floats: b1 = f32(beta_1),
  * omb1 = f32(1 - beta_1), b2 = f32(beta_2), omb2 = f32(1 - beta_2), eta = f32(eta),
  * tau = f32(tau) for fp32 but dtype(tau) for bf16/fp16 (torch-CPU rounds a scalar to a
@@ -356,6 +363,18 @@ typedef struct flame_tile_copy {
 } flame_tile_copy;
 int flame_slab_write(const flame_tile_copy *table, int32_t n_entries, void *stream);
 int flame_slab_write_2d(const flame_tile_copy *table, int32_t n_entries, void *stream);
+
+/*
+ * Launch-branch counters (test and audit support; no reference counterpart).  Every
+ * host-side branch of the launch entry points above that picks a kernel instantiation
+ * (dtype, variant, residency, store-group mode) has an index in [0, flame_launch_branches());
+ * each successful launch increments its branch's process-wide counter.
+ *   flame_launch_branch_name  : "entry/mode/dtype[/variant]", NULL outside the range
+ *   flame_launch_branch_count : launches so far, -1 outside the range
+ */
+int32_t flame_launch_branches(void);
+const char *flame_launch_branch_name(int32_t branch);
+int64_t flame_launch_branch_count(int32_t branch);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Interleaved A/B of compile-time variants of flame_feddyn_round through the FedDyn drop-in,
-in ONE process: each variant is a build of flame_amd/csrc/fedagg.hip in build/variants
+in ONE process: each variant is a build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) in build/variants
 (tools/kernel_sweep.py --build), swapped in as the engine's native library round by round;
 the same slab-resident arrivals drive one FedDyn instance per variant; kernel time from HIP
 events; cld_model checked bitwise across variants every round.

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B sweep of compile-time variants of flame_hier_fedbuff (config 5 shard).
 
-Each variant is a separate build of flame_amd/csrc/fedagg.hip loaded side by side with
+Each variant is a separate build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) loaded side by side with
 ctypes; all run in ONE process on the same device-resident tiled slab (64 middles x 64
 arrivals x 15.6M bf16 by default), rounds interleaved; outputs (middle weights, top
 aggregate, top weights) are checked bitwise against the first variant from identical state.
@@ -113,7 +113,7 @@ def build_variants(names):
     for name in names:
         defs = [f"-D{k}={v}" for k, v in VARIANTS[name].items()]
         out = os.path.join(VDIR, f"lib_{name}.so")
-        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SRC])
+        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SWEEP_SRC])
         print("built", out, flush=True)
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B sweep of compile-time variants of flame_agg_reduce (fp32).
 
-Each variant is a separate build of flame_amd/csrc/fedagg.hip (FLAME_BLOCK,
+Each variant is a separate build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) (FLAME_BLOCK,
 FLAME_CU, FLAME_VPT, FLAME_PIPE, FLAME_NT) loaded side by side with ctypes;
 all run in ONE process on the same device-resident 1024 x 25M slab, rounds
 interleaved (cdna_hip_programming.md §5.4 rule 24), outputs checked bitwise
@@ -152,7 +152,7 @@ def build_variants(names):
     for name in names:
         defs = [f"-D{k}={v}" for k, v in VARIANTS[name].items()]
         out = os.path.join(VDIR, f"lib_{name}.so")
-        cmd = [B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SRC]
+        cmd = [B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SWEEP_SRC]
         subprocess.check_call(cmd)
         print("built", out, flush=True)
 

@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -33,43 +32,164 @@
 
 namespace {
 
-// Tunables: fixed for the shipped build (each chosen by an interleaved A/B sweep on MI355X,
-// DESIGN.md §4).  The sweep source tools/sweep/fedagg_sweep.hip exposes them -- and the
-// variants measured no faster, which this file no longer carries -- as -D switches.
-constexpr int kBlock = 256;          // lanes per workgroup of the reduction kernels
-constexpr int kVPT = 1;              // 16-byte vectors per lane per client
-constexpr int kClientUnroll = 8;     // clients whose loads are issued together per lane (full residency)
-constexpr int kClientUnroll16 = 8;   // the same for 16-bit dtypes (8 elements per lane vector)
-// flame_agg_reduce, launches of >= kLoMinClients clients over >= kLoMinChunks chunks: 2 workgroups
-// per CU (kLoLds of dynamic LDS, unused) with a client unroll of 3 (16-bit: 4) -- fewer loads in
-// flight read HBM faster (C3: 14.90 -> 14.18 ms, 99 % of a region probe at that residency;
-// profiles/r03ze_c3_sweep.log, r03zf_c3_sweep.log, r03zf_c3_bf16_sweep.log)
-constexpr int kLoUnroll = 3;
-constexpr int kLoUnroll16 = 4;
-constexpr int kLoLds = 65536;
-constexpr int kLoMinClients = 64;    // 64 x 100M fp32: 4.04 -> 3.90 ms (profiles/r03zn_c64_lomin.log)
-constexpr int64_t kLoMinChunks = 4096;
-// FedOPT (fp32, >= 8 x 256 x kOptWGC chunks): kOptWGC chunks per workgroup, their avg/m/v/cur
-// blocks held in LDS (16 KiB per chunk -> 2 workgroups per CU) and stored in one burst at the end,
-// client unroll kOptUnroll (profiles/r02_fedopt_wgc_sweep.log, r03zf_c4_sweep.log, r03zg_c4_sweep.log)
-constexpr int kOptWGC = 4;
-constexpr int kOptUnroll = 3;
-// hierarchy kernel: register store groups of kHB middles (16-bit client unroll kHierUnroll16);
-// launches of >= kHLdsMinMids middles hold store groups of kHBL middles in LDS (4 KiB each per
-// workgroup, 2 workgroups per CU) with a 16-bit unroll of kHierLdsUnroll16 (C5 shard 20.99 ->
-// 19.51 ms, profiles/r02_hier_lds_sweep.log); one middle over >= 64 arrivals and >= 4,096 chunks
-// (a FedBuff aggregator's fused scale_add): low residency, unroll 3 (profiles/r03zv_fedbuff_*.log)
-constexpr int kHB = 8;
-constexpr int kHierUnroll16 = 4;
-constexpr int kHBL = 16;
-constexpr int kHierLdsUnroll16 = 6;
-constexpr int kHLdsMinMids = 16;
-constexpr int kHLoUnroll = 3;
-constexpr int kHLoMinClients = 64;
-constexpr int64_t kHLoMinChunks = 4096;
-constexpr int kHLoLdsF32 = 65536;    // 2 workgroups per CU
-constexpr int kHLoLds16 = 53248;     // 3 workgroups per CU
-constexpr int kDynUnroll = 4;        // FedDyn kernel: program steps whose loads are issued together
+// Tunables (compile-time; defaults chosen by tools/kernel_sweep.py on MI355X)
+#ifndef FLAME_BLOCK
+#define FLAME_BLOCK 256   // lanes per workgroup of the reduction kernels
+#endif
+#ifndef FLAME_CU
+#define FLAME_CU 8        // clients whose loads are issued together per lane
+#endif
+#ifndef FLAME_CU16
+#define FLAME_CU16 FLAME_CU  // client unroll for 16-bit dtypes (8 elements per lane vector)
+#endif
+#ifndef FLAME_VPT
+#define FLAME_VPT 1       // 16-byte vectors per lane per client (block-strided)
+#endif
+#ifndef FLAME_PIPE
+#define FLAME_PIPE 0      // 1: prefetch the next client batch before combining the current one
+#endif
+#ifndef FLAME_BF16_HI
+#define FLAME_BF16_HI 0   // 1: bf16 rounding as one v_cvt_pk_bf16_f32 into the high half (bf16_round)
+#endif
+#ifndef FLAME_BF16_PK
+#define FLAME_BF16_PK 0   // 1: bf16 client combine on packed fp32 pairs (reduce_clients)
+#endif
+#ifndef FLAME_DYN_OCC_LDS
+#define FLAME_DYN_OCC_LDS 0  // sweep: dynamic LDS bytes per FedDyn workgroup (caps its residency; unused)
+#endif
+#ifndef FLAME_HLO
+#define FLAME_HLO 1       // flame_hier_fedbuff, one middle over >= 64 arrivals and >= 4,096 chunks: low residency
+#endif
+#ifndef FLAME_HXP
+#define FLAME_HXP 0       // hierarchy kernel (LDS store groups, FedBuff mode): > 0 = one double-buffered stream
+                          // of that many arrivals per batch across the middles (must divide the arrivals)
+#endif
+#ifndef FLAME_SPF
+#define FLAME_SPF 0       // 1: prefetch the next client batch's pointers (scalar loads) behind the current
+                          // batch's vector loads (reduce_clients, vector path)
+#endif
+#ifndef FLAME_TAILB
+#define FLAME_TAILB 0     // 1: the init-first client joins the first batch and the last n % CU clients
+                          // load together (reduce_clients, vector path)
+#endif
+#ifndef FLAME_NT
+#define FLAME_NT 1        // non-temporal client loads (read once)
+#endif
+#ifndef FLAME_ST_NT
+#define FLAME_ST_NT 4     // output store policy: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 sc0 sc1 nt (see st_v)
+#endif
+#ifndef FLAME_NOSTORE
+#define FLAME_NOSTORE 0   // DIAGNOSTIC sweep variant only: skip the reduction's output store
+#endif
+#ifndef FLAME_WGC
+#define FLAME_WGC 1       // chunks per workgroup of the reduction kernel
+#endif
+#ifndef FLAME_DEFER_ST
+#define FLAME_DEFER_ST 0  // 1: store a workgroup's FLAME_WGC output chunks together at its end
+#endif
+#ifndef FLAME_HCU16
+#define FLAME_HCU16 4     // client unroll of the hierarchy kernel for 16-bit dtypes (with FLAME_HBATCH 8:
+                          // 90 VGPRs, 5 waves/SIMD; unroll 8 needs 123 VGPRs for the same time)
+#endif
+#ifndef FLAME_HWPE
+#define FLAME_HWPE 0      // hierarchy kernel: minimum waves per SIMD to compile for (0 = compiler's choice)
+#endif
+#ifndef FLAME_HPF
+#define FLAME_HPF 0       // hierarchy kernel: load each middle's weights before its arrival loop
+#endif
+#ifndef FLAME_HDIAG
+#define FLAME_HDIAG 0     // DIAGNOSTIC sweep variants only: 1 = skip middle-weight stores, 2 = also skip their loads
+#endif
+#ifndef FLAME_BUFLD
+#define FLAME_BUFLD 0     // sweep: client loads as buffer loads, cache policy FLAME_BUFLD - 1 (0 = global loads)
+#endif
+#ifndef FLAME_HBATCH
+#define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
+                          // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
+#endif
+#ifndef FLAME_HLDS
+#define FLAME_HLDS 1      // hierarchy kernel, launches with >= FLAME_HLDS_MIN_MIDS middles: 1 = hold a store
+                          // group of FLAME_HLDS_BATCH middles' weights in LDS (4 KiB each per workgroup,
+                          // 2 workgroups per CU) instead of FLAME_HBATCH in registers, arrivals unrolled
+                          // by FLAME_HLDS_CU16 (C5 shard: 20.99 -> 19.51 ms, 0.7 % above the no-store
+                          // diagnostic; tools/hier_sweep.py, profiles/r02_hier_lds_sweep.log)
+#endif
+#ifndef FLAME_HLDS_BATCH
+#define FLAME_HLDS_BATCH 16
+#endif
+#ifndef FLAME_HLDS_CU16
+#define FLAME_HLDS_CU16 6
+#endif
+#ifndef FLAME_HLDS_MIN_MIDS
+#define FLAME_HLDS_MIN_MIDS 16
+#endif
+#ifndef FLAME_HST
+#define FLAME_HST FLAME_ST_NT  // hierarchy kernel: store policy of the middle weights (encoding of FLAME_ST_NT)
+#endif
+#ifndef FLAME_DYN_CU
+#define FLAME_DYN_CU 4    // FedDyn kernel: program steps whose loads are issued together
+#endif
+#ifndef FLAME_DYN_LDS
+#define FLAME_DYN_LDS 0   // FedDyn kernel: > 0 = hold the updated histories of that many program steps in
+                          // LDS (4 KiB each per workgroup) and store them in one burst (multiple of FLAME_DYN_CU)
+#endif
+#ifndef FLAME_DYN_XCD
+#define FLAME_DYN_XCD 1   // FedDyn kernel: XCD-contiguous chunk map (see FLAME_AGG_XCD_MAP); histories are
+                          // per-end rows by default: 512 x 12M fp32 -0.7 % (cache order) / -1.4 %
+                          // (other order), tools/feddyn_sweep.py, profiles/r02_feddyn_xcd_sweep.log
+#endif
+#ifndef FLAME_DYN_ST
+#define FLAME_DYN_ST FLAME_ST_NT  // FedDyn kernel: store policy of the updated histories
+#endif
+#ifndef FLAME_OCC_LDS
+#define FLAME_OCC_LDS 0   // sweep variants: dynamic LDS bytes per reduction / hierarchy workgroup (caps
+                          // resident workgroups per CU at 160 KiB / FLAME_OCC_LDS; the kernels use no LDS)
+#endif
+#ifndef FLAME_LO_CU
+#define FLAME_LO_CU 3     // flame_agg_reduce, launches of >= FLAME_LO_MIN_CLIENTS clients and >= FLAME_LO_MIN_CHUNKS
+                          // chunks: 2 workgroups per CU (FLAME_LO_LDS of dynamic LDS, unused) with this client
+                          // unroll -- fewer loads in flight reads HBM faster (C3: 14.90 -> 14.18 ms, 7.24 TB/s =
+                          // 99 % of a region probe at that residency; tools/kernel_sweep.py occ2cu3 / lo0,
+                          // profiles/r03ze_c3_sweep.log, r03zf_c3_sweep.log); 0 = off
+#endif
+#ifndef FLAME_LO_CU16
+#define FLAME_LO_CU16 4   // the same for 16-bit dtypes (8 elements per load: unroll 3 reads 6.49 TB/s, 4 6.99;
+                          // bf16 1024 x 25M, profiles/r03zf_c3_bf16_sweep.log)
+#endif
+#ifndef FLAME_LO_LDS
+#define FLAME_LO_LDS 65536
+#endif
+#ifndef FLAME_LO_MIN_CLIENTS
+#define FLAME_LO_MIN_CLIENTS 64  // 64 x 100M fp32: 4.04 -> 3.90 ms, bf16 64 x 200M: 4.09 -> 4.00 ms
+                                 // (profiles/r03zn_c64_lomin.log, r03zn_b64_lomin.log)
+#endif
+#ifndef FLAME_LO_MIN_CHUNKS
+#define FLAME_LO_MIN_CHUNKS 4096
+#endif
+#ifndef FLAME_XCD_SWIZZLE
+#define FLAME_XCD_SWIZZLE 0  // sweep variant: each XCD (workgroups are dispatched to XCDs round-robin)
+                             // streams one contiguous eighth of the chunks
+#endif
+#ifndef FLAME_OPT_PREFETCH
+#define FLAME_OPT_PREFETCH 0  // FedOPT: issue the cur/m/v loads before the client loop
+#endif
+#ifndef FLAME_OPT_WGC
+#define FLAME_OPT_WGC 4   // FedOPT (fp32, >= 8 x 256 x WGC chunks): chunks per workgroup; > 1 holds their
+                          // avg/m/v/cur blocks in LDS (16 KiB per chunk; 64 KiB at 4 -> two workgroups
+                          // per CU) and stores them in one burst at the end.  C4 FedAdam, tiled slab:
+                          // 1 chunk 15.18, 8 chunks (one workgroup per CU, unroll 8) 14.62 ms (round 2,
+                          // profiles/r02_fedopt_wgc_sweep.log); 4 chunks with unroll 3 (fewer loads in
+                          // flight, as flame_agg_reduce's FLAME_LO_CU) 1.8-2.0 % under 8 chunks / unroll 8
+                          // (profiles/r03zf_c4_sweep.log, r03zg_c4_sweep.log)
+#endif
+#ifndef FLAME_OPT_CU
+#define FLAME_OPT_CU 3    // FedOPT fp32 client unroll with FLAME_OPT_WGC > 1
+#endif
+
+constexpr int kBlock = FLAME_BLOCK;
+constexpr int kHB = FLAME_HBATCH;
+constexpr int kVPT = FLAME_VPT;
+constexpr int kWGC = FLAME_WGC;
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -91,8 +211,17 @@ int check_launch(const char* what) {
 
 // ---------------------------------------------------------------- rounding helpers
 __device__ __forceinline__ float bf16_round(float x) {
+#if FLAME_BF16_HI
+    // RNE fp32 -> bf16 -> fp32 in ONE instruction: v_cvt_pk_bf16_f32 packs (lo, hi) = (bf16(0),
+    // bf16(x)), and that dword IS the fp32 value of bf16(x) (the compiler's lowering of the cast
+    // puts x in the low half and shifts it back up: two instructions per rounding)
+    float r;
+    asm("v_cvt_pk_bf16_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
     // RNE fp32 -> bf16 -> fp32 (v_cvt_pk_bf16_f32 on gfx950)
     return static_cast<float>(static_cast<__bf16>(x));
+#endif
 }
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
     return __uint_as_float(static_cast<uint32_t>(b) << 16);
@@ -184,9 +313,12 @@ template <typename T> using gcptr = const __attribute__((address_space(1))) T*;
 template <typename T> __device__ __forceinline__ gcptr<T> G(const T* p) { return (gcptr<T>)(p); }
 template <typename T> __device__ __forceinline__ gptr<T> G(T* p) { return (gptr<T>)(p); }
 
-// Client updates are read exactly once: non-temporal loads.
 __device__ __forceinline__ V16 ld_nt(const void* p) {
+#if FLAME_NT
     u4 x = __builtin_nontemporal_load(G(reinterpret_cast<const u4*>(p)));
+#else
+    u4 x = *G(reinterpret_cast<const u4*>(p));
+#endif
     V16 r; r.w[0] = x[0]; r.w[1] = x[1]; r.w[2] = x[2]; r.w[3] = x[3];
     return r;
 }
@@ -201,12 +333,35 @@ __device__ __forceinline__ V16 ld_v(const void* p) {
 // because no builtin sets sc0/sc1; `s_nop 1` covers the store-data hazard.
 __device__ __forceinline__ void st_v(void* p, const V16& v) {
     u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+#if FLAME_ST_NT == 1
+    __builtin_nontemporal_store(x, G(reinterpret_cast<u4*>(p)));
+#elif FLAME_ST_NT == 2
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#elif FLAME_ST_NT == 3
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#elif FLAME_ST_NT == 4
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
-}
-// A plain (write-back) vector store: the slab insert, whose tiles are read again soon.
-__device__ __forceinline__ void st_plain(void* p, const V16& v) {
-    u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+#else
     *G(reinterpret_cast<u4*>(p)) = x;
+#endif
+}
+// Store with an explicit policy (same encoding as FLAME_ST_NT).
+template <int POL>
+__device__ __forceinline__ void st_pol(void* p, const V16& v) {
+    u4 x = {v.w[0], v.w[1], v.w[2], v.w[3]};
+    if constexpr (POL == 1) {
+        __builtin_nontemporal_store(x, G(reinterpret_cast<u4*>(p)));
+    } else if constexpr (POL == 2) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 3) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 4) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else if constexpr (POL == 5) {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    } else {
+        *G(reinterpret_cast<u4*>(p)) = x;
+    }
 }
 template <typename T> __device__ __forceinline__ T ld1(const T* p) { return *G(p); }
 template <typename T> __device__ __forceinline__ void st1(T* p, T x) { *G(p) = x; }
@@ -263,6 +418,27 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
     auto rate64 = [&](int c) -> double { if constexpr (DT == FLAME_F64) return r64[c]; else return 0.0; };
     auto load_client = [&](int c, T (&x)[kVPT][EPT]) {
         const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[c]) + coff);
+#if FLAME_BUFLD
+        if constexpr (VEC) {
+            // buffer loads: the client's chunk base (wave-uniform) in a scalar resource, the
+            // lane's byte offset in one VGPR; FLAME_BUFLD - 1 = cache policy (sc0 1, nt 2, sc1 16)
+            const int32_t lane_b = static_cast<int32_t>(threadIdx.x) * EPT * static_cast<int32_t>(sizeof(T));
+            const uint64_t wb = cp[c] + static_cast<uint64_t>(coff - lane_b);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb));
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb >> 32));
+            void* base = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) {
+                u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, lane_b + v * static_cast<int32_t>(VS * sizeof(T)), 0,
+                                                             FLAME_BUFLD - 1);
+                V16 t;
+                t.w[0] = q[0]; t.w[1] = q[1]; t.w[2] = q[2]; t.w[3] = q[3];
+                unpack<T, EPT>(t, x[v]);
+            }
+            return;
+        }
+#endif
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             if constexpr (VEC) {
@@ -274,12 +450,144 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
         }
     };
     auto combine_r = [&](const float r, const double rd, const T (&x)[kVPT][EPT]) {
+#if FLAME_BF16_PK
+        if constexpr (DT == FLAME_BF16) {
+            // the same two roundings per element, two elements per packed-fp32 multiply and add
+            // (v_pk_mul_f32 / v_pk_add_f32: each lane's result is the IEEE fp32 op's)
+            using f2 = __attribute__((ext_vector_type(2))) float;
+            const f2 r2 = {r, r};
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; j += 2) {
+                    const f2 x2 = {X::ld(x[v][j]), X::ld(x[v][j + 1])};
+                    f2 t2 = x2 * r2;
+                    t2 = f2{bf16_round(t2.x), bf16_round(t2.y)};
+                    f2 a2 = f2{acc[v][j], acc[v][j + 1]} + t2;
+                    acc[v][j] = bf16_round(a2.x);
+                    acc[v][j + 1] = bf16_round(a2.y);
+                }
+            return;
+        }
+#endif
 #pragma unroll
         for (int v = 0; v < kVPT; ++v)
 #pragma unroll
             for (int j = 0; j < EPT; ++j) acc[v][j] = X::add(acc[v][j], X::tmp(x[v][j], r, rd));
     };
     auto combine = [&](int c, const T (&x)[kVPT][EPT]) { combine_r(rate32(c), rate64(c), x); };
+#if FLAME_SPF
+    if constexpr (VEC && CU > 1 && DT != FLAME_F64) {
+        // the next batch's client pointers AND rates are read (scalar loads) while the current
+        // batch's vector loads are in flight: a batch never waits on its pointer row before
+        // issuing, nor its combine on a rate load (a rate loaded in the combine, as the plain
+        // loop does, makes the combine's lgkmcnt(0) wait for every scalar load in flight, the
+        // prefetched pointers included).  Scalar-cache misses matter once a launch's pointer
+        // and rate rows outgrow the scalar cache (4,096 arrivals: 48 KiB per workgroup)
+        if (init_first && n > 0) {    // the init-first client's load goes out with the first batch
+            const int r = n < CU ? n : CU;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(u, x[u]);
+            const float r0 = rate32(0);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[0][v][j], r0, 0.0);
+#pragma unroll
+            for (int u = 1; u < CU; ++u)
+                if (u < r) combine(u, x[u]);
+            i = r;
+        }
+        if (i + CU <= n) {
+            uint64_t pa[CU];
+            float ra[CU];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                pa[u] = cp[i + u];
+                ra[u] = r32[i + u];
+            }
+            while (true) {
+                T x[CU][kVPT][EPT];
+#pragma unroll
+                for (int u = 0; u < CU; ++u) {
+                    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(pa[u]) + coff);
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) unpack<T, EPT>(ld_nt(p + v * VS), x[u][v]);
+                }
+                float rc[CU];
+#pragma unroll
+                for (int u = 0; u < CU; ++u) rc[u] = ra[u];
+                const bool more = i + 2 * CU <= n;
+                if (more) {
+#pragma unroll
+                    for (int u = 0; u < CU; ++u) {
+                        pa[u] = cp[i + CU + u];
+                        ra[u] = r32[i + CU + u];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < CU; ++u) combine_r(rc[u], 0.0, x[u]);
+                i += CU;
+                if (!more) break;
+            }
+        }
+        if (i < n) {                  // the last n % CU clients' loads go out together
+            const int r = n - i;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) combine(i + u, x[u]);
+        }
+        return;
+    }
+#endif
+#if FLAME_TAILB
+    if constexpr (VEC && CU > 1) {
+        // whole batches only: the init-first client's load goes out with the first batch and the
+        // last n % CU clients' loads go out together (one wait each, not one round trip per
+        // client); the arithmetic is the same sequence, in client order
+        if (init_first && n > 0) {
+            const int r = n < CU ? n : CU;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(u, x[u]);
+            const float r0 = rate32(0);
+            const double rd0 = rate64(0);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[0][v][j], r0, rd0);
+#pragma unroll
+            for (int u = 1; u < CU; ++u)
+                if (u < r) combine(u, x[u]);
+            i = r;
+        }
+        for (; i + CU <= n; i += CU) {
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, x[u]);
+        }
+        if (i < n) {
+            const int r = n - i;
+            T x[CU][kVPT][EPT];
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) load_client(i + u, x[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u)
+                if (u < r) combine(i + u, x[u]);
+        }
+        return;
+    }
+#endif
     if (init_first && n > 0) {
         T x[kVPT][EPT];
         load_client(0, x);
@@ -291,6 +599,34 @@ __device__ __forceinline__ void reduce_clients(typename Tr<DT>::A (&acc)[kVPT][T
             for (int j = 0; j < EPT; ++j) acc[v][j] = X::tmp(x[v][j], r, rd);
         i = 1;
     }
+#if FLAME_PIPE
+    if (VEC && i + CU <= n) {
+        // two register batches: batch k+1's loads are in flight while batch k is combined
+        T xa[CU][kVPT][EPT], xb[CU][kVPT][EPT];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) load_client(i + u, xa[u]);
+        while (true) {
+            const bool nb = i + 2 * CU <= n;
+            if (nb) {
+#pragma unroll
+                for (int u = 0; u < CU; ++u) load_client(i + CU + u, xb[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, xa[u]);
+            i += CU;
+            if (!nb) break;
+            const bool na = i + 2 * CU <= n;
+            if (na) {
+#pragma unroll
+                for (int u = 0; u < CU; ++u) load_client(i + CU + u, xa[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) combine(i + u, xb[u]);
+            i += CU;
+            if (!na) break;
+        }
+    }
+#endif
     for (; i + CU <= n; i += CU) {
         T x[CU][kVPT][EPT];
 #pragma unroll
@@ -374,7 +710,12 @@ template <typename T>
 __device__ __forceinline__ void store_chunk(T* op, const V16 (&ov)[kVPT]) {
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * (16 / sizeof(T));
 #pragma unroll
-    for (int v = 0; v < kVPT; ++v) st_v(op + v * VS, ov[v]);
+    for (int v = 0; v < kVPT; ++v) {
+#if FLAME_NOSTORE
+        if (__builtin_expect(ov[v].w[0] == 0x12345u && ov[v].w[1] == 0x54321u, 0))   // keeps the math live
+#endif
+        st_v(op + v * VS, ov[v]);
+    }
 }
 
 // Workgroup slot of block b when the 8 XCDs (dispatched round-robin) each take one
@@ -384,18 +725,40 @@ __device__ __forceinline__ int64_t xcd_slot(int64_t b, int64_t n) {
     return x * q + (x < r ? x : r) + b / 8;
 }
 
-// One chunk per workgroup (chunk = workgroup slot: the launch order, or the XCD-contiguous map).
+// Workgroup w reduces chunks [w*kWGC, (w+1)*kWGC).  With FLAME_DEFER_ST the full
+// chunks' output vectors stay in registers and are stored together at the end.
 template <int DT, int CU>
 __device__ __forceinline__ void agg_reduce_body(const flame_segment* __restrict__ segs, int n_segs,
                                                 const uint64_t* __restrict__ clients, int n_clients,
                                                 const float* __restrict__ r32, const double* __restrict__ r64,
                                                 unsigned flags, int64_t n_chunks) {
     using T = typename Tr<DT>::T;
-    const int64_t chunk = (flags & FLAME_AGG_XCD_MAP) ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
-    if (chunk >= n_chunks) return;
-    V16 ov[kVPT];
-    T* op;
-    if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov, op)) store_chunk(op, ov);
+#if FLAME_DEFER_ST
+    V16 ov[kWGC][kVPT];
+    T* op[kWGC];
+    bool full[kWGC];
+#pragma unroll
+    for (int k = 0; k < kWGC; ++k) {
+        const int64_t chunk = static_cast<int64_t>(blockIdx.x) * kWGC + k;
+        full[k] = chunk < n_chunks &&
+                  reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov[k], op[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kWGC; ++k)
+        if (full[k]) store_chunk(op[k], ov[k]);
+#else
+    const int64_t wg = (FLAME_XCD_SWIZZLE || (flags & FLAME_AGG_XCD_MAP)) ? xcd_slot(blockIdx.x, gridDim.x)
+                                                                           : blockIdx.x;
+#pragma unroll 1
+    for (int k = 0; k < kWGC; ++k) {
+        const int64_t chunk = wg * kWGC + k;
+        if (chunk >= n_chunks) break;
+        V16 ov[kVPT];
+        T* op;
+        if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov, op))
+            store_chunk(op, ov);
+    }
+#endif
 }
 
 template <int DT, int CU>
@@ -486,7 +849,6 @@ __device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ s
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const int64_t coff = client_offset<DT>(sg, chunk);
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
-    const bool cur_avg = (sg.flags & FLAME_SEG_CUR_IS_AVG) != 0;   // cur IS the FedAvg result
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     float acc[kVPT][EPT];
     const T* base = reinterpret_cast<const T*>(sg.in) + e0;
@@ -503,20 +865,35 @@ __device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ s
 #pragma unroll
             for (int j = 0; j < EPT; ++j) acc[v][j] = X::ld(b[j]);
         }
+#if FLAME_OPT_PREFETCH
+        T curs[kVPT][EPT], ms[kVPT][EPT], vs[kVPT][EPT];
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            unpack<T, EPT>(ld_v(curp + v * VS), curs[v]);
+            if (!zero_state) {
+                unpack<T, EPT>(ld_v(mp + v * VS), ms[v]);
+                unpack<T, EPT>(ld_v(vp + v * VS), vs[v]);
+            }
+        }
+#endif
         reduce_clients<DT, CU, true>(acc, false, cp, n_clients, r32, nullptr, e0, sg.numel, coff);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             T cur_t[EPT], m_t[EPT], v_t[EPT], avg_o[EPT], m_o[EPT], v_o[EPT], c_o[EPT];
-            if (!cur_avg) unpack<T, EPT>(ld_v(curp + v * VS), cur_t);
+#if FLAME_OPT_PREFETCH
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) { cur_t[j] = curs[v][j]; m_t[j] = ms[v][j]; v_t[j] = vs[v][j]; }
+#else
+            unpack<T, EPT>(ld_v(curp + v * VS), cur_t);
             if (!zero_state) {
                 unpack<T, EPT>(ld_v(mp + v * VS), m_t);
                 unpack<T, EPT>(ld_v(vp + v * VS), v_t);
             }
+#endif
 #pragma unroll
             for (int j = 0; j < EPT; ++j) {
                 float mj = zero_state ? 0.f : X::ld(m_t[j]), vj = zero_state ? 0.f : X::ld(v_t[j]), cj;
-                adapt_elem<DT, VARIANT>(acc[v][j], cur_avg ? acc[v][j] : X::ld(cur_t[j]), mj, vj, cj, b1, omb1, b2,
-                                        omb2, eta, tau);
+                adapt_elem<DT, VARIANT>(acc[v][j], X::ld(cur_t[j]), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
                 avg_o[j] = X::st(acc[v][j]);
                 m_o[j] = X::st(mj);
                 v_o[j] = X::st(vj);
@@ -550,8 +927,7 @@ __device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ s
                 const int64_t o = v * VS + j;
                 if (e0 + o >= sg.numel) continue;
                 float mj = zero_state ? 0.f : X::ld(ld1(mp + o)), vj = zero_state ? 0.f : X::ld(ld1(vp + o)), cj;
-                adapt_elem<DT, VARIANT>(acc[v][j], cur_avg ? acc[v][j] : X::ld(ld1(curp + o)), mj, vj, cj, b1, omb1,
-                                        b2, omb2, eta, tau);
+                adapt_elem<DT, VARIANT>(acc[v][j], X::ld(ld1(curp + o)), mj, vj, cj, b1, omb1, b2, omb2, eta, tau);
                 if (ap) st1(ap + o, X::st(acc[v][j]));
                 st1(mp + o, X::st(mj));
                 st1(vp + o, X::st(vj));
@@ -562,7 +938,7 @@ __device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ s
 }
 
 // G = 1: one chunk per workgroup, stored as computed.  G > 1: G consecutive chunks per
-// workgroup, their outputs held in LDS and stored together at the end (kOptWGC).
+// workgroup, their outputs held in LDS and stored together at the end (FLAME_OPT_WGC).
 template <int DT, int VARIANT, int CU, int G>
 __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ segs, int n_segs,
                                             const uint64_t* __restrict__ clients, int n_clients,
@@ -577,7 +953,7 @@ __device__ __forceinline__ void fedopt_body(const flame_segment* __restrict__ se
     } else {
         using T = typename Tr<DT>::T;
         constexpr int64_t VS = static_cast<int64_t>(kBlock) * Tr<DT>::EPT;
-        static_assert(G * 4 * kVPT * kBlock * sizeof(V16) <= 160 * 1024, "kOptWGC: outputs exceed the LDS");
+        static_assert(G * 4 * kVPT * kBlock * sizeof(V16) <= 160 * 1024, "FLAME_OPT_WGC: outputs exceed the LDS");
         __shared__ V16 held[G * 4 * kVPT * kBlock];
         unsigned pending = 0;
 #pragma unroll 1
@@ -620,16 +996,16 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel(const flame_segment* __r
 
 // The same with the metadata block as a kernel argument, read in place (flame_fedopt_reduce_adapt_argmeta;
 // see agg_reduce_kernel_argmeta).  Word offsets: client table at off_clients, fp32 rates at off_r32.
-template <int DT, int VARIANT, int CU, int G>
+template <int DT, int VARIANT, int CU>
 __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta meta, int n_segs, int n_clients,
                                                                 int off_clients, int off_r32, unsigned flags,
                                                                 float b1, float omb1, float b2, float omb2,
-                                                                float eta, float tau, int64_t n_chunks) {
+                                                                float eta, float tau) {
     (void)sizeof(meta);
     const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    fedopt_body<DT, VARIANT, CU, G>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
+    fedopt_body<DT, VARIANT, CU, 1>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
                                     off_r32 >= 0 ? reinterpret_cast<const float*>(w + off_r32) : nullptr, flags,
-                                    b1, omb1, b2, omb2, eta, tau, n_chunks);
+                                    b1, omb1, b2, omb2, eta, tau, 0);
 }
 
 // ---------------------------------------------------------------- FedBuff scale-add (+delta)
@@ -715,6 +1091,11 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
 // then top_w += top / top_goal (fedbuff.py:122-127).  Every op rounds in the tensor's
 // dtype exactly as the separate launches do, so results are bit-identical to them; the
 // middle aggregates and deltas never touch HBM (deltas are stored only if asked for).
+#if FLAME_HWPE
+#define FLAME_HIER_ATTR __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FLAME_HWPE, 8)))
+#else
+#define FLAME_HIER_ATTR __launch_bounds__(kBlock)
+#endif
 // SYNC (FLAME_HIER_SYNC): the synchronous hierarchy instead (syncfl/middle_aggregator.py:163-229,
 // syncfl/top_aggregator.py:122-176): each middle's FedAvg starts from its weights,
 //   a = w_m + tmp(c_{m,0}, r_{m,0}) + ...;  w_m' = a;  d_m = w_m' - w_m
@@ -771,6 +1152,87 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
         // weights wait in LDS (lane-private slots, no barrier) rather than in registers -- long
         // store bursts at 2 workgroups per CU
         __shared__ V16 held[HL ? HB * kVPT * kBlock : 1];
+#if FLAME_HXP
+        // ONE double-buffered stream of arrival batches across the middles (FLAME_HXP arrivals per
+        // batch, dividing n_clients): the next batch -- the next middle's first one included -- is in
+        // flight while the current batch is combined and while a finished middle's epilogue runs, so
+        // a wave's loads never drain at a middle boundary.  A middle's weights are loaded one middle
+        // ahead (with the previous middle's first batch): loads complete in issue order, so a
+        // weights load issued behind the current batches would hold the epilogue until they land.
+        // Same per-element operation order as the loop below (bitwise).
+        constexpr int XB = FLAME_HXP;
+        if (HL && !SYNC && kVPT == 1 && n_clients % XB == 0 && n_clients >= XB) {
+            const int bpm = n_clients / XB;
+            const int nbt = n_mids * bpm;
+            T xa[XB][kVPT][EPT], xb[XB][kVPT][EPT];
+            V16 wc, wn;
+            wc = ld_v(mid_ptr(0));
+            if (n_mids > 1) wn = ld_v(mid_ptr(1));
+            A acc[kVPT][EPT];
+            auto issue = [&](int b, T (&x)[XB][kVPT][EPT]) {
+                const int m = b / bpm;
+                const int c0 = (b - m * bpm) * XB;
+                const uint64_t* cp = crow + static_cast<int64_t>(m) * n_clients + c0;
+#pragma unroll
+                for (int u = 0; u < XB; ++u) {
+                    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[u]) + coff);
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) unpack<T, EPT>(ld_nt(p + v * VS), x[u][v]);
+                }
+            };
+            auto combine_batch = [&](int b, const T (&x)[XB][kVPT][EPT]) {
+                const int m = b / bpm;
+                const int c0 = (b - m * bpm) * XB;
+                const float* r = mid_rates + static_cast<int64_t>(m) * n_clients + c0;
+#pragma unroll
+                for (int u = 0; u < XB; ++u) {
+                    const float ru = r[u];
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                        for (int j = 0; j < EPT; ++j) {
+                            const A t = X::tmp(x[u][v][j], ru, 0.0);
+                            acc[v][j] = (u == 0 && c0 == 0) ? t : X::add(acc[v][j], t);   // init-first
+                        }
+                }
+                if (c0 + XB < n_clients) return;
+                // middle m complete: scale_add from its weights, the delta into the top, the new
+                // weights into the LDS-held store group (stored as a burst when the group is full)
+                T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+                const float g = mid_goal[m], rt = top_rates[m];
+                const int u = m % HB;
+                T w[EPT], d[EPT];
+                unpack<T, EPT>(wc, w);
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) {
+                    S::op(w[j], X::st(acc[0][j]), g, static_cast<double>(g), &d[j]);
+                    const A t = X::tmp(d[j], rt, 0.0);
+                    top[0][j] = have_top ? X::add(top[0][j], t) : t;
+                }
+                have_top = true;
+                held[u * kBlock + threadIdx.x] = pack<T, EPT>(w);
+                if (dp) st_v(dp, pack<T, EPT>(d));
+                wc = wn;                           // loaded a whole middle ago
+                if (m + 2 < n_mids) wn = ld_v(mid_ptr(m + 2));
+                if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {
+                    const int mg = m - u;
+#pragma unroll 1
+                    for (int q = 0; q <= u; ++q) st_pol<FLAME_HST>(mid_ptr(mg + q), held[q * kBlock + threadIdx.x]);
+                }
+            };
+            issue(0, xa);
+            int b = 0;
+#pragma unroll 1
+            while (true) {
+                if (b + 1 < nbt) issue(b + 1, xb);
+                combine_batch(b, xa);
+                if (++b >= nbt) break;
+                if (b + 1 < nbt) issue(b + 1, xa);
+                combine_batch(b, xb);
+                if (++b >= nbt) break;
+            }
+        } else
+#endif
 #pragma unroll 1
         for (int m0 = 0; m0 < n_mids; m0 += HB) {
             V16 pend[HL ? 1 : HB][kVPT];
@@ -780,6 +1242,11 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
             const int m = m0 + u;
             if (HB > 1 && m >= n_mids) break;
             T* wp = mid_ptr(m);
+#if FLAME_HPF
+            V16 wv[kVPT];
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) wv[v] = ld_v(wp + v * VS);
+#endif
             A acc[kVPT][EPT];
             T wo[SYNC ? kVPT : 1][EPT];
             if constexpr (SYNC) {     // FedAvg starts from the middle's weights (deepcopy(self.weights))
@@ -806,7 +1273,14 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                         top[v][j] = X::add(top[v][j], X::tmp(d[j], rt, 0.0));
                     }
                 } else {
+#if FLAME_HPF
+                    unpack<T, EPT>(wv[v], w);
+#elif FLAME_HDIAG == 2
+#pragma unroll
+                    for (int j = 0; j < EPT; ++j) w[j] = T(0);
+#else
                     unpack<T, EPT>(ld_v(wp + v * VS), w);
+#endif
 #pragma unroll
                     for (int j = 0; j < EPT; ++j) {
                         S::op(w[j], X::st(acc[v][j]), g, static_cast<double>(g), &d[j]);
@@ -830,7 +1304,10 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                         V16 pv;
                         if constexpr (HL) pv = held[(u * kVPT + v) * kBlock + threadIdx.x];
                         else pv = pend[u][v];
-                        st_v(wp + v * VS, pv);
+#if FLAME_HDIAG
+                        if (__builtin_expect(pv.w[0] == 0x12345u && pv.w[1] == 0x54321u, 0))
+#endif
+                        st_pol<FLAME_HST>(wp + v * VS, pv);
                     }
                 }
             }
@@ -914,7 +1391,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
 }
 
 template <int DT, int CU, bool SYNC, int HB, bool HL>
-__global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
+__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
                                                     int n_mids, int n_clients, const uint64_t* __restrict__ mid_w,
                                                     const uint64_t* __restrict__ mid_delta,
                                                     const uint64_t* __restrict__ clients,
@@ -929,7 +1406,7 @@ __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel(const flame_hier_s
 // The same with the metadata block in the kernel arguments (small launches, e.g. a single
 // FedBuff aggregator's fused scale_add); word offsets into the block, -1 = no delta table.
 template <int DT, int CU, bool SYNC>
-__global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel_argmeta(const ArgMeta meta, int n_segs, int n_mids, int n_clients,
+__global__ FLAME_HIER_ATTR void hier_fedbuff_kernel_argmeta(const ArgMeta meta, int n_segs, int n_mids, int n_clients,
                                                             int o_mid_w, int o_mid_delta, int o_clients,
                                                             int o_mid_rates, int o_mid_goal, int o_top_rates,
                                                             float top_goal, unsigned flags) {
@@ -954,7 +1431,7 @@ __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel_argmeta(const ArgM
 // then out = avg, cld = avg + mean.  Steps [0, n_phase1) run before [n_phase1, n_steps);
 // batched loads never cross that boundary, so a phase-2 step may re-read what a phase-1
 // step stored (history order != arrival order).
-template <int DT, int CU, bool VEC>
+template <int DT, int CU, bool VEC, int G>
 __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const uint64_t* __restrict__ row,
                                              const uint32_t* __restrict__ sflags, int n_steps, int n_phase1,
                                              float ra32, float rm32, double ra64, double rm64, int64_t e0,
@@ -977,17 +1454,33 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
             }
         }
     };
-    auto store = [&](void* base, int64_t off, const T (&x)[kVPT][EPT]) {
+    auto store = [&](void* base, int64_t off, const T (&x)[kVPT][EPT], auto pol) {
+        constexpr int POL = decltype(pol)::value;
         T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
             if constexpr (VEC) {
-                st_v(p + v * VS, pack<T, EPT>(x[v]));
+                st_pol<POL>(p + v * VS, pack<T, EPT>(x[v]));
             } else {
 #pragma unroll
                 for (int j = 0; j < EPT; ++j)
                     if (e0 + v * VS + j < sg.numel) st1(p + v * VS + j, x[v][j]);
             }
+        }
+    };
+    using out_pol = std::integral_constant<int, FLAME_ST_NT>;
+    using hist_pol = std::integral_constant<int, FLAME_DYN_ST>;
+    // G > 0: updated histories wait in LDS (lane-private slots) and go out G steps at a time
+    constexpr bool HL = VEC && G > 0;
+    static_assert(!HL || G % CU == 0, "FLAME_DYN_LDS must be a multiple of FLAME_DYN_CU");
+    __shared__ V16 held[HL ? G * kVPT * kBlock : 1];
+    auto flush = [&](int q0, int q1) {
+#pragma unroll 1
+        for (int q = q0; q < q1; ++q) {
+            if (!(sflags[q] & FLAME_DYN_HOUT)) continue;
+            T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(row[static_cast<int64_t>(q) * 3 + 2]) + hoff);
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) st_pol<FLAME_DYN_ST>(p + v * VS, held[((q - q0) * kVPT + v) * kBlock + threadIdx.x]);
         }
     };
     A avg[kVPT][EPT], mean[kVPT][EPT];
@@ -1002,6 +1495,7 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
 #pragma unroll 1
     for (int phase = 0; phase < 2; ++phase) {
         const int end = phase ? n_steps : n_phase1;
+        int kg = phase ? n_phase1 : 0;       // first step whose history is still held (HL)
 #pragma unroll 1
         for (int k = phase ? n_phase1 : 0; k < end; k += CU) {
             const int nb = (end - k < CU) ? end - k : CU;
@@ -1036,13 +1530,26 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
 #pragma unroll
                             for (int j = 0; j < EPT; ++j) h[u][v][j] = w[u][v][j];
                     }
-                    store(reinterpret_cast<void*>(row[static_cast<int64_t>(k + u) * 3 + 2]), hoff, h[u]);
+                    if constexpr (HL) {
+#pragma unroll
+                        for (int v = 0; v < kVPT; ++v)
+                            held[((k + u - kg) * kVPT + v) * kBlock + threadIdx.x] = pack<T, EPT>(h[u][v]);
+                    } else {
+                        store(reinterpret_cast<void*>(row[static_cast<int64_t>(k + u) * 3 + 2]), hoff, h[u], hist_pol{});
+                    }
                 }
                 if (f & FLAME_DYN_MEAN) {
 #pragma unroll
                     for (int v = 0; v < kVPT; ++v)
 #pragma unroll
                         for (int j = 0; j < EPT; ++j) mean[v][j] = X::add(mean[v][j], X::tmp(h[u][v][j], rm32, rm64));
+                }
+            }
+            if constexpr (HL) {     // a full group, or the phase's last steps: store the held histories
+                const int k1 = k + nb;
+                if (k1 - kg >= G || k1 >= end) {
+                    flush(kg, k1);
+                    kg = k1;
                 }
             }
         }
@@ -1052,8 +1559,8 @@ __device__ __forceinline__ void feddyn_chunk(const flame_dyn_segment& sg, const 
     for (int v = 0; v < kVPT; ++v)
 #pragma unroll
         for (int j = 0; j < EPT; ++j) { o[v][j] = X::st(avg[v][j]); c[v][j] = X::st(X::add(avg[v][j], mean[v][j])); }
-    store(sg.out, ooff, o);
-    store(sg.cld, ooff, c);
+    store(sg.out, ooff, o, out_pol{});
+    store(sg.cld, ooff, c, out_pol{});
 }
 
 template <int DT, int CU>
@@ -1065,9 +1572,7 @@ __global__ __launch_bounds__(kBlock) void feddyn_kernel(const flame_dyn_segment*
     using X = Tr<DT>;
     constexpr int EPT = X::EPT;
     constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
-    // XCD-contiguous chunk map: 512 x 12M fp32 -0.7 % (cache order) / -1.4 % (other order)
-    // (profiles/r02_feddyn_xcd_sweep.log)
-    const int64_t chunk = xcd_slot(blockIdx.x, gridDim.x);
+    const int64_t chunk = FLAME_DYN_XCD ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_dyn_segment sg = segs[s];
     const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
@@ -1080,9 +1585,10 @@ __global__ __launch_bounds__(kBlock) void feddyn_kernel(const flame_dyn_segment*
     const uint64_t* row = steps + static_cast<int64_t>(s) * n_steps * 3;
     const bool vec = (e0 + (kVPT - 1) * VS + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     if (vec)
-        feddyn_chunk<DT, CU, true>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+        feddyn_chunk<DT, CU, true, FLAME_DYN_LDS>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff,
+                                                  hoff);
     else
-        feddyn_chunk<DT, 1, false>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
+        feddyn_chunk<DT, 1, false, 0>(sg, row, sflags, n_steps, n_phase1, ra32, rm32, ra64, rm64, e0, coff, hoff);
 }
 
 // ---------------------------------------------------------------- synthetic generator
@@ -1112,9 +1618,13 @@ __global__ __launch_bounds__(kEwBlock) void synth_kernel(void* out, int64_t nume
 // workgroup copies kSlabTPW tiles, every lane 16 B of each (all its loads issued before its
 // stores); the entry table rides in the kernel arguments, so an insert is ONE launch and no
 // H2D of metadata.
-// 2 tiles per workgroup (1-8 within noise) and plain stores (measured best of the store policies,
-// profiles/r03b_slab_sweep.log)
-constexpr int kSlabTPW = 2;
+#ifndef FLAME_SLAB_TPW
+#define FLAME_SLAB_TPW 2   // slab insert: 4 KiB tiles per workgroup (1-8 within noise, profiles/r03b_slab_sweep.log)
+#endif
+#ifndef FLAME_SLAB_ST
+#define FLAME_SLAB_ST 0    // slab insert: store policy (encoding of FLAME_ST_NT; plain stores measured best)
+#endif
+constexpr int kSlabTPW = FLAME_SLAB_TPW;
 struct SlabEntry { const uint8_t* src; uint8_t* dst; int64_t nbytes; int64_t stride; int64_t tile_begin; };
 constexpr int kSlabMaxEntries = static_cast<int>(sizeof(ArgMeta) / sizeof(SlabEntry));
 static_assert(FLAME_TILE_BYTES == kBlock * 16, "a slab tile is one 16-byte vector per lane");
@@ -1173,69 +1683,17 @@ __global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, 
     }
 #pragma unroll
     for (int j = 0; j < kSlabTPW; ++j)
-        if (kind[j] == 1) st_plain(dp[j], v[j]);
+        if (kind[j] == 1) st_pol<FLAME_SLAB_ST>(dp[j], v[j]);
 }
 
-// ---------------------------------------------------------------- launch-branch counters
-// Every host-side launch branch of the C ABI has an index; a successful launch counts it, so
-// tests can assert which instantiation a call took and that every branch is reached by an
-// oracle test (tests/test_gpu_zz_launch_branches.py).  dt = FLAME_F32 .. FLAME_I32.
-enum : int {
-    BR_AGG = 0,           // + dt (6): flame_agg_reduce, full residency
-    BR_AGG_LO = 6,        // + dt (f32, bf16, f16): flame_agg_reduce, 2 workgroups per CU
-    BR_AGG_ARG = 9,       // + dt (6): flame_agg_reduce_argmeta
-    BR_OPT = 15,          // + dt * 3 + variant (f32, bf16, f16): flame_fedopt_reduce_adapt, one chunk per workgroup
-    BR_OPT_MULTI = 24,    // + variant: fp32, kOptWGC chunks per workgroup
-    BR_OPT_ARG = 27,      // + dt * 3 + variant: flame_fedopt_reduce_adapt_argmeta
-    BR_SA = 36,           // + dt (f32, bf16, f16, f64): flame_fedbuff_scale_add
-    BR_HIER_REG = 40,     // + dt * 2 + sync: flame_hier_fedbuff, register store groups
-    BR_HIER_LDS = 46,     // + dt * 2 + sync: LDS store groups (>= kHLdsMinMids middles)
-    BR_HIER_LO = 52,      // + dt: one middle over a long launch, low residency (FedBuff only)
-    BR_HIER_ARG = 55,     // + dt * 2 + sync: flame_hier_fedbuff_argmeta
-    BR_DYN = 61,          // + dt (f32, bf16, f16, f64): flame_feddyn_round
-    BR_AGG_ARG_LO = 65,   // + dt (f32, bf16, f16): flame_agg_reduce_argmeta, 2 workgroups per CU
-    BR_HIER_ARG_LO = 68,  // + dt: flame_hier_fedbuff_argmeta, one middle over a long launch
-    BR_OPT_ARG_MULTI = 71,  // + variant: flame_fedopt_reduce_adapt_argmeta, fp32, kOptWGC chunks per workgroup
-    BR_COUNT = 74
-};
-std::atomic<long long> g_launches[BR_COUNT];
-
-const char* branch_name(int i) {
-    static const char* const dts[6] = {"f32", "bf16", "f16", "f64", "i64", "i32"};
-    static const char* const var[3] = {"fedadam", "fedyogi", "fedadagrad"};
-    static char names[BR_COUNT][64];
-    static const bool once = [] {
-        for (int b = 0; b < BR_COUNT; ++b) {
-            char* n = names[b];
-            const size_t z = sizeof(names[b]);
-            if (b < BR_AGG_LO) snprintf(n, z, "flame_agg_reduce/%s", dts[b - BR_AGG]);
-            else if (b < BR_AGG_ARG) snprintf(n, z, "flame_agg_reduce/lo/%s", dts[b - BR_AGG_LO]);
-            else if (b < BR_OPT) snprintf(n, z, "flame_agg_reduce_argmeta/%s", dts[b - BR_AGG_ARG]);
-            else if (b < BR_OPT_MULTI) snprintf(n, z, "flame_fedopt_reduce_adapt/%s/%s", dts[(b - BR_OPT) / 3], var[(b - BR_OPT) % 3]);
-            else if (b < BR_OPT_ARG) snprintf(n, z, "flame_fedopt_reduce_adapt/multi/f32/%s", var[b - BR_OPT_MULTI]);
-            else if (b < BR_SA) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/%s/%s", dts[(b - BR_OPT_ARG) / 3], var[(b - BR_OPT_ARG) % 3]);
-            else if (b < BR_HIER_REG) snprintf(n, z, "flame_fedbuff_scale_add/%s", dts[b - BR_SA]);
-            else if (b < BR_HIER_LDS) snprintf(n, z, "flame_hier_fedbuff/reg/%s/%s", dts[(b - BR_HIER_REG) / 2], (b - BR_HIER_REG) % 2 ? "sync" : "fedbuff");
-            else if (b < BR_HIER_LO) snprintf(n, z, "flame_hier_fedbuff/lds/%s/%s", dts[(b - BR_HIER_LDS) / 2], (b - BR_HIER_LDS) % 2 ? "sync" : "fedbuff");
-            else if (b < BR_HIER_ARG) snprintf(n, z, "flame_hier_fedbuff/lo/%s/fedbuff", dts[b - BR_HIER_LO]);
-            else if (b < BR_DYN) snprintf(n, z, "flame_hier_fedbuff_argmeta/%s/%s", dts[(b - BR_HIER_ARG) / 2], (b - BR_HIER_ARG) % 2 ? "sync" : "fedbuff");
-            else if (b < BR_AGG_ARG_LO) snprintf(n, z, "flame_feddyn_round/%s", dts[b - BR_DYN]);
-            else if (b < BR_HIER_ARG_LO) snprintf(n, z, "flame_agg_reduce_argmeta/lo/%s", dts[b - BR_AGG_ARG_LO]);
-            else if (b < BR_OPT_ARG_MULTI) snprintf(n, z, "flame_hier_fedbuff_argmeta/lo/%s/fedbuff", dts[b - BR_HIER_ARG_LO]);
-            else snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
-        }
-        return true;
-    }();
-    (void)once;
-    return (i >= 0 && i < BR_COUNT) ? names[i] : nullptr;
-}
-
-// check_launch + count the branch on success
-int launched(int br, const char* what) {
-    const int rc = check_launch(what);
-    if (rc == FLAME_OK) g_launches[br].fetch_add(1, std::memory_order_relaxed);
-    return rc;
-}
+constexpr int kClientUnroll = FLAME_CU;
+constexpr int kClientUnroll16 = FLAME_CU16;
+constexpr int kHierUnroll16 = FLAME_HCU16;
+constexpr int kOptWGC = FLAME_OPT_WGC;
+constexpr int kOptUnroll = FLAME_OPT_CU;
+static_assert(kOptWGC >= 1 && kOptWGC <= 32, "FLAME_OPT_WGC: 1..32 chunks per workgroup");
+constexpr int kHierLdsUnroll16 = FLAME_HLDS_CU16;
+constexpr int kHBL = FLAME_HLDS_BATCH;
 
 int validate(const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int32_t n_clients, const void* clients) {
     if (!segs || n_segs <= 0) return set_err(FLAME_EINVAL, "segment table is NULL or n_segs <= 0");
@@ -1288,32 +1746,49 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
         return set_err(FLAME_EINVAL, "rate array is NULL");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const dim3 grid(static_cast<unsigned>((n_chunks + kWGC - 1) / kWGC)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-#define FLAME_AGG_LAUNCH(DT, CUV, LDS, BR)                                                                      \
-    hipLaunchKernelGGL((agg_reduce_kernel<DT, CUV>), grid, block, LDS, st, segs, n_segs, cl, n_clients, rates32, \
-                       rates64, flags, n_chunks);                                                              \
-    return launched(BR, "flame_agg_reduce");
-    // long-lived workgroups over many chunks: two per CU, fewer loads in flight per lane
-    if (n_clients >= kLoMinClients && n_chunks >= kLoMinChunks) {
+#if FLAME_LO_CU > 0
+    // long-lived workgroups over many chunks: two per CU, FLAME_LO_CU loads in flight per lane
+    if (n_clients >= FLAME_LO_MIN_CLIENTS && n_chunks >= FLAME_LO_MIN_CHUNKS && kWGC == 1 && FLAME_OCC_LDS == 0) {
         switch (dtype) {
-        case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kLoUnroll, kLoLds, BR_AGG_LO + FLAME_F32)
-        case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kLoUnroll16, kLoLds, BR_AGG_LO + FLAME_BF16)
-        case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kLoUnroll16, kLoLds, BR_AGG_LO + FLAME_F16)
-        default: break;      // f64 / integers: the general launch below
+        case FLAME_F32:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, FLAME_LO_CU>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        case FLAME_BF16:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, FLAME_LO_CU16>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        case FLAME_F16:
+            hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, FLAME_LO_CU16>), grid, block, FLAME_LO_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+            return check_launch("flame_agg_reduce");
+        default:
+            break;      // f64 / integers: the general launch below
         }
     }
+#endif
     switch (dtype) {
-    case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kClientUnroll, 0, BR_AGG + FLAME_F32)
-    case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kClientUnroll16, 0, BR_AGG + FLAME_BF16)
-    case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kClientUnroll16, 0, BR_AGG + FLAME_F16)
-    case FLAME_F64: FLAME_AGG_LAUNCH(FLAME_F64, kClientUnroll, 0, BR_AGG + FLAME_F64)
-    case FLAME_I64: FLAME_AGG_LAUNCH(FLAME_I64, 4, 0, BR_AGG + FLAME_I64)
-    case FLAME_I32: FLAME_AGG_LAUNCH(FLAME_I32, 4, 0, BR_AGG + FLAME_I32)
+    case FLAME_F32:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F32, kClientUnroll>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
+    case FLAME_BF16:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_BF16, kClientUnroll16>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
+    case FLAME_F16:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F16, kClientUnroll16>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
+    case FLAME_F64:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_F64, kClientUnroll>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
+    case FLAME_I64:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I64, 4>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
+    case FLAME_I32:
+        hipLaunchKernelGGL((agg_reduce_kernel<FLAME_I32, 4>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);
+        break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_agg_reduce: unsupported dtype %d", dtype);
     }
-#undef FLAME_AGG_LAUNCH
+    return check_launch("flame_agg_reduce");
 }
 
 int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void* host_meta, int64_t meta_bytes, int32_t n_segs,
@@ -1342,23 +1817,10 @@ int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void* host_meta, i
     const int o32 = (!f64 && n_clients > 0) ? static_cast<int>(off_r32 / 8) : -1;
     const int o64 = (f64 && n_clients > 0) ? static_cast<int>(off_r64 / 8) : -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const dim3 grid(static_cast<unsigned>((n_chunks + kWGC - 1) / kWGC)), block(kBlock);
 #define FLAME_ARGMETA_LAUNCH(DT, CUV) \
-    hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV>), grid, block, 0, st, m, n_segs, n_clients, \
+    hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV>), grid, block, FLAME_OCC_LDS, st, m, n_segs, n_clients, \
                        oc, o32, o64, flags, n_chunks)
-    // a long launch with few segments (its table fits the kernel arguments): the same low-residency
-    // instantiation as flame_agg_reduce's
-    if (n_clients >= kLoMinClients && n_chunks >= kLoMinChunks &&
-        (dtype == FLAME_F32 || dtype == FLAME_BF16 || dtype == FLAME_F16)) {
-#define FLAME_ARGMETA_LO(DT, CUV)                                                                              \
-        hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV>), grid, block, kLoLds, st, m, n_segs, n_clients, \
-                           oc, o32, o64, flags, n_chunks)
-        if (dtype == FLAME_F32) FLAME_ARGMETA_LO(FLAME_F32, kLoUnroll);
-        else if (dtype == FLAME_BF16) FLAME_ARGMETA_LO(FLAME_BF16, kLoUnroll16);
-        else FLAME_ARGMETA_LO(FLAME_F16, kLoUnroll16);
-#undef FLAME_ARGMETA_LO
-        return launched(BR_AGG_ARG_LO + dtype, "flame_agg_reduce_argmeta");
-    }
     switch (dtype) {
     case FLAME_F32: FLAME_ARGMETA_LAUNCH(FLAME_F32, kClientUnroll); break;
     case FLAME_BF16: FLAME_ARGMETA_LAUNCH(FLAME_BF16, kClientUnroll16); break;
@@ -1370,7 +1832,7 @@ int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void* host_meta, i
         return set_err(FLAME_ENOTSUP, "flame_agg_reduce_argmeta: unsupported dtype %d", dtype);
     }
 #undef FLAME_ARGMETA_LAUNCH
-    return launched(BR_AGG_ARG + dtype, "flame_agg_reduce_argmeta");
+    return check_launch("flame_agg_reduce_argmeta");
 }
 
 int64_t flame_agg_argmeta_max_bytes(void) { return static_cast<int64_t>(sizeof(ArgMeta)); }
@@ -1387,9 +1849,9 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
     if (flags & ~(FLAME_OPT_STATE_ZERO | FLAME_OPT_XCD_MAP))
         return set_err(FLAME_EINVAL, "flame_fedopt_reduce_adapt: unknown flags 0x%x", flags);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // kOptWGC chunks per workgroup (outputs held in LDS) for fp32 launches big enough to fill
+    // FLAME_OPT_WGC chunks per workgroup (outputs held in LDS) for fp32 launches big enough to fill
     // the GPU several times over; one chunk per workgroup otherwise
-    const bool multi = dtype == FLAME_F32 && n_chunks >= 8ll * 256 * kOptWGC;
+    const bool multi = kOptWGC > 1 && n_chunks >= 8ll * 256 * kOptWGC;
     const dim3 grid(static_cast<unsigned>(multi ? (n_chunks + kOptWGC - 1) / kOptWGC : n_chunks)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
 #define FLAME_OPT_LAUNCH1(DT, CUV, G)                                                                          \
@@ -1418,7 +1880,7 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt: dtype %d not supported (f32, bf16, f16)", dtype);
     }
 #undef FLAME_OPT_LAUNCH1
-    return launched(multi ? BR_OPT_MULTI + variant : BR_OPT + dtype * 3 + variant, "flame_fedopt_reduce_adapt");
+    return check_launch("flame_fedopt_reduce_adapt");
 }
 
 int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, const void* host_meta,
@@ -1445,37 +1907,31 @@ int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, co
     const int oc = static_cast<int>(off_clients / 8);
     const int o32 = n_clients > 0 ? static_cast<int>(off_r32 / 8) : -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // the instantiation flame_fedopt_reduce_adapt picks for the same launch
-    const bool multi = dtype == FLAME_F32 && n_chunks >= 8ll * 256 * kOptWGC;
-    const dim3 grid(static_cast<unsigned>(multi ? (n_chunks + kOptWGC - 1) / kOptWGC : n_chunks)), block(kBlock);
-#define FLAME_OPT_ARGMETA_LAUNCH(DT, CUV, G)                                                                     \
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+#define FLAME_OPT_ARGMETA_LAUNCH(DT, CUV)                                                                        \
     switch (variant) {                                                                                           \
     case FLAME_FEDADAM:                                                                                          \
-        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAM, CUV, G>), grid, block, 0, st, m, n_segs,     \
-                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                   \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAM, CUV>), grid, block, 0, st, m, n_segs,        \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
         break;                                                                                                   \
     case FLAME_FEDYOGI:                                                                                          \
-        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDYOGI, CUV, G>), grid, block, 0, st, m, n_segs,     \
-                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                   \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDYOGI, CUV>), grid, block, 0, st, m, n_segs,        \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
         break;                                                                                                   \
     default:                                                                                                     \
-        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAGRAD, CUV, G>), grid, block, 0, st, m, n_segs,  \
-                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau, n_chunks);                   \
+        hipLaunchKernelGGL((fedopt_kernel_argmeta<DT, FLAME_FEDADAGRAD, CUV>), grid, block, 0, st, m, n_segs,     \
+                           n_clients, oc, o32, flags, b1, omb1, b2, omb2, eta, tau);                             \
         break;                                                                                                   \
     }
     switch (dtype) {
-    case FLAME_F32:
-        if (multi) { FLAME_OPT_ARGMETA_LAUNCH(FLAME_F32, kOptUnroll, kOptWGC) }
-        else { FLAME_OPT_ARGMETA_LAUNCH(FLAME_F32, kClientUnroll, 1) }
-        break;
-    case FLAME_BF16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_BF16, kClientUnroll16, 1) break;
-    case FLAME_F16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_F16, kClientUnroll16, 1) break;
+    case FLAME_F32: FLAME_OPT_ARGMETA_LAUNCH(FLAME_F32, kClientUnroll) break;
+    case FLAME_BF16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_BF16, kClientUnroll16) break;
+    case FLAME_F16: FLAME_OPT_ARGMETA_LAUNCH(FLAME_F16, kClientUnroll16) break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_fedopt_reduce_adapt_argmeta: dtype %d not supported (f32, bf16, f16)", dtype);
     }
 #undef FLAME_OPT_ARGMETA_LAUNCH
-    if (multi) return launched(BR_OPT_ARG_MULTI + variant, "flame_fedopt_reduce_adapt_argmeta");
-    return launched(BR_OPT_ARG + dtype * 3 + variant, "flame_fedopt_reduce_adapt_argmeta");
+    return check_launch("flame_fedopt_reduce_adapt_argmeta");
 }
 
 int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs, int64_t n_chunks, int64_t goal,
@@ -1495,7 +1951,7 @@ int flame_fedbuff_scale_add(int dtype, const flame_segment* segs, int32_t n_segs
     default:
         return set_err(FLAME_ENOTSUP, "flame_fedbuff_scale_add: dtype %d not supported (integer tensors raise in the reference)", dtype);
     }
-    return launched(BR_SA + dtype, "flame_fedbuff_scale_add");
+    return check_launch("flame_fedbuff_scale_add");
 }
 
 int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs, int32_t n_segs, int64_t n_chunks,
@@ -1518,41 +1974,39 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
     auto w = reinterpret_cast<const uint64_t*>(mid_w);
     auto d = reinterpret_cast<const uint64_t*>(mid_delta);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
+#define FLAME_HIER_LAUNCH1(DT, CUV, HB, HL)                                                                    \
+    if (sync)                                                                                                  \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, true, HB, HL>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, \
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);      \
+    else                                                                                                       \
+        hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, false, HB, HL>), grid, block, FLAME_OCC_LDS, st, segs, n_segs, \
+                           n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+    // many middles (config 5: 64 per GPU): LDS-held store groups; a few (a single FedBuff's fused
+    // scale_add, small hierarchies): register groups, no LDS, full occupancy
+    // one middle over a long launch (a FedBuff aggregator's fused scale_add / a middle's scale_add +
+    // delta over >= 64 queued arrivals): fewer workgroups per CU, fewer loads in flight -- fp32 2 per
+    // CU unroll 3, 16-bit 3 per CU unroll 3 (64 x 25M: 1.058 -> 0.989 ms fp32, 0.533 -> 0.509 ms bf16;
+    // tools/fedbuff_sweep.py, profiles/r03zv_fedbuff_*.log); FLAME_HLO=0 turns it off
+#define FLAME_HIER_LO(DT, LDS)                                                                                   \
+    hipLaunchKernelGGL((hier_fedbuff_kernel<DT, 3, false, kHB, false>), grid, block, LDS, st, segs, n_segs,     \
+                       n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);
+#define FLAME_HIER_LAUNCH(DT, CUV, CUL)                                                                        \
+    if (FLAME_HLDS && n_mids >= FLAME_HLDS_MIN_MIDS) { FLAME_HIER_LAUNCH1(DT, CUL, kHBL, true) }             \
+    else if (FLAME_HLO && !sync && n_mids == 1 && n_clients >= 64 && n_chunks >= 4096 && FLAME_OCC_LDS == 0) {  \
+        FLAME_HIER_LO(DT, (DT == FLAME_F32 ? 65536 : 53248))                                                    \
+    } else { FLAME_HIER_LAUNCH1(DT, CUV, kHB, false) }
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
-    // many middles (config 5: 64 per GPU): LDS-held store groups.  One middle over a long launch
-    // (a FedBuff aggregator's fused scale_add / a middle's scale_add + delta over >= 64 queued
-    // arrivals): fewer workgroups per CU, fewer loads in flight -- fp32 2 per CU, 16-bit 3 per CU,
-    // unroll 3 (64 x 25M: 1.058 -> 0.989 ms fp32, 0.533 -> 0.509 ms bf16; tools/fedbuff_sweep.py,
-    // profiles/r03zv_fedbuff_*.log).  Otherwise (small hierarchies): register groups, full residency.
-    const bool lds = n_mids >= kHLdsMinMids;
-    const bool lo = !lds && !sync && n_mids == 1 && n_clients >= kHLoMinClients && n_chunks >= kHLoMinChunks;
-#define FLAME_HIER_GO(DT, CUV, SY, HB, HL, LDSB)                                                              \
-    hipLaunchKernelGGL((hier_fedbuff_kernel<DT, CUV, SY, HB, HL>), grid, block, LDSB, st, segs, n_segs, n_mids, \
-                       n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags)
-#define FLAME_HIER_LAUNCH(DT, CUV, CUL, LOLDS)                                                                  \
-    if (lds) {                                                                                                 \
-        if (sync) FLAME_HIER_GO(DT, CUL, true, kHBL, true, 0);                                                 \
-        else FLAME_HIER_GO(DT, CUL, false, kHBL, true, 0);                                                     \
-        br = BR_HIER_LDS + DT * 2 + sync;                                                                      \
-    } else if (lo) {                                                                                           \
-        FLAME_HIER_GO(DT, kHLoUnroll, false, kHB, false, LOLDS);                                               \
-        br = BR_HIER_LO + DT;                                                                                  \
-    } else {                                                                                                   \
-        if (sync) FLAME_HIER_GO(DT, CUV, true, kHB, false, 0);                                                 \
-        else FLAME_HIER_GO(DT, CUV, false, kHB, false, 0);                                                     \
-        br = BR_HIER_REG + DT * 2 + sync;                                                                      \
-    }
-    int br = 0;
     switch (dtype) {
-    case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll, kClientUnroll, kHLoLdsF32) break;
-    case FLAME_BF16: FLAME_HIER_LAUNCH(FLAME_BF16, kHierUnroll16, kHierLdsUnroll16, kHLoLds16) break;
-    case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16, kHierLdsUnroll16, kHLoLds16) break;
-#undef FLAME_HIER_GO
+    case FLAME_F32: FLAME_HIER_LAUNCH(FLAME_F32, kClientUnroll, kClientUnroll) break;
+    case FLAME_BF16: FLAME_HIER_LAUNCH(FLAME_BF16, kHierUnroll16, kHierLdsUnroll16) break;
+    case FLAME_F16: FLAME_HIER_LAUNCH(FLAME_F16, kHierUnroll16, kHierLdsUnroll16) break;
+#undef FLAME_HIER_LAUNCH1
 #undef FLAME_HIER_LAUNCH
+#undef FLAME_HIER_LO
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff: dtype %d not supported (f32, bf16, f16)", dtype);
     }
-    return launched(br, "flame_hier_fedbuff");
+    return check_launch("flame_hier_fedbuff");
 }
 
 int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta, int64_t meta_bytes, int32_t n_segs,
@@ -1584,25 +2038,12 @@ int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta,
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
-    // one middle over a long launch (a FedBuff aggregator's fused scale_add of >= 64 arrivals into
-    // a model of a few keys): the low-residency instantiation, as in flame_hier_fedbuff
-    if (!sync && n_mids == 1 && n_clients >= kHLoMinClients && n_chunks >= kHLoMinChunks &&
-        (dtype == FLAME_F32 || dtype == FLAME_BF16 || dtype == FLAME_F16)) {
-#define FLAME_HIER_ARG_LO(DT, LDSB)                                                                              \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, kHLoUnroll, false>), grid, block, LDSB, st, m, n_segs, \
-                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags)
-        if (dtype == FLAME_F32) FLAME_HIER_ARG_LO(FLAME_F32, kHLoLdsF32);
-        else if (dtype == FLAME_BF16) FLAME_HIER_ARG_LO(FLAME_BF16, kHLoLds16);
-        else FLAME_HIER_ARG_LO(FLAME_F16, kHLoLds16);
-#undef FLAME_HIER_ARG_LO
-        return launched(BR_HIER_ARG_LO + dtype, "flame_hier_fedbuff_argmeta");
-    }
 #define FLAME_HIER_ARG_LAUNCH(DT, CUV)                                                                          \
     if (sync)                                                                                                  \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, true>), grid, block, 0, st, m, n_segs,             \
+        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, true>), grid, block, FLAME_OCC_LDS, st, m, n_segs, \
                            n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);                      \
     else                                                                                                       \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, false>), grid, block, 0, st, m, n_segs,            \
+        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, false>), grid, block, FLAME_OCC_LDS, st, m, n_segs, \
                            n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);
     switch (dtype) {
     case FLAME_F32: FLAME_HIER_ARG_LAUNCH(FLAME_F32, kClientUnroll) break;
@@ -1612,16 +2053,15 @@ int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta,
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff_argmeta: dtype %d not supported (f32, bf16, f16)", dtype);
     }
-    return launched(BR_HIER_ARG + dtype * 2 + sync, "flame_hier_fedbuff_argmeta");
+    return check_launch("flame_hier_fedbuff_argmeta");
 }
 
 int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
     if (n_mids < 1) return -set_err(FLAME_EINVAL, "flame_hier_resident_per_cu: n_mids < 1");
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
-    const bool lds = n_mids >= kHLdsMinMids;
+    const bool lds = FLAME_HLDS && n_mids >= FLAME_HLDS_MIN_MIDS;
     const void* f = nullptr;
-    // the instantiation flame_hier_fedbuff picks for these arguments (the one-middle low-residency
-    // launch aside, which depends on the launch size)
+    // the instantiation FLAME_HIER_LAUNCH in flame_hier_fedbuff picks for these arguments
 #define FLAME_HIER_PICK(DT, CUV, CUL)                                                                          \
     if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)          \
                       : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, false, kHBL, true>);        \
@@ -1636,7 +2076,7 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
         return -set_err(FLAME_ENOTSUP, "flame_hier_resident_per_cu: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     int blocks = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, kBlock, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, kBlock, FLAME_OCC_LDS);
     if (e != hipSuccess) return -set_err(FLAME_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
     return blocks < 1 ? 1 : blocks;
 }
@@ -1657,25 +2097,25 @@ int flame_feddyn_round(int dtype, const flame_dyn_segment* segs, int32_t n_segs,
     const float ra32 = static_cast<float>(rate_avg), rm32 = static_cast<float>(rate_mean);
     switch (dtype) {
     case FLAME_F32:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F32, kDynUnroll>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F32, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_BF16:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_BF16, kDynUnroll>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_BF16, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_F16:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F16, kDynUnroll>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F16, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     case FLAME_F64:
-        hipLaunchKernelGGL((feddyn_kernel<FLAME_F64, kDynUnroll>), grid, block, 0, st, segs, n_segs, sp, step_flags, n_steps,
+        hipLaunchKernelGGL((feddyn_kernel<FLAME_F64, FLAME_DYN_CU>), grid, block, FLAME_DYN_OCC_LDS, st, segs, n_segs, sp, step_flags, n_steps,
                            n_phase1, ra32, rm32, rate_avg, rate_mean);
         break;
     default:
         return set_err(FLAME_ENOTSUP, "flame_feddyn_round: dtype %d not supported (f32, bf16, f16, f64)", dtype);
     }
-    return launched(BR_DYN + dtype, "flame_feddyn_round");
+    return check_launch("flame_feddyn_round");
 }
 
 int flame_host_register(void* host, uint64_t nbytes) {
@@ -1780,15 +2220,6 @@ int flame_slab_write_2d(const flame_tile_copy* table, int32_t n_entries, void* s
     }
     g_err[0] = 0;
     return FLAME_OK;
-}
-
-int32_t flame_launch_branches(void) { return BR_COUNT; }
-
-const char* flame_launch_branch_name(int32_t branch) { return branch_name(branch); }
-
-int64_t flame_launch_branch_count(int32_t branch) {
-    if (branch < 0 || branch >= BR_COUNT) return -1;
-    return g_launches[branch].load(std::memory_order_relaxed);
 }
 
 }  // extern "C"
