@@ -928,14 +928,14 @@ __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel(const flame_hier_s
 
 // The same with the metadata block in the kernel arguments (small launches, e.g. a single
 // FedBuff aggregator's fused scale_add); word offsets into the block, -1 = no delta table.
-template <int DT, int CU, bool SYNC>
+template <int DT, int CU, bool SYNC, int HB, bool HL>
 __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel_argmeta(const ArgMeta meta, int n_segs, int n_mids, int n_clients,
                                                             int o_mid_w, int o_mid_delta, int o_clients,
                                                             int o_mid_rates, int o_mid_goal, int o_top_rates,
                                                             float top_goal, unsigned flags) {
     (void)sizeof(meta);     // read in place in the kernarg segment (see agg_reduce_kernel_argmeta)
     const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    hier_fedbuff_body<DT, CU, SYNC, kHB, false>(reinterpret_cast<const flame_hier_segment*>(w), n_segs, n_mids, n_clients,
+    hier_fedbuff_body<DT, CU, SYNC, HB, HL>(reinterpret_cast<const flame_hier_segment*>(w), n_segs, n_mids, n_clients,
                                     w + o_mid_w, o_mid_delta >= 0 ? w + o_mid_delta : nullptr, w + o_clients,
                                     reinterpret_cast<const float*>(w + o_mid_rates),
                                     reinterpret_cast<const float*>(w + o_mid_goal),
@@ -1196,7 +1196,8 @@ enum : int {
     BR_AGG_ARG_LO = 65,   // + dt (f32, bf16, f16): flame_agg_reduce_argmeta, 2 workgroups per CU
     BR_HIER_ARG_LO = 68,  // + dt: flame_hier_fedbuff_argmeta, one middle over a long launch
     BR_OPT_ARG_MULTI = 71,  // + variant: flame_fedopt_reduce_adapt_argmeta, fp32, kOptWGC chunks per workgroup
-    BR_COUNT = 74
+    BR_HIER_ARG_LDS = 74,   // + dt * 2 + sync: flame_hier_fedbuff_argmeta, LDS store groups
+    BR_COUNT = 80
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -1222,7 +1223,8 @@ const char* branch_name(int i) {
             else if (b < BR_AGG_ARG_LO) snprintf(n, z, "flame_feddyn_round/%s", dts[b - BR_DYN]);
             else if (b < BR_HIER_ARG_LO) snprintf(n, z, "flame_agg_reduce_argmeta/lo/%s", dts[b - BR_AGG_ARG_LO]);
             else if (b < BR_OPT_ARG_MULTI) snprintf(n, z, "flame_hier_fedbuff_argmeta/lo/%s/fedbuff", dts[b - BR_HIER_ARG_LO]);
-            else snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
+            else if (b < BR_HIER_ARG_LDS) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
+            else snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
         }
         return true;
     }();
@@ -1584,35 +1586,38 @@ int flame_hier_fedbuff_argmeta(int dtype, unsigned flags, const void* host_meta,
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     const bool sync = (flags & FLAME_HIER_SYNC) != 0;
-    // one middle over a long launch (a FedBuff aggregator's fused scale_add of >= 64 arrivals into
-    // a model of a few keys): the low-residency instantiation, as in flame_hier_fedbuff
-    if (!sync && n_mids == 1 && n_clients >= kHLoMinClients && n_chunks >= kHLoMinChunks &&
-        (dtype == FLAME_F32 || dtype == FLAME_BF16 || dtype == FLAME_F16)) {
-#define FLAME_HIER_ARG_LO(DT, LDSB)                                                                              \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, kHLoUnroll, false>), grid, block, LDSB, st, m, n_segs, \
-                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags)
-        if (dtype == FLAME_F32) FLAME_HIER_ARG_LO(FLAME_F32, kHLoLdsF32);
-        else if (dtype == FLAME_BF16) FLAME_HIER_ARG_LO(FLAME_BF16, kHLoLds16);
-        else FLAME_HIER_ARG_LO(FLAME_F16, kHLoLds16);
-#undef FLAME_HIER_ARG_LO
-        return launched(BR_HIER_ARG_LO + dtype, "flame_hier_fedbuff_argmeta");
+    // the instantiation flame_hier_fedbuff picks for the same launch shape: LDS store groups for
+    // many middles, the low-residency one for one middle over a long launch (a FedBuff
+    // aggregator's fused scale_add of >= 64 arrivals into a model of a few keys), else register groups
+    const bool lds = n_mids >= kHLdsMinMids;
+    const bool lo = !lds && !sync && n_mids == 1 && n_clients >= kHLoMinClients && n_chunks >= kHLoMinChunks;
+#define FLAME_HIER_ARG_GO(DT, CUV, SY, HB, HL, LDSB)                                                            \
+    hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, SY, HB, HL>), grid, block, LDSB, st, m, n_segs, n_mids, \
+                       n_clients, ow, od, oc, orr, og, ot, top_goal, flags)
+#define FLAME_HIER_ARG_LAUNCH(DT, CUV, CUL, LOLDS)                                                              \
+    if (lds) {                                                                                                 \
+        if (sync) FLAME_HIER_ARG_GO(DT, CUL, true, kHBL, true, 0);                                             \
+        else FLAME_HIER_ARG_GO(DT, CUL, false, kHBL, true, 0);                                                 \
+        br = BR_HIER_ARG_LDS + DT * 2 + sync;                                                                  \
+    } else if (lo) {                                                                                           \
+        FLAME_HIER_ARG_GO(DT, kHLoUnroll, false, kHB, false, LOLDS);                                           \
+        br = BR_HIER_ARG_LO + DT;                                                                              \
+    } else {                                                                                                   \
+        if (sync) FLAME_HIER_ARG_GO(DT, CUV, true, kHB, false, 0);                                             \
+        else FLAME_HIER_ARG_GO(DT, CUV, false, kHB, false, 0);                                                 \
+        br = BR_HIER_ARG + DT * 2 + sync;                                                                      \
     }
-#define FLAME_HIER_ARG_LAUNCH(DT, CUV)                                                                          \
-    if (sync)                                                                                                  \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, true>), grid, block, 0, st, m, n_segs,             \
-                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);                      \
-    else                                                                                                       \
-        hipLaunchKernelGGL((hier_fedbuff_kernel_argmeta<DT, CUV, false>), grid, block, 0, st, m, n_segs,            \
-                           n_mids, n_clients, ow, od, oc, orr, og, ot, top_goal, flags);
+    int br = 0;
     switch (dtype) {
-    case FLAME_F32: FLAME_HIER_ARG_LAUNCH(FLAME_F32, kClientUnroll) break;
-    case FLAME_BF16: FLAME_HIER_ARG_LAUNCH(FLAME_BF16, kHierUnroll16) break;
-    case FLAME_F16: FLAME_HIER_ARG_LAUNCH(FLAME_F16, kHierUnroll16) break;
+    case FLAME_F32: FLAME_HIER_ARG_LAUNCH(FLAME_F32, kClientUnroll, kClientUnroll, kHLoLdsF32) break;
+    case FLAME_BF16: FLAME_HIER_ARG_LAUNCH(FLAME_BF16, kHierUnroll16, kHierLdsUnroll16, kHLoLds16) break;
+    case FLAME_F16: FLAME_HIER_ARG_LAUNCH(FLAME_F16, kHierUnroll16, kHierLdsUnroll16, kHLoLds16) break;
+#undef FLAME_HIER_ARG_GO
 #undef FLAME_HIER_ARG_LAUNCH
     default:
         return set_err(FLAME_ENOTSUP, "flame_hier_fedbuff_argmeta: dtype %d not supported (f32, bf16, f16)", dtype);
     }
-    return launched(BR_HIER_ARG + dtype * 2 + sync, "flame_hier_fedbuff_argmeta");
+    return launched(br, "flame_hier_fedbuff_argmeta");
 }
 
 int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {

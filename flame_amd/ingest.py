@@ -39,9 +39,6 @@ from typing import Any, Dict
 
 import torch
 
-# torch.frombuffer warns on a read-only buffer (a received `bytes` payload); the views are only
-# read, so that one warning is silenced (once, instead of a catch_warnings block per tensor)
-warnings.filterwarnings("ignore", message="The given buffer is not writable", category=UserWarning)
 
 # ------------------------------------------------------------------ legacy storage stream
 _STORAGE_DTYPES = {
@@ -373,9 +370,7 @@ class PayloadDecoder:
         nbytes = numel * torch.empty(0, dtype=obj.dtype).element_size()
         if q + nbytes > span.start + span.n:
             raise pickle.UnpicklingError("storage runs past its bytes")
-        seen = _STORAGE_RECORDS.setdefault(q - rec0, {})
-        if len(seen) < 4096:
-            seen[bytes(self.mv[rec0:q])] = (obj.dtype, numel, nbytes)
+        _remember_record(bytes(self.mv[rec0:q]), (obj.dtype, numel, nbytes))
         return _StorageRef(self.buf, q, numel, obj.dtype)
 
 
@@ -468,6 +463,23 @@ def _parse_storage_record_slow(mv, q):
 
 _STORAGE_HEADERS = []   # validated legacy-stream headers (bytes)
 _STORAGE_RECORDS = {}   # record length -> {record bytes: (dtype, numel, nbytes)} (see _storage_from_span)
+# The record cache is keyed by bytes the sender controls: bounded in total so no sender can grow
+# host memory or the per-message lookup cost -- short records only, few distinct lengths, few
+# entries (a record of another length or past the caps is simply parsed by the VM again).
+RECORD_CACHE_MAX_BYTES = 512
+RECORD_CACHE_MAX_LENGTHS = 8
+RECORD_CACHE_MAX_ENTRIES = 4096
+
+
+def _remember_record(rec: bytes, parsed) -> None:
+    n = len(rec)
+    if n > RECORD_CACHE_MAX_BYTES:
+        return
+    if n not in _STORAGE_RECORDS and len(_STORAGE_RECORDS) >= RECORD_CACHE_MAX_LENGTHS:
+        return
+    if sum(len(v) for v in _STORAGE_RECORDS.values()) >= RECORD_CACHE_MAX_ENTRIES:
+        return
+    _STORAGE_RECORDS.setdefault(n, {})[rec] = parsed
 
 
 class _Span:
@@ -560,7 +572,8 @@ def decode(payload, extra_globals: Dict[tuple, Any] = None):
     """Decode a flame update message; tensors are zero-copy views into ``payload``.
 
     ``payload`` must stay alive (and unmodified) while the tensors are in use;
-    they are read-only views.  Raises ``pickle.UnpicklingError`` for anything
+    they are read-only views -- modifying one in place would write into the
+    payload (a ``bytes`` object) without any warning.  Raises ``pickle.UnpicklingError`` for anything
     outside the allowlist (use the reference ``cloudpickle.loads`` for such
     messages).
     """
@@ -570,7 +583,12 @@ def decode(payload, extra_globals: Dict[tuple, Any] = None):
             if isinstance(v, type) and issubclass(v, enum.Enum):
                 _CALLABLE_ALLOW.add(v)
     try:
-        obj, _ = dec.load(0)
+        # torch.frombuffer warns on a read-only buffer (a received `bytes` payload): the decoded
+        # views are READ-ONLY by contract (see above) -- the warning is silenced for this
+        # payload's decode only, once, not process-wide
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message="The given buffer is not writable", category=UserWarning)
+            obj, _ = dec.load(0)
     except pickle.UnpicklingError:
         raise
     except (IndexError, KeyError, ValueError, TypeError, struct.error, UnicodeDecodeError) as e:

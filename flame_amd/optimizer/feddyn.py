@@ -202,7 +202,13 @@ class FedDyn(FedAvg):
         pp = self.history.startswith("pingpong")
         if pp and self._pp is None:
             self._init_pingpong(arrivals, device)
-        fused = [k for k in base_weights if (self._fusable_pp(k, arrivals) if pp
+        # keys some end's history of which left the stores (one pass over the ends, not one per key)
+        moved = set()
+        if pp:
+            for h in self.local_param_dict.values():
+                if isinstance(h, _StoredHistory) and h.rest:
+                    moved.update(h.rest.keys())
+        fused = [k for k in base_weights if (self._fusable_pp(k, arrivals, moved) if pp
                                              else self._fusable(k, arrivals, had, device))]
         rest = [k for k in base_weights if k not in fused]
         new_hist = {e: {} for e, _ in arrivals if e not in had}
@@ -259,7 +265,7 @@ class FedDyn(FedAvg):
         self._pp = _PingPongHistories(template, device, max(len(self.local_param_dict), 1),
                                       tiled=self.history == "pingpong")
 
-    def _fusable_pp(self, k, arrivals) -> bool:
+    def _fusable_pp(self, k, arrivals, moved) -> bool:
         a = self.agg_weights[k]
         t = self._pp.template.get(k)
         if t is None or t.dtype != a.dtype or t.shape != a.shape:
@@ -268,7 +274,7 @@ class FedDyn(FedAvg):
             return False
         # an end whose history of k left the stores (another dtype, see _pp_absorb) keeps the
         # key on the reference path: the stores do not hold its current value
-        return not any(isinstance(h, _StoredHistory) and k in h.rest for h in self.local_param_dict.values())
+        return k not in moved
 
     def _pp_absorb(self, keys, arrivals, had, new_hist):
         """Template keys that took the reference path this round (an arrival in another dtype):

@@ -203,6 +203,15 @@ class UpdateSlab:
         """
         cur = engine.current_stream(self.device)
         st = stream or cur
+        for k in self.keys:     # validate before the slot's reader event is consumed (a refused
+            if k not in weights:    # write leaves the slot guarded for the next writer)
+                raise KeyError(k)
+            dt, _, n, _, _ = self.meta[k]
+            src = weights[k]
+            if src.numel() != n:
+                raise RuntimeError(f"{k}: {src.numel()} elements, slab expects {n}")
+            if src.dtype != dt:
+                raise NotImplementedError(f"{k}: dtype {src.dtype} != slab dtype {dt}")
         ev = self._ready.pop(slot, None)
         if ev is not None:
             st.wait_event(ev)
@@ -210,14 +219,8 @@ class UpdateSlab:
         dev_rows, host_rows, keep = [], [], []
         sync = False
         for i, k in enumerate(self.keys):
-            if k not in weights:
-                raise KeyError(k)
             dt, shape, n, tile0, tiles = self.meta[k]
             src = weights[k]
-            if src.numel() != n:
-                raise RuntimeError(f"{k}: {src.numel()} elements, slab expects {n}")
-            if src.dtype != dt:
-                raise NotImplementedError(f"{k}: dtype {src.dtype} != slab dtype {dt}")
             if src.is_cuda and src.device != self.device:
                 with torch.cuda.stream(st):
                     src = src.to(self.device, non_blocking=True)

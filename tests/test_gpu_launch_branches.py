@@ -323,3 +323,39 @@ def test_fedopt_eager_aliased_step_fused(dt, sort):
         elif i >= 2:
             S.assert_close_fedopt(f"eager/{sort}/{dt}/step{i}/cur", S.to_cpu(got), exp, elementwise=i == 2)
         S.assert_bitwise(f"eager/{sort}/{dt}/step{i}/avg", S.to_cpu(bw), ob)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64,
+                                   torch.int32])
+def test_device_table_reduction_every_dtype(dtype, monkeypatch):
+    """flame_agg_reduce through the device-table launch (engine.ARGMETA off) for every dtype
+    the kernel instantiates, 37 clients over a ragged 70,001 + 3-element model, bitwise ==
+    the oracle (the kernel-argument launch is test_reduce_vs_oracle_dtypes)."""
+    from flame_amd import engine
+    O = _oracle()
+    monkeypatch.setattr(engine, "ARGMETA", False)
+    g = torch.Generator().manual_seed(23)
+    n, shapes = 37, {"a": (70_001,), "b": (3,)}
+    if dtype.is_floating_point:
+        base = {k: torch.randn(s, generator=g, dtype=torch.float64).to(dtype) for k, s in shapes.items()}
+        cl = [{k: (torch.randn(s, generator=g, dtype=torch.float64) * 1e-2).to(dtype) for k, s in shapes.items()}
+              for _ in range(n)]
+    else:
+        base = {k: torch.randint(-1000, 1000, s, generator=g, dtype=dtype) for k, s in shapes.items()}
+        cl = [{k: torch.randint(-100, 100, s, generator=g, dtype=dtype) for k, s in shapes.items()} for _ in range(n)]
+    counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+    total = sum(counts)
+    exp = {k: v.clone() for k, v in base.items()}
+    for k in exp:
+        O.reduce_tensor(exp[k], [c[k] for c in cl], [c / total for c in counts])
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i:03d}"] = S.TR({k: v.to(DEV) for k, v in cl[i].items()}, counts[i])
+    before = _counts()
+    out = S_make("fedavg").do({k: v.to(DEV) for k, v in base.items()}, cache, total=total)
+    torch.cuda.synchronize()
+    hits = _diff(before, _counts())
+    code = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.float64: "f64",
+            torch.int64: "i64", torch.int32: "i32"}[dtype]
+    assert hits == {f"flame_agg_reduce/{code}": 1}, hits
+    S.assert_bitwise(f"table/{code}", out, exp)

@@ -911,15 +911,20 @@ def test_middle_group_flush_and_scale_add_many(dtype):
 @pytest.mark.parametrize("placement", ["slab", "tensors", "mixed"])
 @pytest.mark.parametrize("top_start", ["none", "existing"])
 @pytest.mark.parametrize("M", [5, 21])
-def test_hierarchy_round_one_pass(dtype, placement, top_start, M):
+@pytest.mark.parametrize("path", ["argmeta", "table"])
+def test_hierarchy_round_one_pass(dtype, placement, top_start, M, path, monkeypatch):
     """flame_hier_fedbuff (the co-located middles + top in ONE launch) == the separate
     launches (scale_add_agg_weights_with_delta per middle, top FedBuff.do per delta,
     top scale_add) == the oracle's op sequence, bitwise: top aggregate, top weights,
     middle weights and deltas.  M = 5 takes the register store groups, M = 21 the LDS-held
-    groups of 16 (>= FLAME_HLDS_MIN_MIDS) with a partial last group."""
+    groups of 16 (>= kHLdsMinMids) with a partial last group; both through the kernel-argument
+    launch and the device-table one (engine.ARGMETA off)."""
+    from flame_amd import engine
     from flame_amd.optimizer.fedbuff import hierarchy_round, _compose_hierarchy
     from flame_amd.slab import UpdateSlab
     O = _oracle()
+    if path == "table":
+        monkeypatch.setattr(engine, "ARGMETA", False)
     g = torch.Generator().manual_seed(41)
     shapes = {"w": (3001,), "m": (17, 129), "b": (5,)}
     C, rnd = 4, 12
@@ -1269,13 +1274,17 @@ def test_sync_hierarchy_golden(golden, with_delta, slab):
 
 
 @pytest.mark.parametrize("M", [8, 20])
-def test_sync_hierarchy_vs_oracle_readonly_middles(M):
+@pytest.mark.parametrize("path", ["argmeta", "table"])
+def test_sync_hierarchy_vs_oracle_readonly_middles(M, path, monkeypatch):
     """8 / 20 middles x 16 trainers over ~1M params (tails, every float dtype + int64): top
     and deltas == the oracle's FedAvg / delta / FedAvg composition; with
     update_middle_weights=False one shared middle tensor is read, never written.  20
-    middles take the LDS-held store groups (a full group of 16 + 4)."""
+    middles take the LDS-held store groups (a full group of 16 + 4).  Both metadata paths."""
+    from flame_amd import engine
     from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
     O = _oracle()
+    if path == "table":
+        monkeypatch.setattr(engine, "ARGMETA", False)
     g = torch.Generator().manual_seed(41)
     tmpl = _dyn_model(g, 1_000_003)
     C = 16

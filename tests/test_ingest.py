@@ -232,3 +232,31 @@ def test_storage_records_parsed_without_the_vm(monkeypatch):
     payload[i:i + len(b"torch\nFloatStorage\n")] = b"torch\nFloatXtorage\n"
     with pytest.raises(pickle.UnpicklingError):
         ingest.decode(bytes(payload))
+
+
+def test_storage_record_cache_is_bounded():
+    """The VM's record cache is keyed by sender-controlled bytes: long records are never kept,
+    and neither the number of distinct lengths nor the entry count can grow past the caps."""
+    from flame_amd import ingest
+    saved = {k: dict(v) for k, v in ingest._STORAGE_RECORDS.items()}
+    ingest._STORAGE_RECORDS.clear()
+    try:
+        ingest._remember_record(b"x" * (ingest.RECORD_CACHE_MAX_BYTES + 1), (None, 0, 0))
+        assert not ingest._STORAGE_RECORDS
+        for n in range(1, 3 * ingest.RECORD_CACHE_MAX_LENGTHS):
+            ingest._remember_record(b"y" * n, (None, 0, 0))
+        assert len(ingest._STORAGE_RECORDS) == ingest.RECORD_CACHE_MAX_LENGTHS
+        for i in range(2 * ingest.RECORD_CACHE_MAX_ENTRIES):
+            ingest._remember_record(i.to_bytes(4, "little"), (None, 0, 0))
+        assert sum(len(v) for v in ingest._STORAGE_RECORDS.values()) == ingest.RECORD_CACHE_MAX_ENTRIES
+    finally:
+        ingest._STORAGE_RECORDS.clear()
+        ingest._STORAGE_RECORDS.update(saved)
+
+
+def test_decode_does_not_silence_warnings_process_wide():
+    """Importing / using the decoder leaves the process's warning filters alone."""
+    import warnings
+    from flame_amd import ingest  # noqa: F401
+    assert not any(f[1] is not None and "not writable" in f[1].pattern for f in warnings.filters
+                   if f[1] is not None)

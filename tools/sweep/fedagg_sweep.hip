@@ -103,6 +103,12 @@ namespace {
 #ifndef FLAME_BUFLD
 #define FLAME_BUFLD 0     // sweep: client loads as buffer loads, cache policy FLAME_BUFLD - 1 (0 = global loads)
 #endif
+#ifndef FLAME_HTIME
+#define FLAME_HTIME 0     // DIAGNOSTIC: per-workgroup timestamps of the hierarchy kernel (wave 0, lane 0;
+                          // s_memrealtime, 100 MHz) into the buffer flame_sweep_htime() sets
+                          // (tools/hier_attrib.py): start, end, hw ids, each middle's reduction and
+                          // epilogue ends, each LDS store burst's end
+#endif
 #ifndef FLAME_HBATCH
 #define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
                           // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
@@ -187,6 +193,17 @@ namespace {
 #endif
 
 constexpr int kBlock = FLAME_BLOCK;
+#if FLAME_HTIME
+__device__ uint64_t* g_htime = nullptr;
+__device__ int g_htime_slots = 0;
+__device__ __forceinline__ void htime(int slot, uint64_t v) {
+    if (threadIdx.x == 0 && g_htime && slot < g_htime_slots)
+        g_htime[static_cast<int64_t>(blockIdx.x) * g_htime_slots + slot] = v;
+}
+#define FLAME_HT(slot) htime((slot), __builtin_amdgcn_s_memrealtime())
+#else
+#define FLAME_HT(slot) do {} while (0)
+#endif
 constexpr int kHB = FLAME_HBATCH;
 constexpr int kVPT = FLAME_VPT;
 constexpr int kWGC = FLAME_WGC;
@@ -1138,6 +1155,12 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
     bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
     const T* tin = reinterpret_cast<const T*>(sg.top_agg_in) + e0;
     if (vec) {
+        FLAME_HT(0);
+#if FLAME_HTIME
+        // HW_ID (wave / SIMD / CU / SH / SE) and the XCC id of this workgroup's wave 0
+        htime(2, static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) |
+                     (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((15 << 11) | 20)) << 32));
+#endif
         if (have_top) {
 #pragma unroll
             for (int v = 0; v < kVPT; ++v) {
@@ -1260,6 +1283,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
             reduce_clients<DT, CU, true>(acc, !SYNC, crow + static_cast<int64_t>(m) * n_clients, n_clients,
                                          mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
                                          coff);
+            FLAME_HT(3 + 2 * m);
             T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
             const float g = mid_goal[m], rt = top_rates[m];
 #pragma unroll
@@ -1293,6 +1317,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                 if (dp) st_v(dp + v * VS, pack<T, EPT>(d));
             }
             have_top = true;
+            FLAME_HT(4 + 2 * m);
             }
             if (!(flags & FLAME_HIER_MID_READONLY)) {
 #pragma unroll
@@ -1311,6 +1336,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                     }
                 }
             }
+            FLAME_HT(3 + 2 * n_mids + m0 / HB);
         }
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
@@ -1327,6 +1353,7 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                 st_v(gp, pack<T, EPT>(gw));
             }
         }
+        FLAME_HT(1);
         return;
     }
     // tails / misaligned views: element-wise, same op sequence
@@ -2221,5 +2248,16 @@ int flame_slab_write_2d(const flame_tile_copy* table, int32_t n_entries, void* s
     g_err[0] = 0;
     return FLAME_OK;
 }
+
+#if FLAME_HTIME
+// Diagnostic builds only: where the hierarchy kernel writes its timestamps (NULL = nowhere).
+int flame_sweep_htime(void* buf, int32_t slots) {
+    uint64_t* p = static_cast<uint64_t*>(buf);
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_htime), &p, sizeof(p));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_htime_slots), &slots, sizeof(slots));
+    if (e != hipSuccess) return set_err(FLAME_EHIP, "flame_sweep_htime: %s", hipGetErrorString(e));
+    return FLAME_OK;
+}
+#endif
 
 }  // extern "C"
