@@ -76,7 +76,7 @@ def parse():
                          "one tiled UpdateSlab (a chunk's middles are one contiguous block) or one tensor each")
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "hier_fedbuff", "feddyn",
-                             "scaffold", "fedavg_eager"])
+                             "scaffold", "fedavg_eager", "fedadam_eager", "fedyogi_eager", "fedadagrad_eager"])
     ap.add_argument("--eager-defer", default="on", choices=["on", "off"],
                     help="fedavg_eager / --e2e-mode eager: FedAvg(defer=True) queues the one-arrival do() "
                          "calls and reduces them in one launch (on) or launches per arrival (off)")
@@ -476,12 +476,20 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     """The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) on
     device-resident updates: base = deepcopy(weights), then one do() per arrival with the
     running total; the role keeps the returned object (read once, at the round's end).
-    --eager-defer on: FedAvg(defer=True), one launch per round; off: one per arrival."""
+    fedavg_eager: --eager-defer on: FedAvg(defer=True), one launch per round; off: one per
+    arrival.  fed{adam,yogi,adagrad}_eager: FedOPT.do per arrival, one fused
+    flame_fedopt_reduce_adapt launch each (FedAvg of the arrival + the adaptive step); the
+    first round -- untimed, reported apart -- holds the round-1 passthrough and the aliased
+    step (current_weights IS base: FLAME_SEG_CUR_IS_AVG)."""
+    from flame_amd import engine
     from flame_amd.optimizers import optimizer_provider
     if world > 1:
-        raise SystemExit("--workload fedavg_eager is a one-GPU bench")
+        raise SystemExit(f"--workload {args.workload} is a one-GPU bench")
     defer = args.eager_defer == "on"
-    opt = optimizer_provider.get("fedavg", defer=defer)
+    sort = args.workload[:-len("_eager")]
+    fedopt = sort != "fedavg"
+    opt = optimizer_provider.get(sort) if fedopt else optimizer_provider.get("fedavg", defer=defer)
+    kname = "flame_fedopt_reduce_adapt" if fedopt else "flame_agg_reduce"
     keys = [f"{i:05d}" for i in range(n)]
     state = {"weights": {"model": base}}
 
@@ -495,19 +503,30 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
             out = opt.do(bw, cache, total=running, num_trainers=n)
         state["weights"] = {"model": out["model"]}              # self.weights = global_weights; read
 
+    first = None
+    if fedopt:
+        engine.kernel_events = []
+        step()                  # round 1: passthrough, then the aliased step, then the rest
+        torch.cuda.synchronize()
+        ev = [e for e in engine.kernel_events if e[0] == kname]
+        engine.kernel_events = None
+        first = {"launches": len(ev), "aliased_step_kernel_ms": ev[0][1].elapsed_time(ev[0][2]) if ev else None,
+                 "note": "arrival 1: FedAvg passthrough (flame_agg_reduce); arrival 2: current IS base, the "
+                         "fused step with FLAME_SEG_CUR_IS_AVG (its kernel time here); arrivals 3..n: fused"}
     elapsed, events = timed(world, args.steps, args.warmup, step)
-    ks = kernel_stats(events, "flame_agg_reduce")
+    ks = kernel_stats(events, kname)
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
         print(json.dumps({
-            "metric": "aggregated params/sec (device-resident), eager FedAvg round",
+            "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
             "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32",
-            "config": {"workload": f"fedavg_eager: {n} arrivals (one do() each, running total) x {P} fp32 "
-                                   f"params, {args.layout} layout, defer {args.eager_defer}"},
+            "config": {"workload": f"{args.workload}: {n} arrivals (one do() each, running total) x {P} fp32 "
+                                   f"params, {args.layout} layout" + ("" if fedopt else f", defer {args.eager_defer}")},
+            "first_round": first,
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": "flame_agg_reduce",
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes,
                          "bytes_per_client_param": k_bytes / (n * P * 4)},
@@ -527,7 +546,8 @@ def main():
     if args.workload == "fedbuff":
         return bench_fedbuff(args, world, rank, dev)
 
-    n = args.clients or {"feddyn": 512, "scaffold": 512, "fedavg_eager": 64}.get(args.workload, 1024)
+    n = args.clients or {"feddyn": 512, "scaffold": 512}.get(args.workload,
+                                                          64 if args.workload.endswith("_eager") else 1024)
     P = args.params or 25_000_000
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
@@ -540,7 +560,7 @@ def main():
     counts = synth.counts(args.seed, n)
     if args.workload in ("feddyn", "scaffold"):
         return bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts)
-    if args.workload == "fedavg_eager":
+    if args.workload.endswith("_eager"):
         return bench_eager(args, world, rank, dev, n, P, client_w, base, counts)
     base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
     total = int(counts.sum())
@@ -583,7 +603,8 @@ def main():
             doc = json.load(open(args.traffic))
             for tr in (doc["entries"] if "entries" in doc else [doc]):
                 if (tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P
-                        and tr.get("layout", "row") == args.layout):
+                        and tr.get("layout", "row") == args.layout
+                        and tr.get("workload", args.workload) == args.workload):
                     traffic = tr["hbm_bytes_per_launch"]
         except Exception:  # noqa: BLE001
             pass
@@ -1091,6 +1112,14 @@ def bench_fedbuff(args, world, rank, dev):
 
     elapsed, events = timed(world, args.steps, args.warmup, step)
     if rank == 0:
+        traffic = None
+        try:
+            for tr in json.load(open(args.traffic))["entries"]:
+                if (tr.get("kernel") == "flame_hier_fedbuff" and tr.get("workload") == "fedbuff"
+                        and tr.get("clients") == K and tr.get("params") == P):
+                    traffic = tr["hbm_bytes_per_launch"]
+        except Exception:  # noqa: BLE001
+            pass
         kst = {nm: kernel_stats(events, nm) for nm in sorted({e[0] for e in events})}
         k_time = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         k_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kst.values()) / args.steps
@@ -1102,7 +1131,7 @@ def bench_fedbuff(args, world, rank, dev):
                        "fuse_scale_add": args.fedbuff_fuse},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel_ms_per_step": k_time * 1e3,
-                         "algorithmic_bytes_per_step": k_bytes,
+                         "algorithmic_bytes_per_step": k_bytes, "traffic": traffic,
                          "bytes_per_client_param": k_bytes / (K * P * 4)},
             "kernels": kst,
         }), flush=True)

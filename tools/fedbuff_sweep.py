@@ -46,7 +46,9 @@ def main():
     names = a.variants.split(",")
     libs = {}
     for nm in names:
-        _native._lib, _native.LIB_PATH = None, os.path.join(VDIR, f"lib_{nm}.so")
+        # a name with a "/" is a library path (e.g. flame_amd/libflame_amd.so, build/diag/lib_base.so)
+        path = os.path.join(ROOT, nm) if "/" in nm else os.path.join(VDIR, f"lib_{nm}.so")
+        _native._lib, _native.LIB_PATH = None, path
         libs[nm] = _native.lib()
     dev = torch.device("cuda", 0)
     K, P = a.arrivals, a.params

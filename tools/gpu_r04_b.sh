@@ -28,6 +28,9 @@ step gloo8_fedavg 400 $G8 bench.py --gpus 8 --clients 64 --params 1000000 --step
 step gloo8_fedadagrad 400 $G8 bench.py --gpus 8 --clients 64 --params 1000000 --steps 3 --warmup 1 --workload fedadagrad
 step gloo8_hier 400 $G8 bench.py --gpus 8 --clients 256 --params 1000000 --steps 3 --warmup 1 --workload hier_fedbuff
 unset FLAME_BENCH_BACKEND
+step fedadam_eager 300 python bench.py --workload fedadam_eager --steps 5 --warmup 2
+TAIL=3 step fedbuff_ab_f32 300 python -u tools/fedbuff_sweep.py --variants build/diag/lib_base.so,flame_amd/libflame_amd.so --rounds 6
+TAIL=3 step fedbuff_ab_bf16 300 python -u tools/fedbuff_sweep.py --dtype bf16 --variants build/diag/lib_base.so,flame_amd/libflame_amd.so --rounds 6
 TAIL=2 step fedopt_spread 500 python -u tools/fedopt_spread.py --rounds 9
 TAIL=40 step hier_attrib 400 python -u tools/hier_attrib.py --reps 5 --out $OUT/hier_attrib.json
 exit 0

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--layout", default="slab")
+    ap.add_argument("--workload", default=None,
+                    help="bench.py workload the passes ran (part of the entry's key: FedAdam / FedYogi / "
+                         "FedAdaGrad share a kernel name)")
     ap.add_argument("--itemsize", type=int, default=4, help="bytes per element (bf16: 2)")
     ap.add_argument("--extra-arrays", type=int, default=2,
                     help="P-sized arrays besides the N clients in the algorithmic bytes (FedAvg 2, FedOPT 8)")
@@ -52,6 +55,7 @@ def main():
     algo = (a.clients + a.extra_arrays) * a.params * a.itemsize
     res = {
         "kernel": a.name, "clients": a.clients, "params": a.params, "layout": a.layout,
+        **({"workload": a.workload} if a.workload else {}),
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb, "dispatches": [len(fetch), len(write)],
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
@@ -66,7 +70,8 @@ def main():
         entries = doc["entries"] if "entries" in doc else [doc]
     except Exception:  # noqa: BLE001
         entries = []
-    key = lambda e: (e.get("kernel"), e.get("clients"), e.get("params"), e.get("layout", "row"))  # noqa: E731
+    key = lambda e: (e.get("kernel"), e.get("clients"), e.get("params"), e.get("layout", "row"),  # noqa: E731
+                     e.get("workload"))
     entries = [e for e in entries if key(e) != key(res)] + [res]
     json.dump({"entries": entries}, open(a.out, "w"), indent=1)
     print(json.dumps(res))

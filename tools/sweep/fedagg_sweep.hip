@@ -2260,4 +2260,10 @@ int flame_sweep_htime(void* buf, int32_t slots) {
 }
 #endif
 
+// The product library's launch-branch counters are not kept in sweep builds (the same symbols,
+// so flame_amd._native binds a sweep build too): no branches.
+int32_t flame_launch_branches(void) { return 0; }
+const char* flame_launch_branch_name(int32_t) { return nullptr; }
+int64_t flame_launch_branch_count(int32_t) { return -1; }
+
 }  // extern "C"
