@@ -595,3 +595,25 @@ def test_deferred_aggregates_pickle_as_plain_dicts(monkeypatch):
     torch.save(agg, buf)
     back = torch.load(io.BytesIO(buf.getvalue()), weights_only=True)
     assert isinstance(back, dict) and torch.equal(back["x"], torch.ones(4))
+
+
+def test_shard_collective_failure_names_rank_and_wave():
+    """A failing all-gather (or its wait) re-raises naming this rank and the wave, so an N>1
+    bench that dies in a collective says where (bench.py exits non-zero with it)."""
+    import pytest
+    from flame_amd import shard
+    comm = shard._Comm()
+    comm.dist, comm.rank, comm.world, comm.backend = object(), 3, 8, "nccl"
+
+    def boom(pairs, wave):
+        raise RuntimeError("NCCL error: unhandled system error")
+    comm._all_gather_inplace = boom
+    with pytest.raises(RuntimeError, match=r"rank 3 of 8 \(nccl\): all-gather of wave 2 failed"):
+        comm.all_gather_inplace([(None, None)], wave=2)
+
+    class W:
+        def wait(self):
+            raise RuntimeError("timeout")
+    comm._works = [(1, W())]
+    with pytest.raises(RuntimeError, match=r"rank 3 of 8 \(nccl\): wait on the all-gather of wave 1 failed"):
+        comm.wait()
