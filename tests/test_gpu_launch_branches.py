@@ -359,3 +359,81 @@ def test_device_table_reduction_every_dtype(dtype, monkeypatch):
             torch.int64: "i64", torch.int32: "i32"}[dtype]
     assert hits == {f"flame_agg_reduce/{code}": 1}, hits
     S.assert_bitwise(f"table/{code}", out, exp)
+
+
+@pytest.mark.parametrize("dt", list(DTS))
+@pytest.mark.parametrize("mode", ["fedbuff", "sync"])
+def test_hierarchy_lds_groups_kernel_argument_launch(dt, mode):
+    """16 middles (>= kHLdsMinMids: LDS-held store groups) small enough for the kernel-argument
+    launch -- flame_hier_fedbuff_argmeta/lds -- bitwise == the roles' separate calls on the
+    oracle: FedBuff mode (asyncfl middles' FedBuff + scale_add + delta, the top's FedBuff of
+    the deltas + scale_add) and sync mode (syncfl middles' FedAvg from their weights, deltas,
+    the top's FedAvg of the deltas)."""
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    O = _oracle()
+    dtype = DTS[dt]
+    g = torch.Generator().manual_seed(29)
+    M, C, P, rnd = 16, 2, 5_003, 9
+    ups = [[(torch.randn(P, generator=g) * 1e-2).to(dtype) for _ in range(C)] for _ in range(M)]
+    mid0 = [torch.randn(P, generator=g).to(dtype) for _ in range(M)]
+    top0 = torch.randn(P, generator=g).to(dtype)
+    counts = [[int(x) for x in torch.randint(1, 100, (C,), generator=g)] for _ in range(M)]
+    mids = [{"x": w.to(DEV)} for w in mid0]
+    top = {"x": top0.to(DEV)}
+    before = _counts()
+    if mode == "fedbuff":
+        aggs = []
+        for m in range(M):
+            opt = S_make("fedbuff")
+            aggs.append(opt.do_arrivals(None, [S.TR({"x": u.to(DEV)}, 1, rnd - (m + t) % 3)
+                                               for t, u in enumerate(ups[m])], version=rnd))
+        before = _counts()
+        hierarchy_round([(mids[m], aggs[m], C, rnd - m % 2) for m in range(M)], None, version=rnd,
+                        top_weights=top, top_goal=M)
+    else:
+        specs = []
+        for m in range(M):
+            c = S.SortedCache()
+            for t in range(C):
+                c[f"{t}"] = S.TR({"x": ups[m][t].to(DEV)}, counts[m][t])
+            specs.append((mids[m], c, sum(counts[m])))
+        sync_hierarchy_round(specs, top)
+    torch.cuda.synchronize()
+    hits = _diff(before, _counts())
+    assert hits == {f"flame_hier_fedbuff_argmeta/lds/{dt}/{mode}": 1}, hits
+    # the oracle: the roles' separate calls
+    exp_mids, deltas = [], []
+    for m in range(M):
+        w = {"x": mid0[m].clone()}
+        if mode == "fedbuff":
+            fb, agg = O.OracleFedBuff(), None
+            for t in range(C):
+                c = S.SortedCache()
+                c["a"] = S.TR({"x": ups[m][t].clone()}, 1, rnd - (m + t) % 3)
+                agg = fb.do(agg, c, total=1, version=rnd)
+            deltas.append({"x": O.scale_add_tensor(w["x"], agg["x"], C, want_delta=True)})
+        else:
+            c = S.SortedCache()
+            for t in range(C):
+                c[f"{t}"] = S.TR({"x": ups[m][t].clone()}, counts[m][t])
+            new = O.OracleFedAvg().do({"x": w["x"].clone()}, c, total=sum(counts[m]))
+            deltas.append({"x": new["x"] - w["x"]})
+            w = new
+        exp_mids.append(w)
+    exp_top = {"x": top0.clone()}
+    if mode == "fedbuff":
+        ot, tagg = O.OracleFedBuff(), None
+        for m in range(M):
+            c = S.SortedCache()
+            c["d"] = S.TR(deltas[m], 1, rnd - m % 2)
+            tagg = ot.do(tagg, c, total=1, version=rnd)
+        ot.scale_add_agg_weights(exp_top, tagg, M)
+    else:
+        c = S.SortedCache()
+        for m in range(M):
+            c[f"mid{m:02d}"] = S.TR(deltas[m], sum(counts[m]))
+        O.OracleFedAvg().do(exp_top, c, total=sum(sum(x) for x in counts))
+    for m in range(M):
+        S.assert_bitwise(f"lds-argmeta/{mode}/{dt}/mid{m}", S.to_cpu(mids[m]), exp_mids[m])
+    S.assert_bitwise(f"lds-argmeta/{mode}/{dt}/top", S.to_cpu(top), exp_top)

@@ -25,7 +25,6 @@ step gloo2_hier 300 $G2 bench.py --gpus 2 --clients 256 --params 1000000 --steps
 step gloo2_hier_sync_fetched 300 $G2 bench.py --gpus 2 --clients 256 --params 1000000 --steps 3 --warmup 1 --workload hier_fedbuff --hier-mode sync --hier-middles fetched
 G8="python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29547"
 step gloo8_fedavg 400 $G8 bench.py --gpus 8 --clients 64 --params 1000000 --steps 3 --warmup 1
-step gloo8_fedadagrad 400 $G8 bench.py --gpus 8 --clients 64 --params 1000000 --steps 3 --warmup 1 --workload fedadagrad
 step gloo8_hier 400 $G8 bench.py --gpus 8 --clients 256 --params 1000000 --steps 3 --warmup 1 --workload hier_fedbuff
 unset FLAME_BENCH_BACKEND
 step fedadam_eager 300 python bench.py --workload fedadam_eager --steps 5 --warmup 2
