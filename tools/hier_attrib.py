@@ -36,7 +36,8 @@ SLOTS = 256
 def build():
     from flame_amd import build as B
     os.makedirs(VDIR, exist_ok=True)
-    for nm, defs in (("base", []), ("htime", ["-DFLAME_HTIME=1"])):
+    for nm, defs in (("base", []), ("htime", ["-DFLAME_HTIME=1"]), ("hnx", ["-DFLAME_HNX=1"]),
+                     ("htime_hnx", ["-DFLAME_HTIME=1", "-DFLAME_HNX=1"])):
         subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", os.path.join(VDIR, f"lib_{nm}.so"),
                                B.SWEEP_SRC])
 
@@ -63,6 +64,7 @@ def main():
     ap.add_argument("--params", type=int, default=125_000_000 // 8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variant", default="", help="'' = base / htime, 'hnx' = hnx / htime_hnx")
     a = ap.parse_args()
     if a.build:
         build()
@@ -93,7 +95,8 @@ def main():
     dm = torch.from_numpy(p.meta).to(dev)
     b = dm.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    libs = {nm: load(nm) for nm in ("base", "htime")}
+    plain, stamped = ("hnx", "htime_hnx") if a.variant == "hnx" else ("base", "htime")
+    libs = {"base": load(plain), "htime": load(stamped)}
     ts = torch.zeros(p.n_chunks * SLOTS, dtype=torch.int64, device=dev)
     assert libs["htime"].flame_sweep_htime(ts.data_ptr(), SLOTS) == 0
     per_cu = libs["base"].flame_hier_resident_per_cu(code, 0, M)

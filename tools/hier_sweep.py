@@ -118,7 +118,8 @@ def build_variants(names):
 
 
 def load(name):
-    L = ctypes.CDLL(os.path.join(VDIR, f"lib_{name}.so"))
+    # a name with a "/" is a library path (e.g. build/diag/lib_hnx.so, flame_amd/libflame_amd.so)
+    L = ctypes.CDLL(os.path.join(ROOT, name) if "/" in name else os.path.join(VDIR, f"lib_{name}.so"))
     vp, i32, i64, u32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint, ctypes.c_float
     L.flame_hier_fedbuff.restype = ctypes.c_int
     L.flame_hier_fedbuff.argtypes = [ctypes.c_int, u32, vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, f32, vp]

@@ -109,6 +109,12 @@ namespace {
                           // (tools/hier_attrib.py): start, end, hw ids, each middle's reduction and
                           // epilogue ends, each LDS store burst's end
 #endif
+#ifndef FLAME_HNX
+#define FLAME_HNX 0       // hierarchy kernel (LDS store groups, FedBuff mode): the next middle's first batch of
+                          // arrivals is loaded BEFORE the current middle's epilogue (weights load, scale_add,
+                          // delta, top), so loads stay in flight across it; whole batches only (the remainder
+                          // loads together)
+#endif
 #ifndef FLAME_HBATCH
 #define FLAME_HBATCH 8    // hierarchy kernel: middles whose weight stores are issued together
                           // (C5 shard: 8 -> -1.3..1.6 % vs 1, tools/hier_sweep.py; 16+ spills)
@@ -1253,6 +1259,92 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
                 if (b + 1 < nbt) issue(b + 1, xa);
                 combine_batch(b, xb);
                 if (++b >= nbt) break;
+            }
+        } else
+#endif
+#if FLAME_HNX
+        if (HL && !SYNC && kVPT == 1 && n_clients >= CU) {
+            T xf[CU][EPT];        // the next middle's first CU arrivals, loaded ahead
+            auto issue_first = [&](int m) {
+                const uint64_t* cp = crow + static_cast<int64_t>(m) * n_clients;
+#pragma unroll
+                for (int u = 0; u < CU; ++u)
+                    unpack<T, EPT>(ld_nt(reinterpret_cast<const char*>(cp[u]) + coff), xf[u]);
+            };
+            issue_first(0);
+#pragma unroll 1
+            for (int m0 = 0; m0 < n_mids; m0 += HB) {
+                const int nb = n_mids - m0 < HB ? n_mids - m0 : HB;
+#pragma unroll 1
+                for (int u = 0; u < nb; ++u) {
+                    const int m = m0 + u;
+                    const uint64_t* cp = crow + static_cast<int64_t>(m) * n_clients;
+                    const float* rr = mid_rates + static_cast<int64_t>(m) * n_clients;
+                    A acc[EPT];
+                    {   // init-first: acc = tmp(a_0), then + tmp(a_u) in arrival order
+                        const float r0 = rr[0];
+#pragma unroll
+                        for (int j = 0; j < EPT; ++j) acc[j] = X::tmp(xf[0][j], r0, 0.0);
+#pragma unroll
+                        for (int q = 1; q < CU; ++q) {
+                            const float r = rr[q];
+#pragma unroll
+                            for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(xf[q][j], r, 0.0));
+                        }
+                    }
+                    int i = CU;
+#pragma unroll 1
+                    for (; i + CU <= n_clients; i += CU) {
+                        T x[CU][EPT];
+#pragma unroll
+                        for (int q = 0; q < CU; ++q)
+                            unpack<T, EPT>(ld_nt(reinterpret_cast<const char*>(cp[i + q]) + coff), x[q]);
+#pragma unroll
+                        for (int q = 0; q < CU; ++q) {
+                            const float r = rr[i + q];
+#pragma unroll
+                            for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[q][j], r, 0.0));
+                        }
+                    }
+                    if (i < n_clients) {      // the remainder's loads go out together
+                        const int rem = n_clients - i;
+                        T x[CU][EPT];
+#pragma unroll
+                        for (int q = 0; q < CU; ++q)
+                            if (q < rem) unpack<T, EPT>(ld_nt(reinterpret_cast<const char*>(cp[i + q]) + coff), x[q]);
+#pragma unroll
+                        for (int q = 0; q < CU; ++q) {
+                            if (q >= rem) break;
+                            const float r = rr[i + q];
+#pragma unroll
+                            for (int j = 0; j < EPT; ++j) acc[j] = X::add(acc[j], X::tmp(x[q][j], r, 0.0));
+                        }
+                    }
+                    FLAME_HT(3 + 2 * m);
+                    // the middle's weights, then the next middle's first batch: both in flight
+                    // while this middle's epilogue waits for the weights
+                    const V16 wv = ld_v(mid_ptr(m));
+                    if (m + 1 < n_mids) issue_first(m + 1);
+                    T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+                    const float g = mid_goal[m], rt = top_rates[m];
+                    T w[EPT], d[EPT];
+                    unpack<T, EPT>(wv, w);
+#pragma unroll
+                    for (int j = 0; j < EPT; ++j) {
+                        S::op(w[j], X::st(acc[j]), g, static_cast<double>(g), &d[j]);
+                        const A t = X::tmp(d[j], rt, 0.0);
+                        top[0][j] = have_top ? X::add(top[0][j], t) : t;
+                    }
+                    held[u * kBlock + threadIdx.x] = pack<T, EPT>(w);
+                    if (dp) st_v(dp, pack<T, EPT>(d));
+                    have_top = true;
+                    FLAME_HT(4 + 2 * m);
+                }
+                if (!(flags & FLAME_HIER_MID_READONLY)) {
+#pragma unroll 1
+                    for (int u = 0; u < nb; ++u) st_pol<FLAME_HST>(mid_ptr(m0 + u), held[u * kBlock + threadIdx.x]);
+                }
+                FLAME_HT(3 + 2 * n_mids + m0 / HB);
             }
         } else
 #endif
