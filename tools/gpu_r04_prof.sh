@@ -33,6 +33,15 @@ if [ "${PART:-A}" = A ]; then
   prof fedavg agg_reduce flame_agg_reduce 1024 25000000 4 2 --steps 10 --warmup 3
   prof fedadam fedopt_kernel flame_fedopt_reduce_adapt 1024 25000000 4 8 --workload fedadam --steps 10 --warmup 3
   prof fedyogi fedopt_kernel flame_fedopt_reduce_adapt 1024 25000000 4 8 --workload fedyogi --steps 10 --warmup 3
+elif [ "${PART:-A}" = C ]; then
+  # the other shipped paths' bench lines (kernels unchanged this round; re-measured on this build)
+  step bench_c2 300 python bench.py --clients 256 --params 1000000 --steps 50 --warmup 5 --cpu-clients 0
+  step bench_eager 300 python bench.py --workload fedavg_eager --steps 10 --warmup 3 --cpu-clients 0
+  step bench_fedadam_eager 300 python bench.py --workload fedadam_eager --steps 5 --warmup 2
+  step bench_scaffold 400 python bench.py --workload scaffold --steps 10 --warmup 3 --cpu-clients 0
+  step bench_feddyn 400 python bench.py --workload feddyn --steps 8 --warmup 2
+  step bench_hier_fetched 400 python bench.py --workload hier_fedbuff --hier-middles fetched --steps 10 --warmup 3 --cpu-clients 0
+  step bench_hier_sync 400 python bench.py --workload hier_fedbuff --hier-mode sync --steps 10 --warmup 3 --cpu-clients 0
 else
   prof fedadagrad fedopt_kernel flame_fedopt_reduce_adapt 1024 25000000 4 8 --workload fedadagrad --steps 10 --warmup 3
   prof hier_fedbuff hier_fedbuff flame_hier_fedbuff 4096 15625000 2 131 --workload hier_fedbuff --steps 10 --warmup 3
