@@ -617,3 +617,17 @@ def test_shard_collective_failure_names_rank_and_wave():
     comm._works = [(1, W())]
     with pytest.raises(RuntimeError, match=r"rank 3 of 8 \(nccl\): wait on the all-gather of wave 1 failed"):
         comm.wait()
+
+
+def test_plan_carries_caller_segment_flags():
+    """A segment's caller flags (FLAME_SEG_CUR_IS_AVG: the eager caller's aliased FedOPT step)
+    land in the flags word next to the computed FLAME_SEG_UNALIGNED bit."""
+    from flame_amd import engine
+    from flame_amd import _native as N
+    segs = [engine.Seg(4096, out=4096, inp=4096, cur=0, cur_out=8192, m=12288, v=16384, clients=[20480],
+                       flags=N.FLAME_SEG_CUR_IS_AVG),
+            engine.Seg(4096, out=4096, inp=4096, cur=4100, cur_out=8192, m=12288, v=16384, clients=[20480])]
+    p = engine.plan(N.FLAME_F32, segs, [1.0])
+    head = p.meta[:2 * engine.SEG_WORDS].reshape(2, engine.SEG_WORDS)
+    assert int(head[0, 8]) == N.FLAME_SEG_CUR_IS_AVG                 # aligned, aliased
+    assert int(head[1, 8]) == N.FLAME_SEG_UNALIGNED                  # cur at 4100: not 16-byte aligned
