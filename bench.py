@@ -834,7 +834,7 @@ def verify_sharded(model: torch.Tensor, idx, expected) -> dict:
     import hashlib
     import torch.distributed as dist
     t = model.detach().contiguous().view(-1)
-    h = hashlib.blake2b(t.view(torch.uint8).cpu().numpy().tobytes(), digest_size=16).hexdigest()
+    h = hashlib.blake2b(t.view(torch.uint8).cpu().numpy(), digest_size=16).hexdigest()   # (no bytes copy)
     got = t[torch.as_tensor(idx, device=t.device)].cpu()
     if got.dtype == torch.bfloat16:
         gb = got.view(torch.int16).numpy().view(np.uint16)

@@ -5,8 +5,10 @@
 //   optimizer/fedavg.py:79-104, optimizer/fedbuff.py:89-97,122-157,
 //   optimizer/fedopt.py:102-129 (+ fedadam.py:33-35, fedyogi.py:34-36, fedadagrad.py:33-35).
 //
-// Design (DESIGN.md §3):
-//   * HBM-read bound (≈1 flop per byte): no MFMA, no LDS; every byte is read once.
+// Design (DESIGN.md §3, §4):
+//   * HBM-read bound (≈1 flop per byte): no MFMA; every byte is read once.  LDS only holds
+//     output blocks so their HBM writes go out as bursts (FedOPT, the hierarchy), or caps
+//     residency at 2 workgroups per CU for long launches (HBM streams fastest there).
 //   * One workgroup (256 lanes) owns one chunk of one segment; each lane owns
 //     16 contiguous bytes of every client's update (dwordx4, non-temporal), so
 //     every wave instruction is a 1 KiB fully-coalesced read.
@@ -19,6 +21,8 @@
 //     flight (memory-level parallelism); client pointers and rates are
 //     wave-uniform and come through the scalar cache.
 //   * Built with -ffp-contract=off and explicit __f*_rn ops: no FMA contraction.
+//   * Every host-side launch branch (which instantiation a launch takes) is counted
+//     (flame_launch_branch_count) and pinned by a GPU oracle test.
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
