@@ -43,8 +43,8 @@ def trace_avg(tag, sub):
 
 def main():
     traffic = json.load(open(os.path.join(P, "traffic.json")))["entries"]
-    print("| path | kernel (HIP events) | trace avg (same process) | ms / step | frac | PMC / algorithmic | files |")
-    print("|---|---|---|---|---|---|---|")
+    print("| path | kernel (HIP events) | trace avg (same process) | ms / step | frac | frac of the process's probe ceiling | PMC / algorithmic | files |")
+    print("|---|---|---|---|---|---|---|---|")
     for tag, label, sub, (kname, clients, wl) in PATHS:
         f = os.path.join(P, f"r04prof_prof_{tag}.log")
         if not os.path.exists(f):
@@ -55,9 +55,11 @@ def main():
         avg, calls = trace_avg(tag, sub)
         tr = [e for e in traffic if e.get("kernel") == kname and e.get("clients") == clients and e.get("workload") == wl]
         ratio = tr[-1]["traffic_over_algorithmic"] if tr else None
+        fc = rf.get("frac_of_measured_ceiling")
+        ceil = f"{fc:.3f} ({rf['measured_read_ceiling_GBps'] / 1e3:.2f} TB/s)" if fc else "--"
         print(f"| {label} | {kms:.3f} ms | {avg:.3f} ms x {calls} |" if avg else f"| {label} | {kms:.3f} ms | -- |",
-              f"{b['ms_per_step']:.3f} | {rf['frac']:.3f} | {ratio:.6f} |" if ratio else
-              f"{b['ms_per_step']:.3f} | {rf['frac']:.3f} | -- |",
+              f"{b['ms_per_step']:.3f} | {rf['frac']:.3f} | {ceil} |",
+              f"{ratio:.6f} |" if ratio else "-- |",
               f"`r04prof_prof_{tag}.log`, `r04prof_{tag}_kernel_stats.csv` |")
 
 
