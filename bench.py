@@ -1101,6 +1101,8 @@ def bench_fedbuff(args, world, rank, dev):
     rnd = 10
     opt = optimizer_provider.get("fedbuff", fuse_scale_add=args.fedbuff_fuse == "on")
     torch.cuda.synchronize()
+    from flame_amd import _native
+    br0 = _native.launch_branch_counts()
 
     def step():
         agg = None
@@ -1123,6 +1125,7 @@ def bench_fedbuff(args, world, rank, dev):
         kst = {nm: kernel_stats(events, nm) for nm in sorted({e[0] for e in events})}
         k_time = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         k_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kst.values()) / args.steps
+        br = {k: v - br0[k] for k, v in _native.launch_branch_counts().items() if v != br0[k]}
         print(json.dumps({
             "metric": "aggregated params/sec (device-resident), async FedBuff top aggregator round",
             "value": K * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -1133,7 +1136,7 @@ def bench_fedbuff(args, world, rank, dev):
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel_ms_per_step": k_time * 1e3,
                          "algorithmic_bytes_per_step": k_bytes, "traffic": traffic,
                          "bytes_per_client_param": k_bytes / (K * P * 4)},
-            "kernels": kst,
+            "kernels": kst, "launch_branches": br,
         }), flush=True)
 
 

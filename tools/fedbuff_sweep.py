@@ -39,6 +39,11 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--delta", action="store_true", help="scale_add_agg_weights_with_delta (a middle's upload)")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--stale", default="mod4", choices=["mod4", "synth"],
+                    help="synth = bench.py's staleness draw (synth.counts(seed + 5, K) % 4)")
+    ap.add_argument("--persistent-model", action="store_true",
+                    help="one model tensor updated in place every round, as bench.py's step does "
+                         "(default: a fresh clone of the start model per round)")
     a = ap.parse_args()
     from flame_amd import _native, engine
     from flame_amd.optimizers import optimizer_provider
@@ -62,7 +67,13 @@ def main():
     engine.synth_fill_(tmp, 5, 0, 0, 1.0)
     model0 = tmp.clone()
     del tmp
-    stale = [i % 4 for i in range(K)]
+    if a.stale == "synth":
+        from flame_amd import synth
+        stale = [int(x) % 4 for x in synth.counts(5, K)]
+    else:
+        stale = [i % 4 for i in range(K)]
+    persistent = {nm: {"model": model0.clone()} for nm in names} if a.persistent_model else None
+    before = {nm: _native.launch_branch_counts() for nm in names} if len(names) == 1 else None
     rnd = 10
     times = {nm: [] for nm in names}
     for r in range(a.rounds + 1):
@@ -70,7 +81,7 @@ def main():
         for nm in (names if r % 2 == 0 else names[::-1]):
             _native._lib = libs[nm]
             opt = optimizer_provider.get("fedbuff")
-            model = {"model": model0.clone()}
+            model = persistent[nm] if persistent else {"model": model0.clone()}
             agg = None
             for i in range(K):
                 c = Cache()
@@ -101,6 +112,10 @@ def main():
         print(f"{nm:10s} kernel median {med:.4f} ms  {gb / med * 1e3:.0f} GB/s  "
               f"({', '.join(f'{t:.3f}' for t in times[nm])})", flush=True)
     print("bitwise: model (and delta) equal across variants every round", flush=True)
+    if before is not None:
+        after = _native.launch_branch_counts()
+        print("launch branches:", {k: v - before[names[0]][k] for k, v in after.items() if v != before[names[0]][k]},
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -158,7 +158,8 @@ def build_variants(names):
 
 
 def load(name):
-    L = ctypes.CDLL(os.path.join(VDIR, f"lib_{name}.so"))
+    # a name with a "/" is a library path (e.g. build/diag/lib_prev.so)
+    L = ctypes.CDLL(os.path.join(ROOT, name) if "/" in name else os.path.join(VDIR, f"lib_{name}.so"))
     vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint
     L.flame_chunk_elems.restype = i64
     L.flame_chunk_elems.argtypes = [ctypes.c_int]
