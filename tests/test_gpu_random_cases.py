@@ -1,0 +1,267 @@
+"""Randomised differential cases: the drop-in optimizers on the GPU vs the oracle, on models and
+rounds drawn from a seeded generator -- the combinations the hand-written tests do not pin one by
+one.  Each case draws: the optimizer (FedAvg, FedBuff do-per-arrival + scale_add with or without
+the middle delta, FedAdam / FedYogi / FedAdaGrad over three rounds, and the eager callers: FedAvg
+with a running total per arrival, deferred or not, and FedOPT whose current aliases the base,
+eager_syncfl/top_aggregator.py:36-90), 1-4 keys whose dtypes and
+sizes mix (0, 1, chunk boundaries +-1, up to 300k elements; FedAvg adds int64 / int32 buffers),
+1-150 clients, and where the updates live (separate HBM tensors, tiled UpdateSlab slots, or views
+one element off their allocation's alignment).  FedAvg / FedBuff: every element bitwise
+(fedavg.py:89-104, fedbuff.py:89-157, including the None-start quirk when a first call carries
+several entries); FedOPT: the first round bitwise, the adaptive rounds within the SURVEY §8(c)
+contract (fedopt.py:102-129).
+"""
+import numpy as np
+import pytest
+import torch
+
+import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SORTS = ["fedavg", "fedbuff", "fedadam", "fedyogi", "fedadagrad", "fedavg_eager", "fedopt_eager"]
+N_CASES = 7 * 40
+FLOATS = [torch.float32, torch.bfloat16, torch.float16, torch.float64]
+INTS = [torch.int64, torch.int32]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native_loaded():
+    from flame_amd import _native
+    _native.lib()
+    assert torch.cuda.is_available()
+    torch.empty(1, device=DEV)
+
+
+def _oracle():
+    from oracle import oracle as O
+    return O
+
+
+def _draw_size(rng, dtype):
+    from flame_amd import engine
+    c = engine.chunk_elems(engine.dtype_code(dtype))
+    pick = rng.integers(0, 8)
+    return int([0, 1, 7, c - 1, c, c + 1, 2 * c + 3, rng.integers(1, 300_000)][pick])
+
+
+def _draw_case(i):
+    rng = np.random.default_rng(7_000 + i)
+    sort = SORTS[i % len(SORTS)]
+    n_keys = int(rng.integers(1, 5))
+    keys = []
+    for k in range(n_keys):
+        if sort in ("fedavg", "fedavg_eager"):
+            dt = FLOATS[rng.integers(0, 4)] if rng.random() < 0.8 else INTS[rng.integers(0, 2)]
+        elif sort == "fedbuff":
+            dt = FLOATS[rng.integers(0, 4)]
+        else:
+            dt = torch.float32
+        keys.append((f"k{k}", dt, _draw_size(rng, dt)))
+    placement = ["hbm", "slab", "views"][rng.integers(0, 3)]
+    if placement == "slab" and any(s == 0 for _, _, s in keys):
+        placement = "hbm"
+    if rng.random() < 0.1:          # now and then one big key (fewer clients)
+        dt = keys[0][1]
+        keys[0] = (keys[0][0], dt, int(rng.integers(1_000_000, 3_000_000)))
+    total_elems = max(1, sum(s for _, _, s in keys))
+    n = int(rng.integers(1, 151 if not sort.endswith("eager") else 40))
+    n = max(1, min(n, 6_000_000 // total_elems))
+    return rng, sort, keys, placement, n
+
+
+def _rand(g, shape, dtype, scale):
+    if dtype.is_floating_point:
+        return (torch.randn(shape, generator=g, dtype=torch.float64) * scale).to(dtype)
+    return torch.randint(-50, 50, shape, generator=g, dtype=dtype)
+
+
+class _Placer:
+    """Puts a client's update on the device the way the case says."""
+
+    def __init__(self, placement, keys, n):
+        from flame_amd.slab import UpdateSlab
+        self.placement = placement
+        self.slab = None
+        if placement == "slab":
+            tmpl = {k: torch.zeros(s, dtype=dt) for k, dt, s in keys}
+            self.slab = UpdateSlab(tmpl, capacity=n, device=DEV)
+
+    def put(self, w):
+        if self.placement == "slab":
+            return self.slab.put({k: v.to(DEV) for k, v in w.items()})
+        if self.placement == "views":
+            out = {}
+            for k, v in w.items():
+                buf = torch.empty(v.numel() + 1, dtype=v.dtype, device=DEV)
+                buf[1:].copy_(v.to(DEV))
+                out[k] = buf[1:]
+            return out
+        return {k: v.to(DEV) for k, v in w.items()}
+
+
+def _run_fedavg(rng, keys, placement, n, label):
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    base = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
+    ups = [{k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys} for _ in range(n)]
+    counts = [int(c) for c in rng.integers(1, 1000, n)]
+    total = sum(counts)
+    P = _Placer(placement, keys, n)
+    cache = S.SortedCache()
+    for i in range(n):
+        cache[f"{i:04d}"] = S.TR(P.put(ups[i]), counts[i])
+    out = optimizer_provider.get("fedavg").do(S.to_dev(base, DEV), cache, total=total)
+    exp = {k: v.clone() for k, v in base.items()}
+    for k in exp:
+        O.reduce_tensor(exp[k], [u[k] for u in ups], [c / total for c in counts])
+    S.assert_bitwise(label, out, exp)
+
+
+def _run_fedbuff(rng, keys, placement, n, label):
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    version = 20
+    P = _Placer(placement, keys, n)
+    amd, ora = optimizer_provider.get("fedbuff"), O.OracleFedBuff()
+    aa = ao = None
+    i = 0
+    while i < n:
+        m = int(min(n - i, rng.integers(1, 4)))        # entries in this do() call
+        ca, co = S.SortedCache(), S.SortedCache()
+        for j in range(m):
+            u = {k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys}
+            stale = int(rng.integers(0, 4))
+            count = int(rng.integers(1, 50))
+            ca[f"{i + j:04d}"] = S.TR(P.put(u), count, version - stale)
+            co[f"{i + j:04d}"] = S.TR(u, count, version - stale)
+        aa = amd.do(aa, ca, total=m, version=version)
+        ao = ora.do(ao, co, total=m, version=version)
+        i += m
+    goal = n
+    model = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
+    dev_model = S.to_dev(model, DEV)
+    want_delta = bool(rng.integers(0, 2))
+    exp_delta = {}
+    for k in model:
+        d = O.scale_add_tensor(model[k], ao[k], goal, want_delta=want_delta)
+        if want_delta:
+            exp_delta[k] = d
+    if want_delta:
+        _, got_delta = amd.scale_add_agg_weights_with_delta(dev_model, aa, goal)
+        S.assert_bitwise(label + "/delta", got_delta, exp_delta)
+    else:
+        amd.scale_add_agg_weights(dev_model, aa, goal)
+    S.assert_bitwise(label + "/model", dev_model, model)
+
+
+def _run_fedopt(rng, sort, keys, placement, n, label):
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    w0 = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
+    P = _Placer(placement, keys, 3 * n)      # three rounds of slots, however soon they return
+    amd, ora = optimizer_provider.get(sort), O.OracleFedOPT(sort)
+    wa, wo = S.to_dev(w0, DEV), {k: v.clone() for k, v in w0.items()}
+    for r in range(3):
+        ups = [{k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys} for _ in range(n)]
+        counts = [int(c) for c in rng.integers(1, 1000, n)]
+        ca, co = S.SortedCache(), S.SortedCache()
+        for i in range(n):
+            ca[f"{i:04d}"] = S.TR(P.put(ups[i]), counts[i])
+            co[f"{i:04d}"] = S.TR(ups[i], counts[i])
+        wa = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=sum(counts))
+        wo = ora.do({k: v.clone() for k, v in wo.items()}, co, total=sum(counts))
+        if r == 0:
+            S.assert_bitwise(f"{label}/r0", wa, wo)
+        else:
+            S.assert_close_fedopt(f"{label}/r{r}", S.to_cpu(wa), wo, elementwise=r == 1)
+        del ca
+
+
+def _run_fedavg_eager(rng, keys, placement, n, label):
+    """One do() per arrival with the running total (eager_syncfl/top_aggregator.py:36-90)."""
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    defer = bool(rng.integers(0, 2))
+    base = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
+    dev_base = S.to_dev(base, DEV)
+    P = _Placer(placement, keys, n)
+    amd, ora = optimizer_provider.get("fedavg", defer=defer), O.OracleFedAvg()
+    ca, co = S.SortedCache(), S.SortedCache()
+    total = 0
+    check_at = int(rng.integers(0, n))
+    for i in range(n):
+        u = {k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys}
+        c = int(rng.integers(1, 1000))
+        total += c
+        ca[f"{i:04d}"] = S.TR(P.put(u), c)
+        co[f"{i:04d}"] = S.TR(u, c)
+        out = amd.do(dev_base, ca, total=total, num_trainers=n)
+        ora.do(base, co, total=total)
+        if i == check_at or i == n - 1:
+            S.assert_bitwise(f"{label}/defer={defer}/after{i}", {k: v for k, v in S.to_cpu(out).items()}, base)
+
+
+def _run_fedopt_eager(rng, keys, placement, n, label):
+    """The eager top's FedOPT: per round base = deepcopy(weights), then do(base, cache,
+    total=running) per arrival -- current aliases base after the first call."""
+    from copy import deepcopy
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    sort = ["fedadam", "fedyogi", "fedadagrad"][rng.integers(0, 3)]
+    w0 = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
+    P = _Placer(placement, keys, 2 * n)
+    amd, ora = optimizer_provider.get(sort), O.OracleFedOPT(sort)
+    wa, wo = S.to_dev(w0, DEV), {k: v.clone() for k, v in w0.items()}
+    for r in range(2):
+        ba, bo = deepcopy(wa), deepcopy(wo)
+        ca, co = S.SortedCache(), S.SortedCache()
+        total = 0
+        for i in range(n):
+            u = {k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys}
+            c = int(rng.integers(1, 1000))
+            total += c
+            ca[f"r{r}e{i:04d}"] = S.TR(P.put(u), c)
+            co[f"r{r}e{i:04d}"] = S.TR(u, c)
+            oa = amd.do(ba, ca, total=total, num_trainers=n)
+            oo = ora.do(bo, co, total=total)
+        S.assert_close_fedopt(f"{label}/{sort}/r{r}", S.to_cpu(oa), oo, elementwise=r == 0)
+        wa, wo = oa, oo
+
+
+@pytest.mark.parametrize("case", range(N_CASES))
+def test_random_case_vs_oracle(case):
+    rng, sort, keys, placement, n = _draw_case(case)
+    label = (f"case {case}: {sort} {placement} n={n} keys=" +
+             ",".join(f"{k}:{str(dt).replace('torch.', '')}[{s}]" for k, dt, s in keys))
+    if sort == "fedavg":
+        _run_fedavg(rng, keys, placement, n, label)
+    elif sort == "fedavg_eager":
+        _run_fedavg_eager(rng, keys, placement, n, label)
+    elif sort == "fedopt_eager":
+        _run_fedopt_eager(rng, keys, placement, n, label)
+    elif sort == "fedbuff":
+        _run_fedbuff(rng, keys, placement, n, label)
+    else:
+        _run_fedopt(rng, sort, keys, placement, n, label)
+
+
+def test_random_cases_cover_every_draw():
+    """The seeded draw reaches every optimizer, placement, float dtype and a zero-size key."""
+    seen = set()
+    for i in range(N_CASES):
+        _, sort, keys, placement, n = _draw_case(i)
+        seen.add(sort)
+        seen.add(placement)
+        for _, dt, s in keys:
+            seen.add(dt)
+            if s == 0:
+                seen.add("empty")
+    for want in (*SORTS, "hbm", "slab", "views", "empty", *FLOATS):
+        assert want in seen, want
