@@ -265,3 +265,146 @@ def test_random_cases_cover_every_draw():
                 seen.add("empty")
     for want in (*SORTS, "hbm", "slab", "views", "empty", *FLOATS):
         assert want in seen, want
+
+
+# ---------------------------------------------------------------- co-located hierarchies
+N_HIER = 60
+HFLOATS = [torch.float32, torch.bfloat16, torch.float16]
+
+
+def _draw_hier(i):
+    rng = np.random.default_rng(9_000 + i)
+    mode = "async" if i % 2 == 0 else "sync"
+    keys = []
+    for k in range(int(rng.integers(1, 4))):
+        dt = HFLOATS[rng.integers(0, 3)]
+        keys.append((f"k{k}", dt, _draw_size(rng, dt)))
+    M = int(rng.integers(1, 25))
+    arrivals = [int(rng.integers(1, 7)) for _ in range(M)]        # ragged middles
+    per_elem = max(1, sum(s for _, _, s in keys))
+    while sum(arrivals) * per_elem > 4_000_000 and max(arrivals) > 1:
+        arrivals = [max(1, a // 2) for a in arrivals]
+    placement = ["slab", "tensors", "mixed"][rng.integers(0, 3)]
+    if any(s == 0 for _, _, s in keys):
+        placement = "tensors"
+    return rng, mode, keys, arrivals, placement
+
+
+def _run_hier_async(rng, keys, arrivals, placement, label):
+    from flame_amd.optimizer.fedbuff import hierarchy_round
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    M, rnd = len(arrivals), 12
+    mk = lambda scale: {k: _rand(g, (s,), dt, scale) for k, dt, s in keys}       # noqa: E731
+    ups = [[mk(1e-2) for _ in range(a)] for a in arrivals]
+    vers = [[rnd - int(rng.integers(0, 4)) for _ in range(a)] for a in arrivals]
+    mid0 = [mk(1.0) for _ in range(M)]
+    goals = [int(rng.integers(1, 9)) for _ in range(M)]
+    mid_ver = [rnd - int(rng.integers(0, 3)) for _ in range(M)]
+    top_start = bool(rng.integers(0, 2))
+    top_prev = mk(1e-3)
+    top_w0 = mk(1.0) if rng.integers(0, 2) else None
+    top_goal = int(rng.integers(1, 10))
+    with_delta = bool(rng.integers(0, 2))
+    update_mids = bool(rng.integers(0, 2))
+    slab = (UpdateSlab({k: torch.empty(s, dtype=dt) for k, dt, s in keys}, capacity=sum(arrivals), device=DEV)
+            if placement != "tensors" else None)
+    aggs = []
+    for m in range(M):
+        opt, agg = optimizer_provider.get("fedbuff"), None
+        for t in range(arrivals[m]):
+            w = S.to_dev(ups[m][t], DEV)
+            in_slab = slab is not None and (placement == "slab" or (m + t) % 2 == 0)
+            c = S.SortedCache()
+            c["a"] = S.TR(slab.put(w) if in_slab else w, 1, vers[m][t])
+            agg = opt.do(agg, c, total=1, version=rnd)
+        aggs.append(agg)
+    mids = [S.to_dev(w, DEV) for w in mid0]
+    tw = S.to_dev(top_w0, DEV) if top_w0 is not None else None
+    ta = S.to_dev(top_prev, DEV) if top_start else None
+    agg, deltas = hierarchy_round([(mids[m], aggs[m], goals[m], mid_ver[m]) for m in range(M)], ta, version=rnd,
+                                  top_weights=tw, top_goal=top_goal, with_delta=with_delta,
+                                  update_middle_weights=update_mids)
+    # oracle
+    oaggs = []
+    for m in range(M):
+        mo, ao = O.OracleFedBuff(), None
+        for t in range(arrivals[m]):
+            c = S.SortedCache()
+            c["a"] = S.TR({k: v.clone() for k, v in ups[m][t].items()}, 1, vers[m][t])
+            ao = mo.do(ao, c, total=1, version=rnd)
+        oaggs.append(ao)
+    omids = [{k: v.clone() for k, v in w.items()} for w in mid0]
+    otw = {k: v.clone() for k, v in top_w0.items()} if top_w0 is not None else None
+    oagg, odeltas = S.oracle_hierarchy_round(
+        [(omids[m], oaggs[m], goals[m], mid_ver[m]) for m in range(M)],
+        {k: v.clone() for k, v in top_prev.items()} if top_start else None, version=rnd, top_weights=otw,
+        top_goal=top_goal, with_delta=with_delta, update_middle_weights=update_mids)
+    label += f" top_start={top_start} top_w={top_w0 is not None} delta={with_delta} update={update_mids}"
+    S.assert_bitwise(label + "/top agg", S.to_cpu(dict(agg)), oagg)
+    for m in range(M):
+        S.assert_bitwise(f"{label}/mid{m}", S.to_cpu(mids[m]), omids[m])
+        if with_delta:
+            S.assert_bitwise(f"{label}/delta{m}", S.to_cpu(deltas[m]), odeltas[m])
+    if otw is not None:
+        S.assert_bitwise(label + "/top w", S.to_cpu(tw), otw)
+
+
+def _run_hier_sync(rng, keys, arrivals, placement, label):
+    from flame_amd.optimizer.sync_hierarchy import sync_hierarchy_round
+    from flame_amd.slab import UpdateSlab
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    M = len(arrivals)
+    mk = lambda scale: {k: _rand(g, (s,), dt, scale) for k, dt, s in keys}       # noqa: E731
+    ups = [[mk(1e-2) for _ in range(a)] for a in arrivals]
+    counts = [[int(rng.integers(1, 500)) for _ in range(a)] for a in arrivals]
+    mid0 = [mk(1.0) for _ in range(M)]
+    top0 = mk(1.0)
+    with_delta = bool(rng.integers(0, 2))
+    update_mids = bool(rng.integers(0, 2))
+    slab = (UpdateSlab({k: torch.empty(s, dtype=dt) for k, dt, s in keys}, capacity=sum(arrivals), device=DEV)
+            if placement != "tensors" else None)
+    mids, tops = [S.to_dev(w, DEV) for w in mid0], S.to_dev(top0, DEV)
+    middles, omiddles = [], []
+    omids = [{k: v.clone() for k, v in w.items()} for w in mid0]
+    for m in range(M):
+        c, oc = S.SortedCache(), S.SortedCache()
+        for t in range(arrivals[m]):
+            w = S.to_dev(ups[m][t], DEV)
+            in_slab = slab is not None and (placement == "slab" or (m + t) % 2 == 0)
+            c[f"e{t:03d}"] = S.TR(slab.put(w) if in_slab else w, counts[m][t])
+            oc[f"e{t:03d}"] = S.TR(ups[m][t], counts[m][t])
+        middles.append((mids[m], c, sum(counts[m])))
+        omiddles.append((omids[m], oc, sum(counts[m])))
+    _, deltas = sync_hierarchy_round(middles, tops, with_delta=with_delta, update_middle_weights=update_mids)
+    otop = {k: v.clone() for k, v in top0.items()}
+    _, odeltas = S.oracle_sync_hierarchy_round(omiddles, otop, with_delta=with_delta,
+                                               update_middle_weights=update_mids)
+    label += f" delta={with_delta} update={update_mids}"
+    S.assert_bitwise(label + "/top", S.to_cpu(tops), otop)
+    for m in range(M):
+        S.assert_bitwise(f"{label}/mid{m}", S.to_cpu(mids[m]), omids[m])
+        if with_delta:
+            S.assert_bitwise(f"{label}/delta{m}", S.to_cpu(deltas[m]), odeltas[m])
+
+
+@pytest.mark.parametrize("case", range(N_HIER))
+def test_random_hierarchy_vs_oracle(case, monkeypatch):
+    """The co-located hierarchies (flame_hier_fedbuff: async FedBuff middles + top, and the
+    synchronous FedAvg one) on drawn shapes: 1-24 middles with 1-6 arrivals each (ragged), mixed
+    key dtypes, slab / tensor / mixed arrivals, an existing or None top aggregate, top weights or
+    not, deltas or not, read-only or updated middles, the kernel-argument or the device-table
+    launch -- every output bitwise against the oracle's per-role op sequence."""
+    from flame_amd import engine
+    rng, mode, keys, arrivals, placement = _draw_hier(case)
+    if rng.integers(0, 2):
+        monkeypatch.setattr(engine, "ARGMETA", False)
+    label = (f"hier case {case}: {mode} {placement} M={len(arrivals)} arrivals={arrivals} "
+             f"argmeta={engine.ARGMETA} keys=" + ",".join(f"{k}:{str(dt).replace('torch.', '')}[{s}]"
+                                                            for k, dt, s in keys))
+    if mode == "async":
+        _run_hier_async(rng, keys, arrivals, placement, label)
+    else:
+        _run_hier_sync(rng, keys, arrivals, placement, label)
