@@ -408,3 +408,115 @@ def test_random_hierarchy_vs_oracle(case, monkeypatch):
         _run_hier_async(rng, keys, arrivals, placement, label)
     else:
         _run_hier_sync(rng, keys, arrivals, placement, label)
+
+
+# ---------------------------------------------------------------- FedDyn / SCAFFOLD
+N_STATEFUL = 30
+
+
+def _draw_model(rng, g):
+    keys = {}
+    for k in range(int(rng.integers(1, 5))):
+        dt = [torch.float32, torch.bfloat16, torch.float16, torch.float64][rng.integers(0, 4)]
+        keys[f"k{k}"] = _rand(g, (_draw_size(rng, dt) or 1,), dt, 1.0)
+    if rng.integers(0, 2):
+        keys["nbt"] = torch.tensor(int(rng.integers(0, 9)), dtype=torch.int64)
+    return keys
+
+
+def _update(g, tmpl, i, scale=1e-2):
+    return {k: _rand(g, v.shape, v.dtype, scale) if v.is_floating_point() else torch.tensor(i, dtype=v.dtype)
+            for k, v in tmpl.items()}
+
+
+def _run_feddyn(rng, label):
+    from flame_amd.optimizers import optimizer_provider
+    from flame_amd.slab import UpdateSlab
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    tmpl = _draw_model(rng, g)
+    per = sum(v.numel() for v in tmpl.values())
+    n_ends = int(max(2, min(rng.integers(2, 41), 3_000_000 // per)))
+    ends = [f"e{i:02d}" for i in range(n_ends)]
+    active = list(ends) if rng.integers(0, 2) else [ends[i] for i in rng.permutation(n_ends)]
+    history = ["rows", "pingpong", "pingpong_rows"][rng.integers(0, 3)]
+    alpha = float(rng.choice([0.01, 0.1, 0.5]))
+    placement = ["hbm", "slab"][rng.integers(0, 2)]
+    label += f" ends={n_ends} history={history} alpha={alpha} {placement} order={'cache' if active == ends else 'other'}"
+    slab = UpdateSlab(tmpl, capacity=2 * n_ends, device=DEV) if placement == "slab" else None
+    amd = optimizer_provider.get("feddyn", alpha=alpha, history=history)
+    ora = O.OracleFedDyn(alpha=alpha)
+    wa, wo = S.to_dev(tmpl, DEV), {k: v.clone() for k, v in tmpl.items()}
+    for r in range(int(rng.integers(2, 5))):
+        amd.save_state(S._PRE, active_ends=active)
+        ora.save_state(S._PRE, active_ends=active)
+        part = [e for e in ends if rng.random() < 0.7] or ends[:1]
+        if rng.random() < 0.2:
+            part = part + ["zz"]                     # an end the channel does not list
+        ca, co = S.SortedCache(), S.SortedCache()
+        counts = [int(rng.integers(1, 300)) for _ in part]
+        for i, (e, c) in enumerate(zip(part, counts)):
+            u = _update(g, tmpl, 10 * r + i)
+            du = S.to_dev(u, DEV)
+            ca[e] = S.TR(slab.put(du) if slab is not None else du, c)
+            co[e] = S.TR(u, c)
+        a = amd.do({k: v.clone() for k, v in wa.items()}, ca, total=sum(counts))
+        o = ora.do({k: v.clone() for k, v in wo.items()}, co, total=sum(counts))
+        S.assert_bitwise(f"{label}/r{r}/avg", S.to_cpu(a), o)
+        S.assert_bitwise(f"{label}/r{r}/cld", S.to_cpu(amd.cld_model), ora.cld_model)
+        wa, wo = amd.cld_model, ora.cld_model
+        del ca, co
+    for e, h in ora.local_param_dict.items():
+        if h is not None:
+            S.assert_bitwise(f"{label}/hist/{e}", S.to_cpu({k: amd.local_param_dict[e][k] for k in h}), h)
+
+
+def _run_scaffold(rng, label):
+    from flame_amd.optimizers import optimizer_provider
+    O = _oracle()
+    g = torch.Generator().manual_seed(int(rng.integers(1 << 31)))
+    tmpl = _draw_model(rng, g)
+    per = sum(v.numel() for v in tmpl.values())
+    n_ends = int(max(2, min(rng.integers(2, 41), 3_000_000 // per)))
+    ends = [f"t{i:02d}" for i in range(n_ends)]
+    sizes = {e: int(rng.integers(1, 1000)) for e in ends}
+    k = int(rng.integers(1, 6))
+    label += f" ends={n_ends} k={k}"
+    amd, ora = optimizer_provider.get("scaffold", k=k), O.OracleScaffold(k=k)
+    for o in (amd, ora):
+        o.save_state(S._PRE, dataset_sizes=sizes)
+    wa, wo = S.to_dev(tmpl, DEV), {kk: v.clone() for kk, v in tmpl.items()}
+    for r in range(int(rng.integers(2, 4))):
+        amd.save_state(S._PRE, glob_weights=wa)
+        ora.save_state(S._PRE, glob_weights=wo)
+        part = [e for e in ends if rng.random() < 0.6] or ends[:1]
+        ws = [_update(g, tmpl, r + i) for i in range(len(part))]
+        cs = [_update(g, tmpl, 0, 1e-3) for _ in part]
+        for i, c in enumerate(cs):
+            if "nbt" in c:
+                c["nbt"] = torch.tensor(1.25 * (i + 1) + r)     # an int buffer's control variate is fp32
+        ca, cca, co, cco = S.SortedCache(), S.SortedCache(), S.SortedCache(), S.SortedCache()
+        for e, w, c in zip(part, ws, cs):
+            ca[e] = S.TR(S.to_dev(w, DEV), sizes[e])
+            cca[e] = S.TR(S.to_dev(c, DEV))
+            co[e] = S.TR(w, sizes[e])
+            cco[e] = S.TR(c)
+        total = sum(sizes[e] for e in part)
+        wa = amd.do({kk: v.clone() for kk, v in wa.items()}, ca, total=total, control_cache=cca)
+        wo = ora.do({kk: v.clone() for kk, v in wo.items()}, co, total=total, control_cache=cco)
+        S.assert_bitwise(f"{label}/r{r}/out", S.to_cpu(wa), wo)
+        S.assert_bitwise(f"{label}/r{r}/c_glob", S.to_cpu(amd.c_glob), ora.c_glob)
+
+
+@pytest.mark.parametrize("case", range(N_STATEFUL))
+def test_random_stateful_vs_oracle(case):
+    """FedDyn (partial participation, ends leaving and returning, an unlisted end, the channel's
+    order equal to the cache's or not, in-place / ping-pong / ping-pong-rows histories, HBM or
+    slab updates; feddyn.py:70-139) and SCAFFOLD (random subsets, k, an int buffer with an fp32
+    control variate; scaffold.py:82-150) on drawn models, every output and state bitwise."""
+    rng = np.random.default_rng(11_000 + case)
+    label = f"stateful case {case}"
+    if case % 2 == 0:
+        _run_feddyn(rng, label + " feddyn")
+    else:
+        _run_scaffold(rng, label + " scaffold")
