@@ -97,7 +97,7 @@ def test_slab_write_one_launch_per_update():
     src = {k: v.to(DEV) for k, v in _model(g).items()}
     slab.put(src)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CUDA], acc_events=True) as prof:
         w = slab.put(src)
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
