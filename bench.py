@@ -78,7 +78,7 @@ def parse():
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "hier_fedbuff", "feddyn",
                              "scaffold", "fedavg_eager", "fedadam_eager", "fedyogi_eager", "fedadagrad_eager"])
     ap.add_argument("--eager-defer", default="on", choices=["on", "off"],
-                    help="fedavg_eager / --e2e-mode eager: FedAvg(defer=True) queues the one-arrival do() "
+                    help="fed*_eager / --e2e-mode eager: FedAvg / FedOPT(defer=True) queues the one-arrival do() "
                          "calls and reduces them in one launch (on) or launches per arrival (off)")
     ap.add_argument("--fedbuff-fuse", default="on", choices=["on", "off"],
                     help="fedbuff: scale_add straight from the queued arrivals (on) or flush + scale_add (off)")
@@ -509,7 +509,11 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes,
-                         "bytes_per_client_param": k_bytes / (n * P * 4)},
+                         "bytes_per_client_param": k_bytes / (n * P * 4),
+                         **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
+                                     "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
+                                     "among them): VALU-bound near its HBM time (DESIGN.md §4)"}
+                            if fedopt and defer else {})},
         }), flush=True)
 
 
@@ -518,10 +522,12 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     device-resident updates: base = deepcopy(weights), then one do() per arrival with the
     running total; the role keeps the returned object (read once, at the round's end).
     fedavg_eager: --eager-defer on: FedAvg(defer=True), one launch per round; off: one per
-    arrival.  fed{adam,yogi,adagrad}_eager: FedOPT.do per arrival, one fused
-    flame_fedopt_reduce_adapt launch each (FedAvg of the arrival + the adaptive step); the
-    first round -- untimed, reported apart -- holds the round-1 passthrough and the aliased
-    step (current_weights IS base: FLAME_SEG_CUR_IS_AVG)."""
+    arrival.  fed{adam,yogi,adagrad}_eager: FedOPT.do per arrival (FedAvg of the arrival + the
+    adaptive step); --eager-defer on: FedOPT(defer=True) queues the calls and runs the round as
+    ONE flame_fedopt_chain launch when the role reads the result; off: one fused
+    flame_fedopt_reduce_adapt launch per arrival.  The first round -- untimed, reported apart --
+    holds the round-1 passthrough and the aliased step (current_weights IS base:
+    FLAME_SEG_CUR_IS_AVG)."""
     from flame_amd import engine
     from flame_amd.optimizers import optimizer_provider
     if world > 1:
@@ -529,8 +535,8 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     defer = args.eager_defer == "on"
     sort = args.workload[:-len("_eager")]
     fedopt = sort != "fedavg"
-    opt = optimizer_provider.get(sort) if fedopt else optimizer_provider.get("fedavg", defer=defer)
-    kname = "flame_fedopt_reduce_adapt" if fedopt else "flame_agg_reduce"
+    opt = optimizer_provider.get(sort, defer=defer)
+    kname = ("flame_fedopt_chain" if defer else "flame_fedopt_reduce_adapt") if fedopt else "flame_agg_reduce"
     keys = [f"{i:05d}" for i in range(n)]
     state = {"weights": {"model": base}}
 
@@ -551,9 +557,10 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
         torch.cuda.synchronize()
         ev = [e for e in engine.kernel_events if e[0] == kname]
         engine.kernel_events = None
-        first = {"launches": len(ev), "aliased_step_kernel_ms": ev[0][1].elapsed_time(ev[0][2]) if ev else None,
+        first = {"launches": len(ev), "first_launch_kernel_ms": ev[0][1].elapsed_time(ev[0][2]) if ev else None,
                  "note": "arrival 1: FedAvg passthrough (flame_agg_reduce); arrival 2: current IS base, the "
-                         "fused step with FLAME_SEG_CUR_IS_AVG (its kernel time here); arrivals 3..n: fused"}
+                         "step with FLAME_SEG_CUR_IS_AVG; " + ("arrivals 2..n: one flame_fedopt_chain launch"
+                                                               if defer else "arrivals 3..n: fused, one launch each")}
     elapsed, events = timed(world, args.steps, args.warmup, step)
     ks = kernel_stats(events, kname)
     if rank == 0:
@@ -564,13 +571,17 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
             "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32", "settle": SETTLE,
             "config": {"workload": f"{args.workload}: {n} arrivals (one do() each, running total) x {P} fp32 "
-                                   f"params, {args.layout} layout" + ("" if fedopt else f", defer {args.eager_defer}")},
+                                   f"params, {args.layout} layout, defer {args.eager_defer}"},
             "first_round": first,
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes,
-                         "bytes_per_client_param": k_bytes / (n * P * 4)},
+                         "bytes_per_client_param": k_bytes / (n * P * 4),
+                         **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
+                                     "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
+                                     "among them): VALU-bound near its HBM time (DESIGN.md §4)"}
+                            if fedopt and defer else {})},
         }), flush=True)
 
 

@@ -36,7 +36,7 @@ FLAME_TILE_BYTES = 4096
 # every symbol include/flame_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
-    "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
+    "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedopt_chain", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
     "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
     "flame_slab_write", "flame_slab_write_2d",
@@ -79,6 +79,8 @@ def lib() -> ctypes.CDLL:
     L.flame_agg_argmeta_max_bytes.argtypes = []
     L.flame_fedopt_reduce_adapt.restype = ctypes.c_int
     L.flame_fedopt_reduce_adapt.argtypes = [ctypes.c_int, ctypes.c_int, u32, vp, i32, i64, vp, i32, vp] + [f32] * 6 + [vp]
+    L.flame_fedopt_chain.restype = ctypes.c_int
+    L.flame_fedopt_chain.argtypes = [ctypes.c_int, ctypes.c_int, u32, vp, i32, i64, vp, i32, vp, vp] + [f32] * 6 + [vp]
     L.flame_fedopt_reduce_adapt_argmeta.restype = ctypes.c_int
     L.flame_fedopt_reduce_adapt_argmeta.argtypes = [ctypes.c_int, ctypes.c_int, u32, vp, i64, i32, i64, i32, i64,
                                                     i64] + [f32] * 6 + [vp]

@@ -636,6 +636,116 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta me
                                     b1, omb1, b2, omb2, eta, tau, n_chunks);
 }
 
+// ---------------------------------------------------------------- eager FedOPT chain (fp32)
+// The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) calls do() once per
+// arrival: FedAvg of that arrival into the round's base (fedavg.py:93-104), then one adaptive
+// step from the optimizer's state (fedopt.py:102-129).  This kernel runs a queue of such calls in
+// one pass.  Per element, for each client i in arrival order:
+//   b = b + tmp(w_i, r_i)
+//   where client i closes a do() call (step_end[i] != 0): d = b - c, m / v / c updated as
+//   adapt_elem (c = b for the first step when the segment is flagged FLAME_SEG_CUR_IS_AVG:
+//   current_weights IS the base right after the round-1 passthrough).
+// Base, current, m and v are read once and base, m, v and the new current written once, instead
+// of every arrival's launch reading and writing all four.  Bitwise equal to those launches: the
+// values stay fp32 in registers between steps, as the per-arrival launches store and reload them.
+template <int VARIANT, int CU>
+__global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                              const uint64_t* __restrict__ clients, int n_clients,
+                                                              const float* __restrict__ r32,
+                                                              const uint8_t* __restrict__ step_end, unsigned flags,
+                                                              float b1, float omb1, float b2, float omb2, float eta,
+                                                              float tau) {
+    using X = Tr<FLAME_F32>;
+    constexpr int EPT = X::EPT;
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_segment sg = segs[s];
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<FLAME_F32>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    if (e0 >= sg.numel) return;
+    const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const int64_t coff = client_offset<FLAME_F32>(sg, chunk);
+    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
+    const int nv = vec ? EPT : static_cast<int>(sg.numel - e0 < EPT ? sg.numel - e0 : EPT);
+    bool aliased = (sg.flags & FLAME_SEG_CUR_IS_AVG) != 0;
+    const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
+    const float* bp = reinterpret_cast<const float*>(sg.in) + e0;
+    const float* curp = reinterpret_cast<const float*>(sg.cur) + e0;
+    float* mp = reinterpret_cast<float*>(sg.m) + e0;
+    float* vp = reinterpret_cast<float*>(sg.v) + e0;
+    auto load4 = [&](const float* p, float (&x)[EPT]) {
+        if (vec) {
+            unpack<float, EPT>(ld_v(p), x);
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) x[j] = j < nv ? ld1(p + j) : 0.f;
+        }
+    };
+    float b[EPT], c[EPT], m[EPT], v[EPT];
+    load4(bp, b);
+    if (!aliased) load4(curp, c);
+    if (zero_state) {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) m[j] = v[j] = 0.f;
+    } else {
+        load4(mp, m);
+        load4(vp, v);
+    }
+    auto load_client = [&](int i, float (&x)[EPT]) {
+        const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(cp[i]) + coff);
+        if (vec) {
+            unpack<float, EPT>(ld_nt(p), x);
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) x[j] = j < nv ? ld1(p + j) : 0.f;
+        }
+    };
+    auto arrive = [&](int i, const float (&x)[EPT]) {
+        const float r = r32[i];
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
+        if (step_end[i]) {     // uniform: one do() call ends here
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                float cn;
+                adapt_elem<FLAME_F32, VARIANT>(b[j], aliased ? b[j] : c[j], m[j], v[j], cn, b1, omb1, b2, omb2, eta,
+                                               tau);
+                c[j] = cn;
+            }
+            aliased = false;
+        }
+    };
+    int i = 0;
+    for (; i + CU <= n_clients; i += CU) {
+        float x[CU][EPT];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
+#pragma unroll
+        for (int u = 0; u < CU; ++u) arrive(i + u, x[u]);
+    }
+    for (; i < n_clients; ++i) {
+        float x[EPT];
+        load_client(i, x);
+        arrive(i, x);
+    }
+    if (aliased) {             // no step closed: current is still the base
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) c[j] = b[j];
+    }
+    float* outs[4] = {reinterpret_cast<float*>(sg.out) + e0, mp, vp, reinterpret_cast<float*>(sg.cur_out) + e0};
+    const float* vals[4] = {b, m, v, c};
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        if (vec) {
+            float t[EPT];
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) t[j] = vals[o][j];
+            st_v(outs[o], pack<float, EPT>(t));
+        } else {
+            for (int j = 0; j < nv; ++j) st1(outs[o] + j, vals[o][j]);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- FedBuff scale-add (+delta)
 template <int DT> struct SA;
 template <> struct SA<FLAME_F32> {
@@ -1201,7 +1311,8 @@ enum : int {
     BR_HIER_ARG_LO = 68,  // + dt: flame_hier_fedbuff_argmeta, one middle over a long launch
     BR_OPT_ARG_MULTI = 71,  // + variant: flame_fedopt_reduce_adapt_argmeta, fp32, kOptWGC chunks per workgroup
     BR_HIER_ARG_LDS = 74,   // + dt * 2 + sync: flame_hier_fedbuff_argmeta, LDS store groups
-    BR_COUNT = 80
+    BR_CHAIN = 80,          // + variant: flame_fedopt_chain, fp32
+    BR_COUNT = 83
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -1228,7 +1339,8 @@ const char* branch_name(int i) {
             else if (b < BR_HIER_ARG_LO) snprintf(n, z, "flame_agg_reduce_argmeta/lo/%s", dts[b - BR_AGG_ARG_LO]);
             else if (b < BR_OPT_ARG_MULTI) snprintf(n, z, "flame_hier_fedbuff_argmeta/lo/%s/fedbuff", dts[b - BR_HIER_ARG_LO]);
             else if (b < BR_HIER_ARG_LDS) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
-            else snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
+            else if (b < BR_CHAIN) snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
+            else snprintf(n, z, "flame_fedopt_chain/f32/%s", var[b - BR_CHAIN]);
         }
         return true;
     }();
@@ -1425,6 +1537,31 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
     }
 #undef FLAME_OPT_LAUNCH1
     return launched(multi ? BR_OPT_MULTI + variant : BR_OPT + dtype * 3 + variant, "flame_fedopt_reduce_adapt");
+}
+
+int flame_fedopt_chain(int dtype, int variant, unsigned flags, const flame_segment* segs, int32_t n_segs,
+                       int64_t n_chunks, const void* const* clients, int32_t n_clients, const float* rates32,
+                       const uint8_t* step_end, float b1, float omb1, float b2, float omb2, float eta, float tau,
+                       void* stream) {
+    int rc = validate(segs, n_segs, n_chunks, n_clients, clients);
+    if (rc) return rc;
+    if (n_clients < 1 || !rates32 || !step_end)
+        return set_err(FLAME_EINVAL, "flame_fedopt_chain: needs >= 1 client, a rate array and a step_end array");
+    if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_chain: unknown variant %d", variant);
+    if (flags & ~FLAME_OPT_STATE_ZERO) return set_err(FLAME_EINVAL, "flame_fedopt_chain: unknown flags 0x%x", flags);
+    if (dtype != FLAME_F32) return set_err(FLAME_ENOTSUP, "flame_fedopt_chain: dtype %d not supported (f32)", dtype);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    auto cl = reinterpret_cast<const uint64_t*>(clients);
+#define FLAME_CHAIN_LAUNCH(V)                                                                                     \
+    hipLaunchKernelGGL((fedopt_chain_kernel<V, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, \
+                       rates32, step_end, flags, b1, omb1, b2, omb2, eta, tau)
+    if (variant == FLAME_FEDADAM) FLAME_CHAIN_LAUNCH(FLAME_FEDADAM);
+    else if (variant == FLAME_FEDYOGI) FLAME_CHAIN_LAUNCH(FLAME_FEDYOGI);
+    else FLAME_CHAIN_LAUNCH(FLAME_FEDADAGRAD);
+#undef FLAME_CHAIN_LAUNCH
+    return launched(BR_CHAIN + variant, "flame_fedopt_chain");
 }
 
 int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, const void* host_meta,

@@ -20,9 +20,20 @@ FedAvg result (``self.agg_weights``); ``m_t``/``v_t`` persist across rounds on
 the device; each round returns a NEW OrderedDict of new tensors, like the
 reference.  ``d_t`` is not materialised by the fused path; it is computed
 lazily from ``agg_weights`` and the previous ``current_weights`` on access.
+
+``defer=True`` (opt-in, like ``FedAvg(defer=True)``) batches the EAGER caller
+(eager_syncfl/top_aggregator.py:36-90: one ``do()`` per arrival into the round's base):
+each eligible call (fp32 keys on the GPU) pops its cache entries, queues them and
+returns a :class:`DeferredCurrent`; the queue runs as ONE ``flame_fedopt_chain`` launch
+when anything reads the results (the returned mapping, ``current_weights``, ``m_t``,
+``v_t``, ``agg_weights``), bit-identical to a launch per call.  Until then the base dict
+lags, as ``FedAvg(defer=True)``'s does.  ``d_t`` is not kept across a deferred queue.
 """
+import collections.abc
+import copy
 import logging
 import os
+import weakref
 from abc import abstractmethod
 from collections import OrderedDict
 
@@ -61,8 +72,18 @@ class FedOPT(FedAvg):
     # with no clients) -- bit-identical; which is faster is measured in DESIGN.md §4
     split_launch = os.environ.get("FLAME_AMD_FEDOPT_SPLIT", "0") == "1"
 
-    def __init__(self, beta_1, beta_2, eta, tau):
+    # deferred eager queue bounds (as FedAvg(defer=True)'s)
+    max_chain_entries = 256
+    max_chain_bytes = 16 << 30
+
+    def __init__(self, beta_1, beta_2, eta, tau, defer: bool = False):
+        self._chain = None
+        self._current = None
+        self._m = None
+        self._v = None
+        self._agg = None
         super().__init__()
+        self.chain_defer = defer
         self.current_weights = None
         self._d_t = None
         self._prev_current = None
@@ -72,6 +93,47 @@ class FedOPT(FedAvg):
         self.beta_2 = beta_2
         self.eta = eta
         self.tau = tau
+
+    # state the reference keeps as attributes: a read runs whatever eager calls are queued
+    @property
+    def current_weights(self):
+        self._flush_chain()
+        return self._current
+
+    @current_weights.setter
+    def current_weights(self, value):
+        self._flush_chain()
+        self._current = value
+
+    @property
+    def m_t(self):
+        self._flush_chain()
+        return self._m
+
+    @m_t.setter
+    def m_t(self, value):
+        self._flush_chain()
+        self._m = value
+
+    @property
+    def v_t(self):
+        self._flush_chain()
+        return self._v
+
+    @v_t.setter
+    def v_t(self, value):
+        self._flush_chain()
+        self._v = value
+
+    @property
+    def agg_weights(self):
+        self._flush_chain()
+        return self._agg
+
+    @agg_weights.setter
+    def agg_weights(self, value):
+        self._flush_chain()
+        self._agg = value
 
     # d_t is an attribute in the reference; keep it readable (and assignable)
     @property
@@ -86,6 +148,13 @@ class FedOPT(FedAvg):
 
     def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         logger.debug("calling fedopt (flame_amd)")
+        if self.chain_defer and not kwargs.keys() & _SHARD_KWARGS:
+            popped = self._try_queue(base_weights, cache, total)
+            if isinstance(popped, DeferredCurrent):
+                return popped
+            if popped is not None:          # not eligible: the popped entries take the normal path
+                cache = _Replay(popped)
+        self._flush_chain()
         if self.current_weights is not None and base_weights is not None and len(cache) > 0 and total != 0:
             # flame_amd.shard passes its plan's waves (one launch per wave, its all-gather started
             # right behind it) and an allocator placing each key's new `current` straight into
@@ -187,6 +256,99 @@ class FedOPT(FedAvg):
             t.writeback()
         new_cur.update(zip(ks, outs))
 
+    # ------------------------------------------------------------------ deferred eager chain
+    def _try_queue(self, base_weights, cache, total):
+        """Queue an eager do() call if it can run on flame_fedopt_chain; returns the
+        DeferredCurrent, or the popped (key, TrainResult) pairs when the call is not eligible
+        (None if nothing was popped)."""
+        if self._current is None and self._chain is None:
+            return None                      # round 1: the passthrough, not an adaptive step
+        if base_weights is None or len(cache) == 0 or total == 0:
+            return None
+        if not _chain_tensors(base_weights):
+            return None
+        ch = self._chain
+        if ch is not None and (ch.base is not base_weights or ch.n_entries >= self.max_chain_entries
+                               or ch.nbytes >= self.max_chain_bytes):
+            self._flush_chain()
+            ch = None
+        popped = [(k, cache.pop(k)) for k in list(cache.iterkeys())]
+        keys = list(base_weights.keys())
+        shapes = {k: base_weights[k].shape for k in keys}
+        device = base_weights[keys[0]].device
+        for _, tres in popped:
+            w = tres.weights
+            # (slab slots are strided (tiles, T) views: their numel is checked by the launch)
+            if set(w.keys()) != set(keys) or not all(
+                    w[k].dtype == torch.float32 and w[k].device == device for k in keys):
+                self._flush_chain()
+                return popped
+        if ch is None:
+            cur = self._current
+            if cur is None or list(cur.keys()) != keys:
+                return popped
+            aliased = {}
+            for k in keys:
+                c, b = cur[k], base_weights[k]
+                if not (isinstance(c, torch.Tensor) and c.dtype == torch.float32 and c.shape == b.shape
+                        and c.device == device and c.is_contiguous()):
+                    return popped
+                aliased[k] = _same_storage(c, b)
+                if not aliased[k] and _overlaps(c, b):
+                    return popped
+            if self._m is not None and not all(
+                    k in self._m and k in self._v and self._m[k].dtype == torch.float32
+                    and self._v[k].dtype == torch.float32 and self._m[k].shape == shapes[k]
+                    and self._m[k].device == device and self._v[k].device == device
+                    and self._m[k].is_contiguous() and self._v[k].is_contiguous() for k in keys):
+                return popped
+            ch = self._chain = _Chain(base_weights, cur, aliased, self._m is None)
+        step = [(tres.weights, tres.count / total) for _, tres in popped]
+        ch.steps.append(step)
+        ch.n_entries += len(step)
+        ch.nbytes += len(step) * sum(base_weights[k].numel() * 4 for k in keys)
+        res = DeferredCurrent(self, ch, len(ch.steps) - 1, keys)
+        ch.results.append(weakref.ref(res))
+        return res
+
+    def _flush_chain(self):
+        """Run the queued eager calls (if any): one flame_fedopt_chain launch per stretch that
+        ends at a still-referenced DeferredCurrent (normally just the last one)."""
+        ch = self.__dict__.get("_chain")
+        if ch is None:
+            return
+        self._chain = None
+        last = len(ch.steps) - 1
+        cuts = sorted({i for i, r in enumerate(ch.results) if r() is not None} | {last})
+        cur, aliased, zero, start = ch.current, ch.aliased, ch.state_zero, 0
+        keys = list(ch.base.keys())
+        hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
+        for cut in cuts:
+            steps = ch.steps[start:cut + 1]
+            base = [ch.base[k] for k in keys]
+            if zero:
+                self._m = {k: torch.empty_like(ch.base[k]) for k in keys}
+                self._v = {k: torch.empty_like(ch.base[k]) for k in keys}
+            outs = [torch.empty_like(ch.base[k]) for k in keys]
+            ends = [j == len(st) - 1 for st in steps for j in range(len(st))]
+            engine.fedopt_chain_(self.variant, base, [None if aliased[k] else cur[k] for k in keys], outs,
+                                 [self._m[k] for k in keys], [self._v[k] for k in keys],
+                                 [[w[k] for st in steps for w, _ in st] for k in keys],
+                                 [r for st in steps for _, r in st], ends, hyper, zero,
+                                 [aliased[k] for k in keys])
+            new = OrderedDict(zip(keys, outs))
+            r = ch.results[cut]()
+            if r is not None:
+                r._value = new
+            cur, aliased, zero, start = new, {k: False for k in keys}, False, cut + 1
+        self._current = cur
+        self._agg = ch.base
+        self._prev_current = None      # d_t is not kept across a deferred queue
+        self._d_t = None
+        # the queued updates (slab slots among them) are released now, not when the last
+        # DeferredCurrent dies (the role keeps that one as its weights)
+        ch.steps, ch.current, ch.base = [], None, None
+
     def _adapt_generic(self, keys, average, current, state_zero):
         """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""
         out = {}
@@ -208,3 +370,84 @@ class FedOPT(FedAvg):
     @abstractmethod
     def _delta_v_tensor(self, v, d):
         """The subclass's _delta_v_pytorch for one key."""
+
+
+_SHARD_KWARGS = {"flame_amd_key_groups", "flame_amd_after_group", "flame_amd_out_alloc"}
+
+
+def _chain_tensors(weights) -> bool:
+    """A base dict flame_fedopt_chain can update in place: fp32, contiguous, one GPU."""
+    try:
+        ts = list(weights.values())
+    except AttributeError:
+        return False
+    if not ts or not all(isinstance(t, torch.Tensor) for t in ts):
+        return False
+    dev = ts[0].device
+    return dev.type == "cuda" and all(t.dtype == torch.float32 and t.is_contiguous() and t.device == dev for t in ts)
+
+
+class _Chain:
+    """Eager do() calls queued for one flame_fedopt_chain launch."""
+
+    def __init__(self, base, current, aliased, state_zero):
+        self.base = base                # the round's base dict (updated in place at the flush)
+        self.current = current          # current_weights when the queue started
+        self.aliased = aliased          # {key: current[key] IS base[key]} (right after the passthrough)
+        self.state_zero = state_zero    # m_t / v_t were None
+        self.steps = []                 # per do(): [(weights, rate), ...]
+        self.results = []               # weakrefs to each do()'s DeferredCurrent
+        self.n_entries = 0
+        self.nbytes = 0
+
+
+class _Replay:
+    """Popped cache entries handed back to the non-deferred path, in the same order."""
+
+    def __init__(self, popped):
+        self._items = list(popped)
+
+    def __len__(self):
+        return len(self._items)
+
+    def iterkeys(self):
+        return iter([k for k, _ in self._items])
+
+    def pop(self, key, default=None):
+        for i, (k, v) in enumerate(self._items):
+            if k == key:
+                del self._items[i]
+                return v
+        return default
+
+
+class DeferredCurrent(collections.abc.Mapping):
+    """The ``current_weights`` a deferred eager ``do()`` returns (the reference returns a new
+    OrderedDict per call): the queued calls up to and including this one run on first read."""
+
+    def __init__(self, owner, chain, step, keys):
+        self._owner, self._chain, self._step, self._keys = owner, chain, step, keys
+        self._value = None
+
+    def materialize(self):
+        if self._value is None:
+            self._owner._flush_chain()
+        return self._value
+
+    def __getitem__(self, k):
+        return self.materialize()[k]
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+    def __contains__(self, k):
+        return k in self._keys
+
+    def __deepcopy__(self, memo):
+        return copy.deepcopy(self.materialize(), memo)
+
+    def __reduce__(self):
+        return (OrderedDict, (list(self.materialize().items()),))

@@ -181,6 +181,23 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
                               float b2, float omb2, float eta, float tau, void *stream);
 
 /*
+ * Eager FedOPT chain (fp32): the eager top aggregator's per-arrival do() calls
+ * (eager_syncfl/top_aggregator.py:36-90, fedavg.py:93-104 then fedopt.py:102-129), queued and
+ * run in one pass.  Per element, for each client i in order: base = base + round(w_i * r_i);
+ * where step_end[i] != 0 (device array, one byte per client; client i closes a do() call) the
+ * adaptive step of flame_fedopt_reduce_adapt with avg = base and the running current (the
+ * first step of a segment flagged FLAME_SEG_CUR_IS_AVG takes cur = base).  Writes base to
+ * seg.out, m and v in place, the final current to seg.cur_out (seg.cur is read unless the
+ * segment is flagged).  FLAME_OPT_STATE_ZERO: m, v start as zeros and are not read.  Bitwise
+ * equal to one flame_fedopt_reduce_adapt launch per do() call.  Replaces, per round,
+ * optimizer/fedopt.py:80-90,102-129 as the eager role calls it.
+ */
+int flame_fedopt_chain(int dtype, int variant, unsigned flags, const flame_segment *segs, int32_t n_segs,
+                       int64_t n_chunks, const void *const *clients, int32_t n_clients,
+                       const float *rates32, const uint8_t *step_end, float b1, float omb1, float b2,
+                       float omb2, float eta, float tau, void *stream);
+
+/*
  * flame_fedopt_reduce_adapt with its metadata block (segments, then the [n_segs][n_clients]
  * client table at byte offset off_clients, then the fp32 rates at off_r32; at most
  * flame_agg_argmeta_max_bytes() bytes, host memory) passed as a kernel argument: no

@@ -1,0 +1,217 @@
+"""GPU: the eager FedOPT caller batched into one launch (``FedAdam/FedYogi/FedAdaGrad(defer=True)``).
+
+The eager top aggregator (eager_syncfl/top_aggregator.py:36-90) calls ``do()`` once per arrival
+on the round's base with the running total; each call FedAvg-s the arrival into the base and
+takes one adaptive step (fedopt.py:80-90,102-129).  The deferred drop-in queues the calls and
+runs them as ONE ``flame_fedopt_chain`` launch when a result is read.  Checked bitwise against
+the per-call drop-in (``defer=False``: one fused launch per call) on the same inputs -- base,
+every returned current, m_t and v_t -- against the oracle within the §8(c) contract, and
+against the reference-generated ``fedadam_eager.npz`` / ``fedyogi_eager.npz``.
+"""
+import copy
+import gc
+
+import numpy as np
+import pytest
+import torch
+
+import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SORTS = ["fedadam", "fedyogi", "fedadagrad"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native_loaded():
+    from flame_amd import _native
+    _native.lib()
+    assert torch.cuda.is_available()
+
+
+def _opt(sort, **kw):
+    from flame_amd.optimizers import optimizer_provider
+    return optimizer_provider.get(sort, **kw)
+
+
+def _shapes():
+    # a whole-chunk key, a ragged one (tail lanes), a scalar-sized one
+    return {"w": (3 * 1024,), "r": (4099,), "s": (1,)}
+
+
+def _rounds(seed, n_rounds, arrivals, multi=False):
+    g = torch.Generator().manual_seed(seed)
+    w0 = {k: torch.randn(s, generator=g) for k, s in _shapes().items()}
+    rounds = []
+    for _ in range(n_rounds):
+        calls = []
+        for _ in range(arrivals):
+            n_entries = int(torch.randint(1, 3, (1,), generator=g)) if multi else 1
+            calls.append([({k: torch.randn(s, generator=g) * 1e-2 for k, s in _shapes().items()},
+                           int(torch.randint(1, 500, (1,), generator=g))) for _ in range(n_entries)])
+        rounds.append(calls)
+    return w0, rounds
+
+
+def _run_eager(opt, w0, rounds, place, read_every=False):
+    """The eager role's calls; returns per round (base, returned current, m_t, v_t) on the CPU,
+    plus every per-call result when ``read_every``."""
+    weights = S.to_dev(w0, DEV)
+    out_rounds, per_call = [], []
+    for r, calls in enumerate(rounds):
+        base = copy.deepcopy(weights) if not isinstance(weights, dict) else {k: v.clone() for k, v in weights.items()}
+        cache = S.SortedCache()
+        total = 0
+        out = None
+        for i, call in enumerate(calls):
+            for j, (w, c) in enumerate(call):
+                total += c
+                cache[f"r{r}e{i:03d}.{j}"] = S.TR(place(w), c)
+            out = opt.do(base, cache, total=total, num_trainers=len(calls))
+            if read_every:
+                per_call.append(S.to_cpu(dict(out)))
+        weights = out
+        cur = S.to_cpu(dict(out))            # the read runs the queue; the base is final after it
+        out_rounds.append((S.to_cpu(base), cur, S.to_cpu(opt.m_t) if opt.m_t is not None else None,
+                           S.to_cpu(opt.v_t) if opt.v_t is not None else None))
+    return out_rounds, per_call
+
+
+def _placer(kind, n):
+    if kind == "slab":
+        from flame_amd.slab import UpdateSlab
+        slab = UpdateSlab({k: torch.zeros(s) for k, s in _shapes().items()}, capacity=n, device=DEV)
+        return lambda w: slab.put(S.to_dev(w, DEV))
+    return lambda w: S.to_dev(w, DEV)
+
+
+@pytest.mark.parametrize("sort", SORTS)
+@pytest.mark.parametrize("place", ["hbm", "slab"])
+@pytest.mark.parametrize("multi", [False, True])
+def test_chain_equals_per_call_launches(sort, place, multi):
+    """Three eager rounds of 9 calls (the first round starts with the passthrough, the second
+    call then finds current aliasing the base): deferred == one fused launch per call, bitwise,
+    for base, the returned current, m_t and v_t after every round."""
+    from flame_amd import engine
+    from flame_amd.optimizer.fedopt import DeferredCurrent
+    w0, rounds = _rounds({"fedadam": 1, "fedyogi": 2, "fedadagrad": 3}[sort] + 10 * multi, 3, 9, multi)
+    n_updates = sum(len(c) for calls in rounds for c in calls)
+    ref, _ = _run_eager(_opt(sort), w0, rounds, _placer(place, n_updates))
+    launches = []
+    engine._recorders.append(launches)
+    try:
+        opt = _opt(sort, defer=True)
+        got, _ = _run_eager(opt, w0, rounds, _placer(place, n_updates))
+    finally:
+        engine._recorders.remove(launches)
+    names = [ev[0] for ev in launches]
+    assert names.count("flame_fedopt_chain") == 3, names      # one launch per round (read once at its end)
+    assert "flame_fedopt_reduce_adapt" not in names
+    for r, (a, b) in enumerate(zip(got, ref)):
+        for lbl, x, y in zip(("base", "current", "m_t", "v_t"), a, b):
+            S.assert_bitwise(f"{sort}/{place}/multi={multi}/r{r}/{lbl}", x, y)
+    assert isinstance(opt.current_weights, dict) and not isinstance(opt.current_weights, DeferredCurrent)
+
+
+@pytest.mark.parametrize("sort", SORTS)
+def test_chain_vs_oracle(sort):
+    """The deferred eager rounds against the oracle's per-call op sequence: the FedAvg part
+    (base) bitwise, current / m_t / v_t within the §8(c) contract."""
+    from oracle import oracle as O
+    w0, rounds = _rounds(40 + len(sort), 2, 7)
+    got, _ = _run_eager(_opt(sort, defer=True), w0, rounds, _placer("hbm", 0))
+    ora = O.OracleFedOPT(sort)
+    weights = {k: v.clone() for k, v in w0.items()}
+    for r, calls in enumerate(rounds):
+        base = copy.deepcopy(weights)
+        cache = S.SortedCache()
+        total = 0
+        for i, call in enumerate(calls):
+            for j, (w, c) in enumerate(call):
+                total += c
+                cache[f"r{r}e{i:03d}.{j}"] = S.TR({k: v.clone() for k, v in w.items()}, c)
+            out = ora.do(base, cache, total=total)
+        weights = out
+        gb, gc_, gm, gv = got[r]
+        S.assert_bitwise(f"{sort}/r{r}/base", gb, base)
+        S.assert_close_fedopt(f"{sort}/r{r}/current", gc_, out, elementwise=r == 0)
+        S.assert_close_fedopt(f"{sort}/r{r}/m", gm, ora.m_t, elementwise=r == 0)
+
+
+@pytest.mark.parametrize("sort", SORTS)
+def test_chain_intermediate_results_keep_their_values(sort):
+    """Results held across later calls (the reference returns a new dict per call) read the
+    state after THEIR call: the queue is cut at every still-referenced result."""
+    w0, rounds = _rounds(7, 2, 6)
+    _, per_call_ref = _run_eager(_opt(sort), w0, rounds, _placer("hbm", 0), read_every=True)
+    opt = _opt(sort, defer=True)
+    weights = S.to_dev(w0, DEV)
+    held = []
+    for r, calls in enumerate(rounds):
+        base = {k: v.clone() for k, v in dict(weights).items()}
+        cache = S.SortedCache()
+        total = 0
+        for i, call in enumerate(calls):
+            for j, (w, c) in enumerate(call):
+                total += c
+                cache[f"r{r}e{i:03d}.{j}"] = S.TR(S.to_dev(w, DEV), c)
+            out = opt.do(base, cache, total=total)
+            held.append(out)                       # nothing read until the end of the round
+        weights = out
+    for i, (h, ref) in enumerate(zip(held, per_call_ref)):
+        if i == 0:     # the passthrough returns the base itself, which the later calls update (as in flame)
+            continue
+        S.assert_bitwise(f"{sort}/call{i}", S.to_cpu(dict(h)), ref)
+
+
+@pytest.mark.parametrize("name", S.FEDOPT_EAGER_FIXTURES)
+def test_chain_eager_fixtures(golden, name):
+    """The reference-generated eager fixtures through the deferred drop-in (read after every
+    call, as the fixture driver does): the §8(c) contract, as for the per-call path."""
+    res = S.run_fedopt_eager(golden(name), lambda sort, **kw: _opt(sort, defer=True, **kw), DEV)
+    S.check_fedopt_eager(res)
+
+
+def test_chain_falls_back_for_ineligible_calls():
+    """A bf16 key (the chain is fp32-only), a key subset and a host-resident base take the
+    per-call path; the results still equal defer=False's, bitwise."""
+    g = torch.Generator().manual_seed(5)
+    w0 = {"w": torch.randn(2048, generator=g), "h": torch.randn(999, generator=g).bfloat16()}
+    for sort in SORTS:
+        outs = []
+        for defer in (False, True):
+            opt = _opt(sort, defer=defer)
+            base = S.to_dev(w0, DEV)
+            cache = S.SortedCache()
+            total = 0
+            for i in range(4):
+                total += 3 + i
+                cache[f"e{i}"] = S.TR({k: (torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) * 1e-2)
+                                       .to(v.dtype).to(DEV) for k, v in w0.items()}, 3 + i)
+                out = opt.do(base, cache, total=total)
+            outs.append((S.to_cpu(dict(out)), S.to_cpu(base)))
+        S.assert_bitwise(f"{sort}/bf16 key: current", outs[1][0], outs[0][0])
+        S.assert_bitwise(f"{sort}/bf16 key: base", outs[1][1], outs[0][1])
+
+
+def test_chain_releases_slab_slots():
+    """Once the queue has run, its slab slots return, though the role keeps the last result."""
+    from flame_amd.slab import UpdateSlab
+    w0, rounds = _rounds(9, 1, 5)
+    slab = UpdateSlab({k: torch.zeros(s) for k, s in _shapes().items()}, capacity=5, device=DEV)
+    opt = _opt("fedadam", defer=True)
+    base = S.to_dev(w0, DEV)
+    cache = S.SortedCache()
+    total = 0
+    for i, call in enumerate(rounds[0]):
+        (w, c), = call
+        total += c
+        cache[f"e{i}"] = S.TR(slab.put(S.to_dev(w, DEV)), c)
+        out = opt.do(base, cache, total=total)
+    assert opt._chain is not None and opt._chain.n_entries == 4     # the passthrough ran at once
+    keep = dict(out)                   # the read runs the queue
+    gc.collect()
+    torch.cuda.synchronize()
+    assert len(slab._free) == 5, "slots must return after the queue ran"
+    assert keep["w"].is_cuda and np.isfinite(keep["w"].cpu().numpy()).all()
