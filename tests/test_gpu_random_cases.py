@@ -217,7 +217,10 @@ def _run_fedopt_eager(rng, keys, placement, n, label):
     sort = ["fedadam", "fedyogi", "fedadagrad"][rng.integers(0, 3)]
     w0 = {k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}
     P = _Placer(placement, keys, 2 * n)
-    amd, ora = optimizer_provider.get(sort), O.OracleFedOPT(sort)
+    # defer=True: the round's calls run as one flame_fedopt_chain launch when the result is read
+    defer = bool(g.initial_seed() % 2)
+    label += f" defer={defer}"
+    amd, ora = optimizer_provider.get(sort, defer=defer), O.OracleFedOPT(sort)
     wa, wo = S.to_dev(w0, DEV), {k: v.clone() for k, v in w0.items()}
     for r in range(2):
         ba, bo = deepcopy(wa), deepcopy(wo)
