@@ -508,7 +508,7 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
-                         "algorithmic_bytes_per_step": k_bytes,
+                         "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
                          "bytes_per_client_param": k_bytes / (n * P * 4),
                          **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
                                      "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
@@ -566,6 +566,13 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
+        traffic = None
+        try:
+            for tr in json.load(open(args.traffic))["entries"]:
+                if tr.get("kernel") == kname and tr.get("clients") == n and tr.get("params") == P:
+                    traffic = tr["hbm_bytes_per_launch"]
+        except Exception:  # noqa: BLE001
+            pass
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -576,7 +583,7 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
-                         "algorithmic_bytes_per_step": k_bytes,
+                         "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
                          "bytes_per_client_param": k_bytes / (n * P * 4),
                          **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
                                      "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
