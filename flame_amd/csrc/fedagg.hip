@@ -636,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta me
                                     b1, omb1, b2, omb2, eta, tau, n_chunks);
 }
 
-// ---------------------------------------------------------------- eager FedOPT chain (fp32)
+// ---------------------------------------------------------------- eager FedOPT chain
 // The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) calls do() once per
 // arrival: FedAvg of that arrival into the round's base (fedavg.py:93-104), then one adaptive
 // step from the optimizer's state (fedopt.py:102-129).  This kernel runs a queue of such calls in
@@ -646,60 +646,62 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta me
 //   adapt_elem (c = b for the first step when the segment is flagged FLAME_SEG_CUR_IS_AVG:
 //   current_weights IS the base right after the round-1 passthrough).
 // Base, current, m and v are read once and base, m, v and the new current written once, instead
-// of every arrival's launch reading and writing all four.  Bitwise equal to those launches: the
-// values stay fp32 in registers between steps, as the per-arrival launches store and reload them.
-template <int VARIANT, int CU>
+// of every arrival's launch reading and writing all four.  Bitwise equal to those launches: every
+// value held in registers between steps is already rounded to the dtype (each op rounds), so it
+// equals what the per-arrival launches store and reload.
+template <int DT, int VARIANT, int CU>
 __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                               const uint64_t* __restrict__ clients, int n_clients,
                                                               const float* __restrict__ r32,
                                                               const uint8_t* __restrict__ step_end, unsigned flags,
                                                               float b1, float omb1, float b2, float omb2, float eta,
                                                               float tau) {
-    using X = Tr<FLAME_F32>;
+    using X = Tr<DT>;
+    using T = typename X::T;
     constexpr int EPT = X::EPT;
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
-    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<FLAME_F32>() + static_cast<int64_t>(threadIdx.x) * EPT;
+    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
-    const int64_t coff = client_offset<FLAME_F32>(sg, chunk);
+    const int64_t coff = client_offset<DT>(sg, chunk);
     const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
     const int nv = vec ? EPT : static_cast<int>(sg.numel - e0 < EPT ? sg.numel - e0 : EPT);
     bool aliased = (sg.flags & FLAME_SEG_CUR_IS_AVG) != 0;
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
-    const float* bp = reinterpret_cast<const float*>(sg.in) + e0;
-    const float* curp = reinterpret_cast<const float*>(sg.cur) + e0;
-    float* mp = reinterpret_cast<float*>(sg.m) + e0;
-    float* vp = reinterpret_cast<float*>(sg.v) + e0;
-    auto load4 = [&](const float* p, float (&x)[EPT]) {
+    const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
+    const T* curp = reinterpret_cast<const T*>(sg.cur) + e0;
+    T* mp = reinterpret_cast<T*>(sg.m) + e0;
+    T* vp = reinterpret_cast<T*>(sg.v) + e0;
+    auto load_t = [&](const T* p, T (&x)[EPT], bool nt) {
         if (vec) {
-            unpack<float, EPT>(ld_v(p), x);
+            unpack<T, EPT>(nt ? ld_nt(p) : ld_v(p), x);
         } else {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) x[j] = j < nv ? ld1(p + j) : 0.f;
+            for (int j = 0; j < EPT; ++j) x[j] = j < nv ? ld1(p + j) : T(0);
         }
     };
+    auto load_f = [&](const T* p, float (&x)[EPT]) {
+        T t[EPT];
+        load_t(p, t, false);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) x[j] = X::ld(t[j]);
+    };
     float b[EPT], c[EPT], m[EPT], v[EPT];
-    load4(bp, b);
-    if (!aliased) load4(curp, c);
+    load_f(bp, b);
+    if (!aliased) load_f(curp, c);
     if (zero_state) {
 #pragma unroll
         for (int j = 0; j < EPT; ++j) m[j] = v[j] = 0.f;
     } else {
-        load4(mp, m);
-        load4(vp, v);
+        load_f(mp, m);
+        load_f(vp, v);
     }
-    auto load_client = [&](int i, float (&x)[EPT]) {
-        const float* p = reinterpret_cast<const float*>(reinterpret_cast<const char*>(cp[i]) + coff);
-        if (vec) {
-            unpack<float, EPT>(ld_nt(p), x);
-        } else {
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) x[j] = j < nv ? ld1(p + j) : 0.f;
-        }
+    auto load_client = [&](int i, T (&x)[EPT]) {
+        load_t(reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[i]) + coff), x, true);
     };
-    auto arrive = [&](int i, const float (&x)[EPT]) {
+    auto arrive = [&](int i, const T (&x)[EPT]) {
         const float r = r32[i];
 #pragma unroll
         for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
@@ -707,8 +709,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
 #pragma unroll
             for (int j = 0; j < EPT; ++j) {
                 float cn;
-                adapt_elem<FLAME_F32, VARIANT>(b[j], aliased ? b[j] : c[j], m[j], v[j], cn, b1, omb1, b2, omb2, eta,
-                                               tau);
+                adapt_elem<DT, VARIANT>(b[j], aliased ? b[j] : c[j], m[j], v[j], cn, b1, omb1, b2, omb2, eta, tau);
                 c[j] = cn;
             }
             aliased = false;
@@ -716,14 +717,14 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
     };
     int i = 0;
     for (; i + CU <= n_clients; i += CU) {
-        float x[CU][EPT];
+        T x[CU][EPT];
 #pragma unroll
         for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
 #pragma unroll
         for (int u = 0; u < CU; ++u) arrive(i + u, x[u]);
     }
     for (; i < n_clients; ++i) {
-        float x[EPT];
+        T x[EPT];
         load_client(i, x);
         arrive(i, x);
     }
@@ -731,17 +732,17 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
 #pragma unroll
         for (int j = 0; j < EPT; ++j) c[j] = b[j];
     }
-    float* outs[4] = {reinterpret_cast<float*>(sg.out) + e0, mp, vp, reinterpret_cast<float*>(sg.cur_out) + e0};
+    T* outs[4] = {reinterpret_cast<T*>(sg.out) + e0, mp, vp, reinterpret_cast<T*>(sg.cur_out) + e0};
     const float* vals[4] = {b, m, v, c};
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-        if (vec) {
-            float t[EPT];
+        T t[EPT];
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) t[j] = vals[o][j];
-            st_v(outs[o], pack<float, EPT>(t));
+        for (int j = 0; j < EPT; ++j) t[j] = X::st(vals[o][j]);
+        if (vec) {
+            st_v(outs[o], pack<T, EPT>(t));
         } else {
-            for (int j = 0; j < nv; ++j) st1(outs[o] + j, vals[o][j]);
+            for (int j = 0; j < nv; ++j) st1(outs[o] + j, t[j]);
         }
     }
 }
@@ -1311,8 +1312,8 @@ enum : int {
     BR_HIER_ARG_LO = 68,  // + dt: flame_hier_fedbuff_argmeta, one middle over a long launch
     BR_OPT_ARG_MULTI = 71,  // + variant: flame_fedopt_reduce_adapt_argmeta, fp32, kOptWGC chunks per workgroup
     BR_HIER_ARG_LDS = 74,   // + dt * 2 + sync: flame_hier_fedbuff_argmeta, LDS store groups
-    BR_CHAIN = 80,          // + variant: flame_fedopt_chain, fp32
-    BR_COUNT = 83
+    BR_CHAIN = 80,          // + dt * 3 + variant (f32, bf16, f16): flame_fedopt_chain
+    BR_COUNT = 89
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -1340,7 +1341,7 @@ const char* branch_name(int i) {
             else if (b < BR_OPT_ARG_MULTI) snprintf(n, z, "flame_hier_fedbuff_argmeta/lo/%s/fedbuff", dts[b - BR_HIER_ARG_LO]);
             else if (b < BR_HIER_ARG_LDS) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
             else if (b < BR_CHAIN) snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
-            else snprintf(n, z, "flame_fedopt_chain/f32/%s", var[b - BR_CHAIN]);
+            else snprintf(n, z, "flame_fedopt_chain/%s/%s", dts[(b - BR_CHAIN) / 3], var[(b - BR_CHAIN) % 3]);
         }
         return true;
     }();
@@ -1550,18 +1551,24 @@ int flame_fedopt_chain(int dtype, int variant, unsigned flags, const flame_segme
     if (variant < FLAME_FEDADAM || variant > FLAME_FEDADAGRAD)
         return set_err(FLAME_ENOTSUP, "flame_fedopt_chain: unknown variant %d", variant);
     if (flags & ~FLAME_OPT_STATE_ZERO) return set_err(FLAME_EINVAL, "flame_fedopt_chain: unknown flags 0x%x", flags);
-    if (dtype != FLAME_F32) return set_err(FLAME_ENOTSUP, "flame_fedopt_chain: dtype %d not supported (f32)", dtype);
+    if (dtype != FLAME_F32 && dtype != FLAME_BF16 && dtype != FLAME_F16)
+        return set_err(FLAME_ENOTSUP, "flame_fedopt_chain: dtype %d not supported (f32, bf16, f16)", dtype);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-#define FLAME_CHAIN_LAUNCH(V)                                                                                     \
-    hipLaunchKernelGGL((fedopt_chain_kernel<V, kClientUnroll>), grid, block, 0, st, segs, n_segs, cl, n_clients, \
-                       rates32, step_end, flags, b1, omb1, b2, omb2, eta, tau)
-    if (variant == FLAME_FEDADAM) FLAME_CHAIN_LAUNCH(FLAME_FEDADAM);
-    else if (variant == FLAME_FEDYOGI) FLAME_CHAIN_LAUNCH(FLAME_FEDYOGI);
-    else FLAME_CHAIN_LAUNCH(FLAME_FEDADAGRAD);
+#define FLAME_CHAIN_LAUNCH(DT, V, CUV)                                                                              \
+    hipLaunchKernelGGL((fedopt_chain_kernel<DT, V, CUV>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, \
+                       step_end, flags, b1, omb1, b2, omb2, eta, tau)
+#define FLAME_CHAIN_VARIANTS(DT, CUV)                                                  \
+    if (variant == FLAME_FEDADAM) FLAME_CHAIN_LAUNCH(DT, FLAME_FEDADAM, CUV);          \
+    else if (variant == FLAME_FEDYOGI) FLAME_CHAIN_LAUNCH(DT, FLAME_FEDYOGI, CUV);     \
+    else FLAME_CHAIN_LAUNCH(DT, FLAME_FEDADAGRAD, CUV);
+    if (dtype == FLAME_F32) { FLAME_CHAIN_VARIANTS(FLAME_F32, kClientUnroll) }
+    else if (dtype == FLAME_BF16) { FLAME_CHAIN_VARIANTS(FLAME_BF16, kClientUnroll16) }
+    else { FLAME_CHAIN_VARIANTS(FLAME_F16, kClientUnroll16) }
+#undef FLAME_CHAIN_VARIANTS
 #undef FLAME_CHAIN_LAUNCH
-    return launched(BR_CHAIN + variant, "flame_fedopt_chain");
+    return launched(BR_CHAIN + dtype * 3 + variant, "flame_fedopt_chain");
 }
 
 int flame_fedopt_reduce_adapt_argmeta(int dtype, int variant, unsigned flags, const void* host_meta,

@@ -522,9 +522,10 @@ def fedopt_chain_(variant: str, base: List[torch.Tensor], cur: List[Optional[tor
                   cur_out: List[torch.Tensor], m: List[torch.Tensor], v: List[torch.Tensor],
                   clients: List[List[torch.Tensor]], rates: Sequence[float], step_end: Sequence[bool], hyper,
                   state_zero: bool, first_aliased: Sequence[bool]) -> None:
-    """A queue of eager FedOPT do() calls in one pass (kernel: flame_fedopt_chain, fp32 only):
-    per element, for each client in order, FedAvg into ``base`` (in place) with its rate, and
-    after every client with ``step_end`` set, the adaptive step from the running current / m / v.
+    """A queue of eager FedOPT do() calls in one pass (kernel: flame_fedopt_chain), one launch
+    per dtype (fp32 / bf16 / fp16; every tensor of a segment shares its dtype): per element,
+    for each client in order, FedAvg into ``base`` (in place) with its rate, and after every
+    client with ``step_end`` set, the adaptive step from the running current / m / v.
     ``first_aliased[s]``: segment s's current IS its base at the first step (``cur[s]`` unread);
     ``cur_out`` receives the final current, ``m`` / ``v`` are updated in place."""
     if not base:
@@ -533,31 +534,41 @@ def fedopt_chain_(variant: str, base: List[torch.Tensor], cur: List[Optional[tor
     L = N.lib()
     if not step_end or not step_end[-1]:
         raise ValueError("fedopt_chain_: the last client must close a do() call")
-    segs, keep = [], []
-    p_alias = 0
+    ends_host = np.asarray([1 if e else 0 for e in step_end], dtype=np.uint8)
+    groups = collections.OrderedDict()
     for s_, b in enumerate(base):
-        alias = bool(first_aliased[s_])
-        for t in (b, cur_out[s_], m[s_], v[s_]) + (() if alias else (cur[s_],)):
-            assert t.dtype == torch.float32 and t.is_contiguous() and t.device == device
-        row, tstride = _client_row(clients[s_], b, device, keep)
-        segs.append(Seg(b.numel(), out=b.data_ptr(), inp=b.data_ptr(), cur=0 if alias else cur[s_].data_ptr(),
-                        cur_out=cur_out[s_].data_ptr(), m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row,
-                        tile_stride=tstride, flags=N.FLAME_SEG_CUR_IS_AVG if alias else 0))
-        p_alias += b.numel() if alias else 0
-    P = sum(sg.numel for sg in segs)
-    # clients + base + cur (+ m, v unless zero state) read once; base, m, v, cur_out written once
-    nbytes = 4 * (P * (len(rates) + 2 + (0 if state_zero else 2) + 4) - p_alias)
-    p = plan(N.FLAME_F32, segs, rates)
-    dm = _staging.upload(p.meta, device)
-    ends = _staging.upload(np.asarray([1 if e else 0 for e in step_end], dtype=np.uint8), device)
-    segp, clp, r32p, _ = _device_ptrs(dm, p)
-    with _timed("flame_fedopt_chain", device, nbytes):
-        N.check(L.flame_fedopt_chain(N.FLAME_F32, FEDOPT_VARIANT[variant],
-                                     N.FLAME_OPT_STATE_ZERO if state_zero else 0, segp, p.n_segs, p.n_chunks,
-                                     clp, p.n_clients, r32p, ends.data_ptr(), *[float(x) for x in hyper],
-                                     _stream_ptr(device)))
-    keep += [dm, ends]
-    _keepalive(keep, device)
+        groups.setdefault(dtype_code(b.dtype), []).append(s_)
+    for code, idx in groups.items():
+        if code not in (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16):
+            raise NotImplementedError(f"fedopt_chain_: dtype {base[idx[0]].dtype}")
+        segs, keep = [], []
+        p_alias = 0
+        for s_ in idx:
+            b = base[s_]
+            alias = bool(first_aliased[s_])
+            for t in (b, cur_out[s_], m[s_], v[s_]) + (() if alias else (cur[s_],)):
+                assert t.dtype == b.dtype and t.is_contiguous() and t.device == device
+            row, tstride = _client_row(clients[s_], b, device, keep)
+            segs.append(Seg(b.numel(), out=b.data_ptr(), inp=b.data_ptr(), cur=0 if alias else cur[s_].data_ptr(),
+                            cur_out=cur_out[s_].data_ptr(), m=m[s_].data_ptr(), v=v[s_].data_ptr(), clients=row,
+                            tile_stride=tstride, flags=N.FLAME_SEG_CUR_IS_AVG if alias else 0))
+            p_alias += b.numel() if alias else 0
+        P = sum(sg.numel for sg in segs)
+        # clients + base + cur (+ m, v unless zero state) read once; base, m, v, cur_out written once
+        nbytes = ITEMSIZE[code] * (P * (len(rates) + 2 + (0 if state_zero else 2) + 4) - p_alias)
+        h = list(hyper)
+        if code in (N.FLAME_BF16, N.FLAME_F16):  # torch-CPU rounds the scalar of `sqrt(v) + tau`
+            h[5] = float(torch.tensor(float(h[5]), dtype=base[idx[0]].dtype))
+        p = plan(code, segs, rates)
+        dm = _staging.upload(p.meta, device)
+        ends = _staging.upload(ends_host, device)
+        segp, clp, r32p, _ = _device_ptrs(dm, p)
+        with _timed("flame_fedopt_chain", device, nbytes):
+            N.check(L.flame_fedopt_chain(code, FEDOPT_VARIANT[variant], N.FLAME_OPT_STATE_ZERO if state_zero else 0,
+                                         segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, ends.data_ptr(),
+                                         *[float(x) for x in h], _stream_ptr(device)))
+        keep += [dm, ends]
+        _keepalive(keep, device)
 
 
 def fedopt_scalars(beta_1, beta_2, eta, tau):

@@ -23,7 +23,7 @@ lazily from ``agg_weights`` and the previous ``current_weights`` on access.
 
 ``defer=True`` (opt-in, like ``FedAvg(defer=True)``) batches the EAGER caller
 (eager_syncfl/top_aggregator.py:36-90: one ``do()`` per arrival into the round's base):
-each eligible call (fp32 keys on the GPU) pops its cache entries, queues them and
+each eligible call (fp32 / bf16 / fp16 keys on the GPU) pops its cache entries, queues them and
 returns a :class:`DeferredCurrent`; the queue runs as ONE ``flame_fedopt_chain`` launch
 when anything reads the results (the returned mapping, ``current_weights``, ``m_t``,
 ``v_t``, ``agg_weights``), bit-identical to a launch per call.  Until then the base dict
@@ -280,7 +280,7 @@ class FedOPT(FedAvg):
             w = tres.weights
             # (slab slots are strided (tiles, T) views: their numel is checked by the launch)
             if set(w.keys()) != set(keys) or not all(
-                    w[k].dtype == torch.float32 and w[k].device == device for k in keys):
+                    w[k].dtype == base_weights[k].dtype and w[k].device == device for k in keys):
                 self._flush_chain()
                 return popped
         if ch is None:
@@ -290,15 +290,15 @@ class FedOPT(FedAvg):
             aliased = {}
             for k in keys:
                 c, b = cur[k], base_weights[k]
-                if not (isinstance(c, torch.Tensor) and c.dtype == torch.float32 and c.shape == b.shape
+                if not (isinstance(c, torch.Tensor) and c.dtype == b.dtype and c.shape == b.shape
                         and c.device == device and c.is_contiguous()):
                     return popped
                 aliased[k] = _same_storage(c, b)
                 if not aliased[k] and _overlaps(c, b):
                     return popped
             if self._m is not None and not all(
-                    k in self._m and k in self._v and self._m[k].dtype == torch.float32
-                    and self._v[k].dtype == torch.float32 and self._m[k].shape == shapes[k]
+                    k in self._m and k in self._v and self._m[k].dtype == base_weights[k].dtype
+                    and self._v[k].dtype == base_weights[k].dtype and self._m[k].shape == shapes[k]
                     and self._m[k].device == device and self._v[k].device == device
                     and self._m[k].is_contiguous() and self._v[k].is_contiguous() for k in keys):
                 return popped
@@ -375,8 +375,11 @@ class FedOPT(FedAvg):
 _SHARD_KWARGS = {"flame_amd_key_groups", "flame_amd_after_group", "flame_amd_out_alloc"}
 
 
+_CHAIN_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
+
 def _chain_tensors(weights) -> bool:
-    """A base dict flame_fedopt_chain can update in place: fp32, contiguous, one GPU."""
+    """A base dict flame_fedopt_chain can update in place: fp32 / bf16 / fp16, contiguous, one GPU."""
     try:
         ts = list(weights.values())
     except AttributeError:
@@ -384,7 +387,7 @@ def _chain_tensors(weights) -> bool:
     if not ts or not all(isinstance(t, torch.Tensor) for t in ts):
         return False
     dev = ts[0].device
-    return dev.type == "cuda" and all(t.dtype == torch.float32 and t.is_contiguous() and t.device == dev for t in ts)
+    return dev.type == "cuda" and all(t.dtype in _CHAIN_DTYPES and t.is_contiguous() and t.device == dev for t in ts)
 
 
 class _Chain:

@@ -181,7 +181,8 @@ int flame_fedopt_reduce_adapt(int dtype, int variant, unsigned flags, const flam
                               float b2, float omb2, float eta, float tau, void *stream);
 
 /*
- * Eager FedOPT chain (fp32): the eager top aggregator's per-arrival do() calls
+ * Eager FedOPT chain (FLAME_F32, FLAME_BF16 or FLAME_F16; every tensor of a segment of that
+ * dtype, scalars as for flame_fedopt_reduce_adapt): the eager top aggregator's per-arrival do() calls
  * (eager_syncfl/top_aggregator.py:36-90, fedavg.py:93-104 then fedopt.py:102-129), queued and
  * run in one pass.  Per element, for each client i in order: base = base + round(w_i * r_i);
  * where step_end[i] != 0 (device array, one byte per client; client i closes a do() call) the

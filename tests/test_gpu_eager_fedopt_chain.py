@@ -40,15 +40,15 @@ def _shapes():
     return {"w": (3 * 1024,), "r": (4099,), "s": (1,)}
 
 
-def _rounds(seed, n_rounds, arrivals, multi=False):
+def _rounds(seed, n_rounds, arrivals, multi=False, dtype=torch.float32):
     g = torch.Generator().manual_seed(seed)
-    w0 = {k: torch.randn(s, generator=g) for k, s in _shapes().items()}
+    w0 = {k: torch.randn(s, generator=g).to(dtype) for k, s in _shapes().items()}
     rounds = []
     for _ in range(n_rounds):
         calls = []
         for _ in range(arrivals):
             n_entries = int(torch.randint(1, 3, (1,), generator=g)) if multi else 1
-            calls.append([({k: torch.randn(s, generator=g) * 1e-2 for k, s in _shapes().items()},
+            calls.append([({k: (torch.randn(s, generator=g) * 1e-2).to(dtype) for k, s in _shapes().items()},
                            int(torch.randint(1, 500, (1,), generator=g))) for _ in range(n_entries)])
         rounds.append(calls)
     return w0, rounds
@@ -78,31 +78,35 @@ def _run_eager(opt, w0, rounds, place, read_every=False):
     return out_rounds, per_call
 
 
-def _placer(kind, n):
+def _placer(kind, n, dtype=torch.float32):
     if kind == "slab":
         from flame_amd.slab import UpdateSlab
-        slab = UpdateSlab({k: torch.zeros(s) for k, s in _shapes().items()}, capacity=n, device=DEV)
+        slab = UpdateSlab({k: torch.zeros(s, dtype=dtype) for k, s in _shapes().items()}, capacity=n, device=DEV)
         return lambda w: slab.put(S.to_dev(w, DEV))
     return lambda w: S.to_dev(w, DEV)
 
 
+CASES = ([(t, p, m) for t in (torch.float32,) for p in ("hbm", "slab") for m in (False, True)]
+         + [(t, p, False) for t in (torch.bfloat16, torch.float16) for p in ("hbm", "slab")])
+
+
 @pytest.mark.parametrize("sort", SORTS)
-@pytest.mark.parametrize("place", ["hbm", "slab"])
-@pytest.mark.parametrize("multi", [False, True])
-def test_chain_equals_per_call_launches(sort, place, multi):
+@pytest.mark.parametrize("dtype,place,multi", CASES, ids=[f"{str(t)[6:]}-{p}-{m}" for t, p, m in CASES])
+def test_chain_equals_per_call_launches(sort, dtype, place, multi):
     """Three eager rounds of 9 calls (the first round starts with the passthrough, the second
     call then finds current aliasing the base): deferred == one fused launch per call, bitwise,
-    for base, the returned current, m_t and v_t after every round."""
+    for base, the returned current, m_t and v_t after every round; fp32, bf16 and fp16 models
+    (every op rounded in the dtype, as the per-call kernel does)."""
     from flame_amd import engine
     from flame_amd.optimizer.fedopt import DeferredCurrent
-    w0, rounds = _rounds({"fedadam": 1, "fedyogi": 2, "fedadagrad": 3}[sort] + 10 * multi, 3, 9, multi)
+    w0, rounds = _rounds({"fedadam": 1, "fedyogi": 2, "fedadagrad": 3}[sort] + 10 * multi, 3, 9, multi, dtype)
     n_updates = sum(len(c) for calls in rounds for c in calls)
-    ref, _ = _run_eager(_opt(sort), w0, rounds, _placer(place, n_updates))
+    ref, _ = _run_eager(_opt(sort), w0, rounds, _placer(place, n_updates, dtype))
     launches = []
     engine._recorders.append(launches)
     try:
         opt = _opt(sort, defer=True)
-        got, _ = _run_eager(opt, w0, rounds, _placer(place, n_updates))
+        got, _ = _run_eager(opt, w0, rounds, _placer(place, n_updates, dtype))
     finally:
         engine._recorders.remove(launches)
     names = [ev[0] for ev in launches]
@@ -110,7 +114,7 @@ def test_chain_equals_per_call_launches(sort, place, multi):
     assert "flame_fedopt_reduce_adapt" not in names
     for r, (a, b) in enumerate(zip(got, ref)):
         for lbl, x, y in zip(("base", "current", "m_t", "v_t"), a, b):
-            S.assert_bitwise(f"{sort}/{place}/multi={multi}/r{r}/{lbl}", x, y)
+            S.assert_bitwise(f"{sort}/{dtype}/{place}/multi={multi}/r{r}/{lbl}", x, y)
     assert isinstance(opt.current_weights, dict) and not isinstance(opt.current_weights, DeferredCurrent)
 
 
@@ -174,10 +178,12 @@ def test_chain_eager_fixtures(golden, name):
 
 
 def test_chain_falls_back_for_ineligible_calls():
-    """A bf16 key (the chain is fp32-only), a key subset and a host-resident base take the
-    per-call path; the results still equal defer=False's, bitwise."""
+    """An int64 buffer in the model (the reference promotes it in the adaptive step, so it takes
+    the op sequence) keeps every call of the round on the per-call path; the results still equal
+    defer=False's, bitwise."""
     g = torch.Generator().manual_seed(5)
-    w0 = {"w": torch.randn(2048, generator=g), "h": torch.randn(999, generator=g).bfloat16()}
+    w0 = {"w": torch.randn(2048, generator=g), "h": torch.randn(999, generator=g).bfloat16(),
+          "n": torch.tensor(3, dtype=torch.int64)}
     for sort in SORTS:
         outs = []
         for defer in (False, True):
@@ -187,12 +193,13 @@ def test_chain_falls_back_for_ineligible_calls():
             total = 0
             for i in range(4):
                 total += 3 + i
-                cache[f"e{i}"] = S.TR({k: (torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) * 1e-2)
-                                       .to(v.dtype).to(DEV) for k, v in w0.items()}, 3 + i)
+                cache[f"e{i}"] = S.TR({k: ((torch.randn(v.shape, generator=torch.Generator().manual_seed(i)) * 1e-2)
+                                           .to(v.dtype) if v.is_floating_point() else torch.tensor(i + 1)).to(DEV)
+                                       for k, v in w0.items()}, 3 + i)
                 out = opt.do(base, cache, total=total)
             outs.append((S.to_cpu(dict(out)), S.to_cpu(base)))
-        S.assert_bitwise(f"{sort}/bf16 key: current", outs[1][0], outs[0][0])
-        S.assert_bitwise(f"{sort}/bf16 key: base", outs[1][1], outs[0][1])
+        S.assert_bitwise(f"{sort}/int64 key: current", outs[1][0], outs[0][0])
+        S.assert_bitwise(f"{sort}/int64 key: base", outs[1][1], outs[0][1])
 
 
 def test_chain_releases_slab_slots():
