@@ -49,6 +49,22 @@ int main(void) {
                FLAME_EINVAL, "");
     EXPECT_ERR(flame_fedopt_reduce_adapt(4, 0, 0, NULL, 0, 1, NULL, 0, NULL, 0, 0, 0, 0, 0, 0, NULL),
                FLAME_EINVAL, "");
+    {   /* eager FedOPT chain: table, step_end, variant, flags and dtype checks before any HIP call */
+        const float r = 0.5f;
+        const uint8_t e = 1;
+        EXPECT_ERR(flame_fedopt_chain(0, 0, 0, NULL, 0, 1, NULL, 1, &r, &e, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_EINVAL, "");
+        EXPECT_ERR(flame_fedopt_chain(0, 0, 0, fake, 1, 1, fake, 1, &r, NULL, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_EINVAL, "step_end");
+        EXPECT_ERR(flame_fedopt_chain(0, 0, 0, fake, 1, 1, fake, 0, &r, &e, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_EINVAL, "client");
+        EXPECT_ERR(flame_fedopt_chain(0, 7, 0, fake, 1, 1, fake, 1, &r, &e, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_ENOTSUP, "variant");
+        EXPECT_ERR(flame_fedopt_chain(0, 0, 2, fake, 1, 1, fake, 1, &r, &e, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_EINVAL, "unknown flags");
+        EXPECT_ERR(flame_fedopt_chain(FLAME_F64, 0, 0, fake, 1, 1, fake, 1, &r, &e, 0, 0, 0, 0, 0, 0, NULL),
+                   FLAME_ENOTSUP, "dtype");
+    }
     EXPECT_ERR(flame_host_register(NULL, 0), FLAME_EINVAL, "");
     EXPECT_ERR(flame_host_unregister(NULL), FLAME_EINVAL, "");
     EXPECT_ERR(flame_host_device_pointer(NULL, NULL), FLAME_EINVAL, "");
