@@ -631,3 +631,108 @@ def test_plan_carries_caller_segment_flags():
     head = p.meta[:2 * engine.SEG_WORDS].reshape(2, engine.SEG_WORDS)
     assert int(head[0, 8]) == N.FLAME_SEG_CUR_IS_AVG                 # aligned, aliased
     assert int(head[1, 8]) == N.FLAME_SEG_UNALIGNED                  # cur at 4100: not 16-byte aligned
+
+
+def _fake_chain_kernels(monkeypatch):
+    """CPU stand-ins for the FedAvg reduction and flame_fedopt_chain, written with the oracle's
+    C restatement, so FedOPT(defer=True)'s queue logic runs without a GPU."""
+    from oracle import oracle as O
+    from flame_amd.optimizer import fedopt as FO
+
+    def accumulate(base, entries, **kw):
+        for k in base:
+            ws = [(w[k], r) for w, r in entries if k in w]
+            O.reduce_tensor(base[k], [w for w, _ in ws], [r for _, r in ws])
+        for gi in range(len(kw.get("key_groups") or ())):
+            kw["after_group"](gi)
+
+    launches = []
+
+    def chain(variant, base, cur, cur_out, m, v, clients, rates, step_end, hyper, state_zero, first_aliased):
+        launches.append((len(rates), sum(step_end)))
+        for s in range(len(base)):
+            b, alias = base[s], first_aliased[s]
+            c = None if alias else cur[s].clone()
+            if state_zero:
+                m[s].zero_()
+                v[s].zero_()
+            for i, r in enumerate(rates):
+                O.reduce_tensor(b, [clients[s][i]], [r])
+                if step_end[i]:
+                    c = O.adapt_tensor(variant, b, b.clone() if alias else c, m[s], v[s], hyper)
+                    alias = False
+            cur_out[s].copy_(b if alias else c)
+
+    monkeypatch.setattr(FO.engine, "accumulate", accumulate)
+    monkeypatch.setattr(FO.engine, "fedopt_chain_", chain)
+    monkeypatch.setattr(FO, "_chain_tensors", lambda w: all(t.dtype == torch.float32 for t in w.values()))
+    return launches
+
+
+@pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
+def test_fedopt_defer_queue_logic(monkeypatch, sort):
+    """FedOPT(defer=True)'s host side against the oracle's per-call sequence, bitwise, with the
+    kernels swapped for CPU stand-ins (the GPU tests check the kernels): the passthrough runs at
+    once, the round's calls queue and run at the first read, a new base lands the queue, a result
+    held across later calls keeps ITS values (the queue is cut there), m_t / v_t reads run it."""
+    from oracle import oracle as O
+    from flame_amd.optimizer.fedopt import DeferredCurrent
+    from flame_amd.optimizers import optimizer_provider
+    launches = _fake_chain_kernels(monkeypatch)
+    g = torch.Generator().manual_seed(3)
+    w0 = {"a": torch.randn(37, generator=g), "b": torch.randn(5, generator=g)}
+    ups = [[({k: torch.randn(v.shape, generator=g) * 1e-2 for k, v in w0.items()}, 1 + 7 * i) for i in range(5)]
+           for _ in range(2)]
+    amd, ora = optimizer_provider.get(sort, defer=True), O.OracleFedOPT(sort)
+    wa, wo = {k: v.clone() for k, v in w0.items()}, {k: v.clone() for k, v in w0.items()}
+    held_a, held_o = [], []
+    for r, calls in enumerate(ups):
+        ba, bo = {k: v.clone() for k, v in dict(wa).items()}, {k: v.clone() for k, v in dict(wo).items()}
+        total = 0
+        for i, (w, c) in enumerate(calls):
+            total += c
+            ca, co = S.SortedCache(), S.SortedCache()
+            ca[f"e{i}"] = S.TR({k: v.clone() for k, v in w.items()}, c)
+            co[f"e{i}"] = S.TR({k: v.clone() for k, v in w.items()}, c)
+            oa, oo = amd.do(ba, ca, total=total), ora.do(bo, co, total=total)
+            assert len(ca) == 0, "a queued call pops its cache as the reference does"
+            if r == 0 and i == 0:
+                assert oa is ba and not launches          # the passthrough: the base itself, at once
+            else:
+                assert isinstance(oa, DeferredCurrent)
+            if i == 2:
+                held_a.append(oa)
+                held_o.append({k: v.clone() for k, v in oo.items()})
+        n_before = len(launches)
+        S.assert_bitwise(f"{sort}/r{r}/current", {k: oa[k] for k in oa}, oo)   # the read runs the queue
+        S.assert_bitwise(f"{sort}/r{r}/base", ba, bo)
+        S.assert_bitwise(f"{sort}/r{r}/m", amd.m_t, ora.m_t)
+        S.assert_bitwise(f"{sort}/r{r}/v", amd.v_t, ora.v_t)
+        # one stand-in launch per stretch: cut after the held call (i = 2) and at the end
+        assert [n for n, _ in launches[n_before:]] == ([2, 2] if r == 0 else [3, 2]), launches
+        wa, wo = oa, oo
+    for j, (h, ref) in enumerate(zip(held_a, held_o)):
+        S.assert_bitwise(f"{sort}/held{j}", {k: h[k] for k in h}, ref)
+
+
+def test_fedopt_defer_replays_ineligible_calls(monkeypatch):
+    """A call the chain cannot take (a key subset) lands the queue and goes through the per-call
+    path with the entries it popped: the per-call path sees them in the same order."""
+    from flame_amd.optimizer import fedopt as FO
+    from flame_amd.optimizers import optimizer_provider
+    _fake_chain_kernels(monkeypatch)
+    seen = []
+    monkeypatch.setattr(FO.FedOPT, "_do_fused",
+                        lambda self, base, cache, total, *a: seen.append(list(cache.iterkeys())) or {"x": 1})
+    opt = optimizer_provider.get("fedadam", defer=True)
+    base = {"a": torch.zeros(4), "b": torch.zeros(2)}
+    c = S.SortedCache()
+    c["x0"] = S.TR({"a": torch.ones(4), "b": torch.ones(2)}, 1)
+    assert opt.do(base, c, total=1) is base                      # passthrough
+    c["x1"] = S.TR({"a": torch.ones(4), "b": torch.ones(2)}, 1)
+    out = opt.do(base, c, total=2)
+    assert opt._chain is not None and opt._chain.n_entries == 1
+    c["x2"] = S.TR({"a": torch.ones(4)}, 1)                      # a key subset: not for the chain
+    c["x3"] = S.TR({"a": torch.ones(4)}, 2)
+    assert opt.do(base, c, total=5) == {"x": 1}
+    assert opt._chain is None and seen == [["x2", "x3"]] and out._value is not None
