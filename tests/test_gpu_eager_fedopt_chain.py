@@ -222,3 +222,47 @@ def test_chain_releases_slab_slots():
     torch.cuda.synchronize()
     assert len(slab._free) == 5, "slots must return after the queue ran"
     assert keep["w"].is_cuda and np.isfinite(keep["w"].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("sort", SORTS)
+def test_chain_long_round_slab_bitwise(sort):
+    """A BASELINE-shaped eager round at reduced width: 64 arrivals x (2M + 4,099) fp32 in a tiled
+    slab (the chain's 64-client queue, the aliased first step in round 1, the tail chunk),
+    two rounds, deferred == one fused launch per call on every element."""
+    from flame_amd import engine, synth
+    from flame_amd.slab import UpdateSlab
+    shapes = {"w": (2_000_000,), "t": (4_099,)}
+    n = 64
+    counts = [int(c) for c in synth.counts(17, n)]
+
+    def run(defer):
+        slab = UpdateSlab({k: torch.zeros(s) for k, s in shapes.items()}, capacity=n, device=DEV)
+        opt = _opt(sort, defer=defer)
+        weights = {}
+        for j, (k, s) in enumerate(shapes.items()):
+            t = torch.empty(s, device=DEV)
+            engine.synth_fill_(t, 17, 100 + j, 0, 1.0)
+            weights[k] = t
+        tmp = {k: torch.empty(s, device=DEV) for k, s in shapes.items()}
+        res = []
+        for r in range(2):
+            base = {k: v.clone() for k, v in dict(weights).items()}
+            total = 0
+            for i in range(n):
+                for j, k in enumerate(shapes):
+                    engine.synth_fill_(tmp[k], 17, 1000 * r + 10 * i + j, 0, 1e-2)
+                total += counts[i]
+                cache = S.SortedCache()
+                cache[f"{i:03d}"] = S.TR(slab.put(tmp), counts[i])
+                out = opt.do(base, cache, total=total)
+            weights = out
+            cur = S.to_cpu(dict(out))
+            res.append((S.to_cpu(base), cur, S.to_cpu(opt.m_t) if opt.m_t is not None else None,
+                        S.to_cpu(opt.v_t) if opt.v_t is not None else None))
+        return res
+
+    ref, got = run(False), run(True)
+    for r, (a, b) in enumerate(zip(got, ref)):
+        for lbl, x, y in zip(("base", "current", "m_t", "v_t"), a, b):
+            if y is not None:
+                S.assert_bitwise(f"{sort}/long/r{r}/{lbl}", x, y)
