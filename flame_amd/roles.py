@@ -19,7 +19,8 @@ drop-in optimizers -- its updates are unpickled into one tensor each (row layout
 The eager top aggregator (``eager_syncfl/top_aggregator.py:36-90``) calls ``do()`` once per
 arrival and reads only the object the last call returns; :func:`patch_eager_role_class`
 (``install_device_cache(eager_batching=True)``) turns on ``FedAvg(defer=True)`` for it, so
-a round's arrivals are reduced in one launch (flame_amd/optimizer/fedavg.py).
+a round's arrivals are reduced in one launch (flame_amd/optimizer/fedavg.py), or, for the
+FedOPT family, ``defer=True``: the round's calls run as one flame_fedopt_chain launch.
 """
 from __future__ import annotations
 
@@ -87,13 +88,18 @@ EAGER_ROLE_CLASS = ("flame.mode.horizontal.eager_syncfl.top_aggregator", "TopAgg
 
 
 def enable_eager_batching(role):
-    """Turn on eager batching (``defer=True``) for ``role.optimizer`` when it is the
-    flame_amd FedAvg itself (subclasses -- FedOPT, FedProx, ... -- keep their own ``do``).
-    Returns whether it was enabled."""
+    """Turn on eager batching for ``role.optimizer``: ``defer=True`` when it is the flame_amd
+    FedAvg itself, the queued chain (``FedOPT(defer=True)``: one flame_fedopt_chain launch per
+    round) when it is a FedAdam / FedYogi / FedAdaGrad.  Other subclasses (FedProx, FedGFT, ...)
+    keep their own ``do``.  Returns whether it was enabled."""
     from .optimizer.fedavg import FedAvg
+    from .optimizer.fedopt import FedOPT
     opt = getattr(role, "optimizer", None)
     if type(opt) is FedAvg:
         opt.defer = True
+        return True
+    if isinstance(opt, FedOPT):
+        opt.chain_defer = True
         return True
     return False
 

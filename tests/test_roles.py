@@ -114,5 +114,12 @@ def test_eager_role_patch_enables_batching_after_cache_patch():
     EagerTop.sort = "fedadam"
     e2 = EagerTop()
     e2.internal_init()
-    assert e2.optimizer.defer is False
+    # FedOPT keeps FedAvg's own defer off (its FedAvg part runs inside the chain) and queues
+    # the round's calls for flame_fedopt_chain instead
+    assert e2.optimizer.defer is False and e2.optimizer.chain_defer is True
+    Top.sort = "fedadam"
+    t2 = Top()
+    t2.internal_init()
+    assert t2.optimizer.chain_defer is False     # only the eager role
+    Top.sort = EagerTop.sort = "fedavg"
     assert isinstance(roles.install_device_cache(eager_batching=True, placement="host"), list)
