@@ -83,8 +83,14 @@ def patch_role_class(cls, **kwargs):
     return cls
 
 
-# the eager top aggregator (inherits syncfl TopAggregator.internal_init)
-EAGER_ROLE_CLASS = ("flame.mode.horizontal.eager_syncfl.top_aggregator", "TopAggregator")
+# the eager aggregators (inherit the syncfl roles' internal_init): one do() per arrival into
+# the round's base, only the last result read (eager_syncfl/top_aggregator.py:36-90,
+# eager_syncfl/middle_aggregator.py:40-80)
+EAGER_ROLE_CLASSES = (
+    ("flame.mode.horizontal.eager_syncfl.top_aggregator", "TopAggregator"),
+    ("flame.mode.horizontal.eager_syncfl.middle_aggregator", "MiddleAggregator"),
+)
+EAGER_ROLE_CLASS = EAGER_ROLE_CLASSES[0]
 
 
 def enable_eager_batching(role):
@@ -133,7 +139,7 @@ def _import_class(mod, name):
 def install_device_cache(eager_batching: bool = False, **kwargs):
     """Patch flame's aggregator role classes (ROLE_CLASSES) in place; call once before roles
     are composed, next to ``flame_amd.optimizers.install()``.  ``eager_batching``: also
-    patch the eager top aggregator (:func:`patch_eager_role_class`).  Returns the patched
+    patch the eager top and middle aggregators (:func:`patch_eager_role_class`).  Returns the patched
     classes; classes whose module does not import here are skipped (logged)."""
     done = []
     for mod, name in ROLE_CLASSES:
@@ -141,7 +147,8 @@ def install_device_cache(eager_batching: bool = False, **kwargs):
         if cls is not None:
             done.append(patch_role_class(cls, **kwargs))
     if eager_batching:
-        cls = _import_class(*EAGER_ROLE_CLASS)
-        if cls is not None:
-            done.append(patch_eager_role_class(cls))
+        for mod, name in EAGER_ROLE_CLASSES:
+            cls = _import_class(mod, name)
+            if cls is not None:
+                done.append(patch_eager_role_class(cls))
     return done
