@@ -39,7 +39,7 @@ from collections import OrderedDict
 
 import torch
 
-from .. import engine
+from .. import engine, metrics
 from .fedavg import FedAvg
 
 logger = logging.getLogger(__name__)
@@ -320,9 +320,13 @@ class FedOPT(FedAvg):
         self._chain = None
         last = len(ch.steps) - 1
         cuts = sorted({i for i, r in enumerate(ch.results) if r() is not None} | {last})
-        cur, aliased, zero, start = ch.current, ch.aliased, ch.state_zero, 0
         keys = list(ch.base.keys())
         hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
+        with metrics.recording(self):      # a queue run at a read is reported like do()'s launches
+            self._run_chain(ch, cuts, keys, hyper)
+
+    def _run_chain(self, ch, cuts, keys, hyper):
+        cur, aliased, zero, start = ch.current, ch.aliased, ch.state_zero, 0
         for cut in cuts:
             steps = ch.steps[start:cut + 1]
             base = [ch.base[k] for k in keys]

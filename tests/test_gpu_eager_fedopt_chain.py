@@ -266,3 +266,33 @@ def test_chain_long_round_slab_bitwise(sort):
         for lbl, x, y in zip(("base", "current", "m_t", "v_t"), a, b):
             if y is not None:
                 S.assert_bitwise(f"{sort}/long/r{r}/{lbl}", x, y)
+
+
+def test_chain_launch_reaches_the_metric_collector():
+    """The queue runs at a read outside do(); its launch is reported to the optimizer's
+    metric_collector under the optimizer's alias, like the launches inside do()."""
+    from flame_amd import metrics
+
+    class MC:
+        def __init__(self):
+            self.state_dict = {}
+
+        def save(self, mtype, alias, value):
+            self.state_dict[f"{alias}.{mtype}"] = value
+
+    w0, rounds = _rounds(31, 1, 5)
+    opt = _opt("fedadam", defer=True)
+    opt.metric_collector = MC()
+    base = S.to_dev(w0, DEV)
+    cache = S.SortedCache()
+    total = 0
+    for i, call in enumerate(rounds[0]):
+        (w, c), = call
+        total += c
+        cache[f"e{i}"] = S.TR(S.to_dev(w, DEV), c)
+        out = opt.do(base, cache, total=total)
+    dict(out)                                        # the read runs the queue
+    metrics.flush()
+    sd = opt.metric_collector.state_dict
+    assert sd["fedadam.flame_fedopt_chain.launches"] == 1, sd
+    assert sd["fedadam.flame_fedopt_chain.runtime"] > 0
