@@ -508,12 +508,8 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
-                         "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
-                         "bytes_per_client_param": k_bytes / (n * P * 4),
-                         **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
-                                     "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
-                                     "among them): VALU-bound near its HBM time (DESIGN.md §4)"}
-                            if fedopt and defer else {})},
+                         "algorithmic_bytes_per_step": k_bytes,
+                         "bytes_per_client_param": k_bytes / (n * P * 4)},
         }), flush=True)
 
 
@@ -586,7 +582,7 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
                          "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
                          "bytes_per_client_param": k_bytes / (n * P * 4),
                          **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
-                                     "element (~33 fp32 VALU ops each, the correctly rounded sqrt and divide "
+                                     "element (~41 VALU ops each, the correctly rounded sqrt and divide "
                                      "among them): VALU-bound near its HBM time (DESIGN.md §4)"}
                             if fedopt and defer else {})},
         }), flush=True)
