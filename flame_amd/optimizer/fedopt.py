@@ -278,9 +278,13 @@ class FedOPT(FedAvg):
         device = base_weights[keys[0]].device
         for _, tres in popped:
             w = tres.weights
-            # (slab slots are strided (tiles, T) views: their numel is checked by the launch)
+            # an update the per-call path would refuse (wrong size) is not queued: it raises from
+            # its own do() there (slab slots are strided (tiles, T) views of the key)
             if set(w.keys()) != set(keys) or not all(
-                    w[k].dtype == base_weights[k].dtype and w[k].device == device for k in keys):
+                    w[k].dtype == base_weights[k].dtype and w[k].device == device
+                    and (w[k].numel() == base_weights[k].numel()
+                         or engine.tiled_stride(w[k], base_weights[k].numel()))
+                    for k in keys):
                 self._flush_chain()
                 return popped
         if ch is None:

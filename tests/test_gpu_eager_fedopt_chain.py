@@ -296,3 +296,27 @@ def test_chain_launch_reaches_the_metric_collector():
     sd = opt.metric_collector.state_dict
     assert sd["fedadam.flame_fedopt_chain.launches"] == 1, sd
     assert sd["fedadam.flame_fedopt_chain.runtime"] > 0
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_wrong_size_update_raises_from_its_own_call(defer):
+    """An update of the wrong size raises from the do() that brings it, queued calls or not
+    (the reference's in-place add raises there); the calls queued before it have run."""
+    from flame_amd.optimizer.fedopt import DeferredCurrent
+    w0, rounds = _rounds(13, 1, 3)
+    opt = _opt("fedyogi", defer=defer)
+    base = S.to_dev(w0, DEV)
+    cache = S.SortedCache()
+    total = 0
+    outs = []
+    for i, call in enumerate(rounds[0]):
+        (w, c), = call
+        total += c
+        cache[f"e{i}"] = S.TR(S.to_dev(w, DEV), c)
+        outs.append(opt.do(base, cache, total=total))
+    bad = {k: torch.zeros(v.numel() + 1, device=DEV) for k, v in w0.items()}
+    cache["zz"] = S.TR(bad, 1)
+    with pytest.raises(RuntimeError):
+        opt.do(base, cache, total=total + 1)
+    if defer:
+        assert isinstance(outs[-1], DeferredCurrent) and outs[-1]._value is not None
