@@ -523,3 +523,55 @@ def test_random_stateful_vs_oracle(case):
         _run_feddyn(rng, label + " feddyn")
     else:
         _run_scaffold(rng, label + " scaffold")
+
+
+# ---------------------------------------------------------------- 16-bit eager FedOPT, deferred
+N_EAGER16 = 20
+
+
+@pytest.mark.parametrize("case", range(N_EAGER16))
+def test_random_eager_fedopt_16bit_defer_equals_per_call(case):
+    """bf16 / fp16 (and mixed) eager FedOPT rounds: FedOPT(defer=True) -- one flame_fedopt_chain
+    launch per dtype per round -- against one fused launch per call, bitwise for base, every
+    round's current, m_t and v_t (the oracle holds these keys to a one-ulp contract, the two
+    GPU paths to each other exactly)."""
+    from copy import deepcopy
+    from flame_amd.optimizers import optimizer_provider
+    rng = np.random.default_rng(13_000 + case)
+    keys = []
+    for k in range(int(rng.integers(1, 4))):
+        dt = [torch.bfloat16, torch.float16, torch.float32][rng.integers(0, 3)] if k else \
+            [torch.bfloat16, torch.float16][rng.integers(0, 2)]
+        keys.append((f"k{k}", dt, _draw_size(rng, dt) or 1))
+    placement = ["hbm", "slab", "views"][rng.integers(0, 3)]
+    n = int(rng.integers(2, 30))
+    sort = ["fedadam", "fedyogi", "fedadagrad"][rng.integers(0, 3)]
+    seed = int(rng.integers(1 << 31))
+    counts = [int(c) for c in rng.integers(1, 1000, 2 * n)]
+    label = (f"eager16 case {case}: {sort} {placement} n={n} keys=" +
+             ",".join(f"{k}:{str(dt).replace('torch.', '')}[{s}]" for k, dt, s in keys))
+
+    def run(defer):
+        g = torch.Generator().manual_seed(seed)
+        w = S.to_dev({k: _rand(g, (s,), dt, 1.0) for k, dt, s in keys}, DEV)
+        P = _Placer(placement, keys, 2 * n)
+        opt = optimizer_provider.get(sort, defer=defer)
+        res = []
+        for r in range(2):
+            base = deepcopy(w)
+            cache = S.SortedCache()
+            total = 0
+            for i in range(n):
+                u = {k: _rand(g, (s,), dt, 1e-2) for k, dt, s in keys}
+                total += counts[r * n + i]
+                cache[f"r{r}e{i:03d}"] = S.TR(P.put(u), counts[r * n + i])
+                out = opt.do(base, cache, total=total)
+            w = out
+            cur = S.to_cpu(dict(out))
+            res.append((S.to_cpu(base), cur, S.to_cpu(opt.m_t) if opt.m_t is not None else {},
+                        S.to_cpu(opt.v_t) if opt.v_t is not None else {}))
+        return res
+
+    for r, (a, b) in enumerate(zip(run(True), run(False))):
+        for lbl, x, y in zip(("base", "current", "m_t", "v_t"), a, b):
+            S.assert_bitwise(f"{label}/r{r}/{lbl}", x, y)
