@@ -560,14 +560,17 @@ def fedopt_chain_(variant: str, base: List[torch.Tensor], cur: List[Optional[tor
         if code in (N.FLAME_BF16, N.FLAME_F16):  # torch-CPU rounds the scalar of `sqrt(v) + tau`
             h[5] = float(torch.tensor(float(h[5]), dtype=base[idx[0]].dtype))
         p = plan(code, segs, rates)
-        dm = _staging.upload(p.meta, device)
-        ends = _staging.upload(ends_host, device)
+        # the step_end bytes ride behind the plan's tables: one upload per launch
+        pad = np.zeros(-(-ends_host.size // 8) * 8, dtype=np.uint8)
+        pad[:ends_host.size] = ends_host
+        dm = _staging.upload(np.concatenate([p.meta, pad.view(np.int64)]), device)
         segp, clp, r32p, _ = _device_ptrs(dm, p)
         with _timed("flame_fedopt_chain", device, nbytes):
             N.check(L.flame_fedopt_chain(code, FEDOPT_VARIANT[variant], N.FLAME_OPT_STATE_ZERO if state_zero else 0,
-                                         segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p, ends.data_ptr(),
-                                         *[float(x) for x in h], _stream_ptr(device)))
-        keep += [dm, ends]
+                                         segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
+                                         dm.data_ptr() + p.meta.nbytes, *[float(x) for x in h],
+                                         _stream_ptr(device)))
+        keep.append(dm)
         _keepalive(keep, device)
 
 
