@@ -588,8 +588,64 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
         }), flush=True)
 
 
+def launch_plan(gpus, env):
+    """What ``bench.py --gpus N`` does in this process, decided before anything touches the GPU.
+
+    ("run", None)    this process is one rank: torchrun's env names the world (and it equals
+                     --gpus), or N == 1 with no launcher;
+    ("spawn", N)     N > 1 and no launcher env: start N ranks under torch.distributed.run;
+    ("error", msg)   the launcher's world and --gpus disagree, or N < 1.
+    Every rank returns the full model (syncfl/top_aggregator.py:161-173), so N is the number of
+    GPUs the line is measured on -- never silently fewer."""
+    if gpus < 1:
+        return "error", f"bench.py: --gpus {gpus}: need at least one GPU"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", (f"bench.py: --gpus {gpus} but the launcher's WORLD_SIZE is {ws}: "
+                             f"run with --gpus {ws} or launch {gpus} ranks")
+        return "run", None
+    if "RANK" in env or gpus == 1:
+        return "run", None
+    return "spawn", gpus
+
+
+def spawn_ranks(gpus, argv):
+    """Start ``gpus`` ranks of this script under torch.distributed.run (fresh child processes:
+    this parent has not initialised the GPU and never execs), relay their stdout line by line
+    (rank 0's JSON line included) and return the launcher's exit code (non-zero when any rank
+    failed)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, FLAME_BENCH_LAUNCHER=f"bench.py --gpus {gpus} -> torch.distributed.run")
+    print(f"bench.py: --gpus {gpus} without a launcher: starting {gpus} ranks: {' '.join(cmd)}",
+          file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+def launcher(world):
+    """How this line's ranks were started (the driver's own torchrun, bench.py --gpus N, or none)."""
+    return os.environ.get("FLAME_BENCH_LAUNCHER",
+                          "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")
+
+
 def main():
     args = parse()
+    what, arg = launch_plan(args.gpus, os.environ)
+    if what == "error":
+        raise SystemExit(arg)
+    if what == "spawn":
+        raise SystemExit(spawn_ranks(arg, sys.argv[1:]))
     world, rank, local = setup_dist(args.force_shard)
     dev = torch.device("cuda", local)
     from flame_amd import _native, engine, synth
@@ -653,7 +709,7 @@ def main():
     ks = kernel_stats(events, name)
 
     if rank == 0:
-        traffic = None
+        traffic, traffic_source = None, None
         try:
             doc = json.load(open(args.traffic))
             for tr in (doc["entries"] if "entries" in doc else [doc]):
@@ -661,6 +717,13 @@ def main():
                         and tr.get("layout", "row") == args.layout
                         and tr.get("workload", args.workload) == args.workload):
                     traffic = tr["hbm_bytes_per_launch"]
+                    # a LOOKUP, not this run's counters: PMC passes run in their own processes
+                    # (rocprofv3 --pmc, tools/pmc_traffic.py); name where the bytes came from
+                    traffic_source = {"kind": "lookup", "file": os.path.relpath(args.traffic, ROOT),
+                                      "entry": {k: tr.get(k) for k in ("kernel", "clients", "params", "layout")},
+                                      "counters": tr.get("source", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                                         "(source not recorded in this entry)"),
+                                      "traffic_over_algorithmic": tr.get("traffic_over_algorithmic")}
         except Exception:  # noqa: BLE001
             pass
         cpu = None
@@ -705,7 +768,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_source,
                 "kernel": name, "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
                 "launches_per_step": launches_per_step,
                 # same device, same buffer: plain streaming-read probe (tools/hbm_probe.hip)
@@ -713,6 +776,7 @@ def main():
                 "frac_of_measured_ceiling": (achieved / ceiling) if ceiling else None,
             },
             "cpu_baseline": cpu,
+            "launcher": launcher(world),
         }
         print(json.dumps(line), flush=True)
     import torch.distributed as dist
@@ -994,6 +1058,7 @@ def bench_sharded(args, world, rank, dev, n, P):
                          "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes, "launches_per_step": lps},
             "collective": _collective_note(plan, world, 4),
             "process_group": process_group_info(),
+            "launcher": launcher(world),
             "gather_check": gc,
             "cpu_baseline": None,
         }), flush=True)
@@ -1125,6 +1190,7 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                          "launches_per_step": lps},
             "collective": _collective_note(plan, world, 2),
             "process_group": process_group_info(),
+            "launcher": launcher(world),
             "gather_check": gc,
         }), flush=True)
     import torch.distributed as dist

@@ -149,6 +149,12 @@ class FedOPT(FedAvg):
     def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         logger.debug("calling fedopt (flame_amd)")
         if self.chain_defer and not kwargs.keys() & _SHARD_KWARGS:
+            ch = self._chain
+            if ch is not None and ch.base is base_weights and (len(cache) == 0 or total == 0):
+                # an arrival with nothing to aggregate: the reference's FedAvg.do returns None
+                # and do() hands back current_weights unchanged (fedopt.py:80-85) -- here the
+                # queued chain's last result, without cutting the chain
+                return ch.result(self, len(ch.steps) - 1, list(base_weights.keys()))
             popped = self._try_queue(base_weights, cache, total)
             if isinstance(popped, DeferredCurrent):
                 return popped
@@ -311,9 +317,8 @@ class FedOPT(FedAvg):
         ch.steps.append(step)
         ch.n_entries += len(step)
         ch.nbytes += len(step) * sum(base_weights[k].numel() * 4 for k in keys)
-        res = DeferredCurrent(self, ch, len(ch.steps) - 1, keys)
-        ch.results.append(weakref.ref(res))
-        return res
+        ch.results.append([])
+        return ch.result(self, len(ch.steps) - 1, keys)
 
     def _flush_chain(self):
         """Run the queued eager calls (if any): one flame_fedopt_chain launch per stretch that
@@ -323,39 +328,51 @@ class FedOPT(FedAvg):
             return
         self._chain = None
         last = len(ch.steps) - 1
-        cuts = sorted({i for i, r in enumerate(ch.results) if r() is not None} | {last})
+        cuts = sorted({i for i, refs in enumerate(ch.results) if any(r() is not None for r in refs)} | {last})
         keys = list(ch.base.keys())
         hyper = engine.fedopt_scalars(self.beta_1, self.beta_2, self.eta, self.tau)
         with metrics.recording(self):      # a queue run at a read is reported like do()'s launches
             self._run_chain(ch, cuts, keys, hyper)
 
     def _run_chain(self, ch, cuts, keys, hyper):
+        """One flame_fedopt_chain launch per stretch of queued calls.  The optimizer's state
+        (m_t / v_t, current_weights, agg_weights) moves to a stretch's results only once its
+        launch has returned; if one fails, the state stays at the last stretch that ran and every
+        result of the stretches that did not run re-raises the failure when read."""
         cur, aliased, zero, start = ch.current, ch.aliased, ch.state_zero, 0
-        for cut in cuts:
-            steps = ch.steps[start:cut + 1]
-            base = [ch.base[k] for k in keys]
-            if zero:
-                self._m = {k: torch.empty_like(ch.base[k]) for k in keys}
-                self._v = {k: torch.empty_like(ch.base[k]) for k in keys}
-            outs = [torch.empty_like(ch.base[k]) for k in keys]
-            ends = [j == len(st) - 1 for st in steps for j in range(len(st))]
-            engine.fedopt_chain_(self.variant, base, [None if aliased[k] else cur[k] for k in keys], outs,
-                                 [self._m[k] for k in keys], [self._v[k] for k in keys],
-                                 [[w[k] for st in steps for w, _ in st] for k in keys],
-                                 [r for st in steps for _, r in st], ends, hyper, zero,
-                                 [aliased[k] for k in keys])
-            new = OrderedDict(zip(keys, outs))
-            r = ch.results[cut]()
-            if r is not None:
-                r._value = new
-            cur, aliased, zero, start = new, {k: False for k in keys}, False, cut + 1
-        self._current = cur
-        self._agg = ch.base
-        self._prev_current = None      # d_t is not kept across a deferred queue
-        self._d_t = None
-        # the queued updates (slab slots among them) are released now, not when the last
-        # DeferredCurrent dies (the role keeps that one as its weights)
-        ch.steps, ch.current, ch.base = [], None, None
+        try:
+            for cut in cuts:
+                steps = ch.steps[start:cut + 1]
+                base = [ch.base[k] for k in keys]
+                m = {k: torch.empty_like(ch.base[k]) for k in keys} if zero else self._m
+                v = {k: torch.empty_like(ch.base[k]) for k in keys} if zero else self._v
+                outs = [torch.empty_like(ch.base[k]) for k in keys]
+                ends = [j == len(st) - 1 for st in steps for j in range(len(st))]
+                engine.fedopt_chain_(self.variant, base, [None if aliased[k] else cur[k] for k in keys], outs,
+                                     [m[k] for k in keys], [v[k] for k in keys],
+                                     [[w[k] for st in steps for w, _ in st] for k in keys],
+                                     [r for st in steps for _, r in st], ends, hyper, zero,
+                                     [aliased[k] for k in keys])
+                new = OrderedDict(zip(keys, outs))
+                self._m, self._v, self._current, self._agg = m, v, new, ch.base
+                self._prev_current = None      # d_t is not kept across a deferred queue
+                self._d_t = None
+                for ref in ch.results[cut]:
+                    r = ref()
+                    if r is not None:
+                        r._value = new
+                cur, aliased, zero, start = new, {k: False for k in keys}, False, cut + 1
+        except BaseException as e:
+            for refs in ch.results[start:]:
+                for ref in refs:
+                    r = ref()
+                    if r is not None and r._value is None:
+                        r._error = e
+            raise
+        finally:
+            # the queued updates (slab slots among them) are released now, not when the last
+            # DeferredCurrent dies (the role keeps that one as its weights)
+            ch.steps, ch.current, ch.base = [], None, None
 
     def _adapt_generic(self, keys, average, current, state_zero):
         """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""
@@ -407,9 +424,14 @@ class _Chain:
         self.aliased = aliased          # {key: current[key] IS base[key]} (right after the passthrough)
         self.state_zero = state_zero    # m_t / v_t were None
         self.steps = []                 # per do(): [(weights, rate), ...]
-        self.results = []               # weakrefs to each do()'s DeferredCurrent
+        self.results = []               # per do(): weakrefs to the DeferredCurrents handed out for it
         self.n_entries = 0
         self.nbytes = 0
+
+    def result(self, owner, step, keys):
+        res = DeferredCurrent(owner, self, step, keys)
+        self.results[step].append(weakref.ref(res))
+        return res
 
 
 class _Replay:
@@ -439,10 +461,14 @@ class DeferredCurrent(collections.abc.Mapping):
     def __init__(self, owner, chain, step, keys):
         self._owner, self._chain, self._step, self._keys = owner, chain, step, keys
         self._value = None
+        self._error = None
 
     def materialize(self):
-        if self._value is None:
+        if self._value is None and self._error is None:
             self._owner._flush_chain()
+        if self._error is not None:
+            raise RuntimeError("the queued FedOPT do() call this result belongs to did not run: "
+                               f"{type(self._error).__name__}: {self._error}") from self._error
         return self._value
 
     def __getitem__(self, k):

@@ -28,6 +28,11 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
+try:
+    from . import consult
+except ImportError:  # loaded as a top-level module
+    import consult
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
@@ -39,6 +44,12 @@ _lib = None
 
 
 def lib():
+    """The C restatement, as a checker: every call counts as a consultation (consult.py)."""
+    consult.note()
+    return _load()
+
+
+def _load():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -160,7 +171,7 @@ def adapt_tensor(sort, avg, cur, m, v, hyper):
 
 def synth_f32(seed, stream, start, n, scale) -> np.ndarray:
     out = np.empty(n, dtype=np.float32)
-    lib().flame_oracle_synth_f32(seed, stream, start, n, float(scale), out.ctypes.data)
+    _load().flame_oracle_synth_f32(seed, stream, start, n, float(scale), out.ctypes.data)
     return out
 
 
@@ -250,6 +261,7 @@ class OracleFedOPT(OracleFedAvg):
     def _adapt_torch(self, k, avg, cur, first):
         """Non-fp32 keys: the reference's own torch op sequence (fedopt.py:106-129 and the
         _delta_v variants), which carries its dtype promotions (int64 -> fp32, bf16 rounding)."""
+        consult.note()
         b1, b2, eta, tau = self.beta_1, self.beta_2, self.eta, self.tau
         d = avg - cur
         m = torch.zeros_like(d) if first else self.m_t[k]

@@ -19,9 +19,15 @@ import math
 
 import torch
 
+try:
+    from . import consult
+except ImportError:  # loaded as a top-level module
+    import consult
+
 
 def fedavg_round(agg_weights, updates, counts, total):
     """agg_weights[k] += (v * count/total) for each update in order (in place)."""
+    consult.note()
     for w, c in zip(updates, counts):
         rate = c / total
         for k, v in w.items():
@@ -32,6 +38,7 @@ def fedavg_round(agg_weights, updates, counts, total):
 
 
 def fedbuff_step(agg, weights, version, tres_version):
+    consult.note()
     rate = 1 / math.sqrt(1 + version - tres_version)
     if agg is None:
         agg = {}
@@ -47,6 +54,7 @@ def fedbuff_step(agg, weights, version, tres_version):
 
 
 def fedbuff_scale_add(base_weights, agg_goal_weights, agg_goal):
+    consult.note()
     for k in base_weights.keys():
         base_weights[k] += agg_goal_weights[k] / agg_goal
     return base_weights
@@ -54,6 +62,7 @@ def fedbuff_scale_add(base_weights, agg_goal_weights, agg_goal):
 
 def fedopt_adapt(sort, avg, cur, m_t, v_t, beta_1, beta_2, eta, tau):
     """One adaptive step per key; m_t / v_t dicts are updated (None entries start at zeros)."""
+    consult.note()
     new = {}
     for k in cur.keys():
         d = avg[k] - cur[k]

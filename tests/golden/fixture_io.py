@@ -74,8 +74,13 @@ class FixtureWriter:
         np.savez_compressed(path, __meta__=blob, **self.arrays)
 
 
+LOADS = 0   # golden fixtures opened this process (tests/conftest.py's oracle-evidence check)
+
+
 class Fixture:
     def __init__(self, path):
+        global LOADS
+        LOADS += 1
         z = np.load(path, allow_pickle=False)
         self.meta = json.loads(bytes(z["__meta__"]).decode())
         self.arrays = {k: z[k] for k in z.files if k != "__meta__"}

@@ -38,6 +38,7 @@ def _undefined(path):
     module = _bound_names(ast.Module(body=[n for n in tree.body if not isinstance(n, ast.FunctionDef)],
                                      type_ignores=[]))
     module.update(n.name for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)))
+    module.update(("__file__", "__name__", "__doc__"))    # module attributes every module has
     bad = []
     for fn in (n for n in tree.body if isinstance(n, ast.FunctionDef)):
         local = _bound_names(fn)

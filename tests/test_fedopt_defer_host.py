@@ -1,0 +1,125 @@
+"""FedOPT(defer=True)'s queue bookkeeping on the host (no GPU: the chain launch is replaced).
+
+* A failed chain launch leaves the optimizer's state where it was (m_t / v_t not replaced by
+  unwritten buffers) and every queued result re-raises the failure when read.
+* An eager arrival with nothing to aggregate (empty cache, or total 0) returns the queued
+  chain's last result without cutting the chain: one launch per round; the
+  reference returns current_weights unchanged there (fedopt.py:80-85, fedavg.py:72-73).
+"""
+import pytest
+import torch
+
+from flame_amd import engine
+from flame_amd.optimizer import fedopt as F
+from flame_amd.optimizers import optimizer_provider
+
+
+class TR:
+    def __init__(self, weights, count):
+        self.weights, self.count, self.version = weights, count, 0
+
+
+class Cache(dict):
+    def iterkeys(self):
+        return iter(sorted(self))
+
+
+@pytest.fixture
+def host_chain(monkeypatch):
+    """The deferred path over CPU tensors: the queue's eligibility check accepts them and the
+    chain launch is a recorder that fills its outputs like the kernel would (or raises)."""
+    monkeypatch.setattr(F, "_chain_tensors", lambda w: True)
+    calls = []
+
+    def fake_chain(variant, base, cur, cur_out, m, v, clients, rates, step_end, hyper, state_zero, first_aliased):
+        calls.append(len(rates))
+        if getattr(fake_chain, "fail", None):
+            raise RuntimeError(fake_chain.fail)
+        for b, o, mm, vv in zip(base, cur_out, m, v):
+            o.copy_(b + 1)
+            mm.fill_(0.5)
+            vv.fill_(0.25)
+    monkeypatch.setattr(engine, "fedopt_chain_", fake_chain)
+    return fake_chain, calls
+
+
+def _after_passthrough(sort="fedadam"):
+    opt = optimizer_provider.get(sort, defer=True)
+    base = {"w": torch.zeros(8)}
+    opt._current = base                 # the state right after round 1's passthrough (current IS base)
+    return opt, base
+
+
+def _arrive(opt, base, i, count):
+    c = Cache()
+    c[f"e{i}"] = TR({"w": torch.full((8,), float(i))}, count)
+    return opt.do(base, c, total=10)
+
+
+def test_failed_chain_keeps_state_and_results_reraise(host_chain):
+    fake, calls = host_chain
+    fake.fail = "launch refused"
+    opt, base = _after_passthrough()
+    r1 = _arrive(opt, base, 1, 3)
+    r2 = _arrive(opt, base, 2, 4)
+    assert isinstance(r1, F.DeferredCurrent) and isinstance(r2, F.DeferredCurrent) and calls == []
+    with pytest.raises(RuntimeError, match="launch refused"):
+        r2["w"]                                      # the read runs the queue: the launch fails
+    assert opt._m is None and opt._v is None       # no unwritten m / v adopted as state
+    assert opt.m_t is None and opt.v_t is None
+    assert opt.current_weights is base             # still the passthrough's state
+    for r in (r1, r2):
+        with pytest.raises(RuntimeError, match="did not run: RuntimeError: launch refused"):
+            r.materialize()
+
+
+def test_failure_after_a_cut_keeps_the_cut(host_chain):
+    """A held result cuts the queue; when the second stretch's launch fails, the state is the
+    first stretch's and only the later result re-raises."""
+    fake, calls = host_chain
+    opt, base = _after_passthrough("fedyogi")
+    r1 = _arrive(opt, base, 1, 3)
+    r2 = _arrive(opt, base, 2, 4)
+    orig = engine.fedopt_chain_
+
+    def second_fails(*a, **k):
+        if calls:
+            calls.append("x")
+            raise RuntimeError("second stretch")
+        return orig(*a, **k)
+    engine.fedopt_chain_ = second_fails
+    try:
+        with pytest.raises(RuntimeError, match="second stretch"):
+            r2["w"]
+    finally:
+        engine.fedopt_chain_ = orig
+    assert torch.equal(r1["w"], torch.ones(8))     # the first stretch ran: its result stands
+    assert opt._current is r1.materialize()
+    assert torch.equal(opt._m["w"], torch.full((8,), 0.5))
+    with pytest.raises(RuntimeError, match="did not run"):
+        r2.materialize()
+
+
+@pytest.mark.parametrize("hold", [False, True])
+@pytest.mark.parametrize("empty", ["cache", "total"])
+def test_nothing_to_aggregate_does_not_cut_the_chain(host_chain, empty, hold):
+    fake, calls = host_chain
+    opt, base = _after_passthrough("fedadagrad")
+    results = [_arrive(opt, base, 1, 3)]
+    c = Cache()
+    if empty == "total":
+        c["z"] = TR({"w": torch.ones(8)}, 0)
+    results.append(opt.do(base, c, total=0 if empty == "total" else 10))
+    assert len(c) == (1 if empty == "total" else 0)     # total 0: nothing popped (fedavg.py:72-73)
+    results.append(_arrive(opt, base, 2, 4))
+    assert isinstance(results[1], F.DeferredCurrent) and calls == []
+    last = results.pop()
+    held = results if hold else []
+    del results
+    final = dict(last)
+    if hold:       # held results cut the queue at their call (both name the first call)
+        assert calls == [1, 1], calls
+        assert held[1]["w"] is held[0]["w"]             # == current_weights after the first call
+    else:          # one launch for the round: the empty arrival did not cut it
+        assert calls == [2], calls
+    assert opt.current_weights["w"] is final["w"]

@@ -8,9 +8,10 @@ import pytest
 import torch
 
 import scenarios as S
+from oracle import torch_cpu
 from test_oracle_dtype_matrix import DTYPES, _rand, _reference
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.oracle]
 
 DEV = "cuda:0"
 
@@ -63,16 +64,10 @@ def test_fedbuff_scale_add_every_model_dtype_vs_torch(agg_dt):
     ups = [_rand(g, agg_dt, 2051, 1e-1) for _ in range(3)]
     for model_dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
         ref_agg = None
-        for i, u in enumerate(ups):
-            tmp = u * (1 / math.sqrt(1 + 10 - (10 - i)))      # fedbuff.py:96
-            tmp = tmp.to(u.dtype) if tmp.dtype != u.dtype else tmp
-            if ref_agg is None:
-                ref_agg = tmp
-            else:
-                ref_agg += tmp
+        for i, u in enumerate(ups):                           # fedbuff.py:94-96,136-157
+            ref_agg = torch_cpu.fedbuff_step(ref_agg, {"k": u}, 10, 10 - i)
         w0 = _rand(g, model_dt, 2051, 1.0)
-        exp = w0.clone()
-        exp += ref_agg / 3
+        exp = torch_cpu.fedbuff_scale_add({"k": w0.clone()}, ref_agg, 3)["k"]   # fedbuff.py:122-127
         opt, agg = _drop_in("fedbuff"), None
         for i, u in enumerate(ups):
             c = S.SortedCache()

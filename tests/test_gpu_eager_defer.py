@@ -31,6 +31,7 @@ def _fedavg(**kw):
     return optimizer_provider.get("fedavg", **kw)
 
 
+@pytest.mark.oracle
 def test_eager_deferred_golden_one_launch(golden):
     """Every arrival queued (base untouched until the read), the final model == the
     reference's state after the last arrival, bitwise."""

@@ -11,7 +11,7 @@ import torch
 
 import scenarios as S
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.oracle]
 
 DEV = "cuda:0"
 P = (1 << 31) + 4099           # a ragged tail after the 2^31st element

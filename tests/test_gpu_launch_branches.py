@@ -22,7 +22,7 @@ import torch
 
 import scenarios as S
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.oracle]
 
 DEV = "cuda:0"
 RND = 20

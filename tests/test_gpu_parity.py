@@ -31,12 +31,14 @@ def make_amd(sort, **kw):
 
 
 # ------------------------------------------------------------------ golden vectors
+@pytest.mark.oracle
 @pytest.mark.parametrize("name,driver", S.BITWISE_FIXTURES, ids=[n for n, _ in S.BITWISE_FIXTURES])
 def test_golden_bitwise(golden, name, driver):
     for label, got, exp in driver(golden(name), make_amd, DEV):
         S.assert_bitwise(f"{name}:{label}", got, exp)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.FEDOPT_FIXTURES)
 def test_golden_fedopt(golden, name):
     for label, got, exp in S.run_fedopt(golden(name), make_amd, DEV):
@@ -48,6 +50,7 @@ def test_golden_fedopt(golden, name):
             S.assert_close_fedopt(f"{name}:{label}", got, exp, elementwise=rnd <= 1)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.FEDOPT_FIXTURES)
 def test_golden_fedopt_single_round_elementwise(golden, name):
     """Each adaptive round from the reference's own state: elementwise 1e-6 (avg bitwise)."""
@@ -67,6 +70,7 @@ def test_golden_fedopt_single_round_elementwise(golden, name):
             S.assert_close_fedopt(f"{name}:r{r}/{key}", S.to_cpu(got), exp[key])
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.FEDOPT_EAGER_FIXTURES)
 def test_golden_fedopt_eager(golden, name):
     """FedAdam / FedYogi driven by the eager top aggregator (same base object every arrival):
@@ -74,6 +78,7 @@ def test_golden_fedopt_eager(golden, name):
     S.check_fedopt_eager(S.run_fedopt_eager(golden(name), make_amd, DEV))
 
 
+@pytest.mark.oracle
 def test_golden_feddyn_pingpong(golden):
     """FedDyn with ping-pong tiled history stores == the reference fixture, bitwise."""
     def make(sort, **kw):
@@ -82,12 +87,14 @@ def test_golden_feddyn_pingpong(golden):
         S.assert_bitwise(f"feddyn_pingpong:{label}", got, exp)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.HIER_FIXTURES)
 def test_golden_hier_torch_delta(golden, name):
     for label, got, exp in S.run_hier(golden(name), make_amd, DEV, S.delta_torch):
         S.assert_bitwise(f"{name}:{label}", got, exp)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.HIER_FIXTURES)
 def test_golden_hier_fused_delta(golden, name):
     """Middle aggregator using the fused scale_add+delta kernel."""
@@ -109,6 +116,7 @@ def test_golden_hier_fused_delta(golden, name):
         S.assert_bitwise(f"m{mid}/delta", delta, fx.weights(f"m{mid}/delta"))
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("name", S.HIER_FIXTURES)
 @pytest.mark.parametrize("update_middle_weights", [True, False])
 def test_golden_hier_one_pass(golden, name, update_middle_weights):
@@ -168,6 +176,7 @@ def test_synth_device_matches_host():
             assert np.array_equal(t.numpy().view(np.uint32), h.view(np.uint32))
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64,
                                    torch.int64, torch.int32])
 @pytest.mark.parametrize("numel", [0, 1, 3, 1023, 1024, 4099, 70_001])
@@ -192,6 +201,7 @@ def test_reduce_vs_oracle_dtypes(dtype, numel):
     S.assert_bitwise(f"{dtype}/{numel}", out, {"x": exp})
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_low_residency_reduction_vs_oracle(dtype):
     """flame_agg_reduce's 2-workgroups-per-CU instantiation (FLAME_LO_CU / FLAME_LO_CU16: launches of
@@ -218,6 +228,7 @@ def test_low_residency_reduction_vs_oracle(dtype):
     S.assert_bitwise(f"low-residency {dtype}", out, exp)
 
 
+@pytest.mark.oracle
 def test_c2_256x1M_bitwise():
     """Config 2: 256 clients x (1,000,000 + 4,099) fp32, counts U{1..1000}, seed 1."""
     from flame_amd import synth
@@ -247,6 +258,7 @@ def test_c2_256x1M_bitwise():
         S.assert_bitwise(f"c2/{k}", {k: out[k]}, {k: exp})
 
 
+@pytest.mark.oracle
 def test_unaligned_and_strided_and_host_base():
     """Views at odd offsets (scalar path), non-contiguous base, CPU-resident base."""
     O = _oracle()
@@ -293,6 +305,7 @@ def test_fedbuff_errors_and_int_scale_add():
                                   {"n": torch.ones(3, dtype=torch.int64, device=DEV)}, 2)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
 def test_fedopt_vs_oracle_random(sort):
     """Four rounds at N=64, P=300,001 fp32 (+ an int64 buffer on the generic path)."""
@@ -323,6 +336,7 @@ def test_fedopt_vs_oracle_random(sort):
     assert wa["nbt"].dtype == torch.float32  # the reference promotes int buffers in the adaptive step
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_fedbuff_stream_vs_oracle(dtype):
     """FedBuff: 12 single-entry do() calls with staleness 0..3, then scale_add (+delta)."""
@@ -363,6 +377,7 @@ def _full_size_columns(P, T, seed):
     return np.unique(np.concatenate([whole, rand, [0, P - 1]])), len(whole)
 
 
+@pytest.mark.oracle
 def test_c3_full_size_every_element():
     """Config 3 at full size (1024 x 25M fp32 = 102.4 GB in HBM, the tiled slab the
     headline runs on): EVERY one of the 25M outputs equals the C oracle (fedavg.py:79-104 op
@@ -479,6 +494,7 @@ def test_fedbuff_fused_scale_add(dtype, placement, with_delta):
     S.assert_bitwise("aggregate read afterwards", res[True][2], res[False][2])
 
 
+@pytest.mark.oracle
 def test_zero_copy_pinned_host_clients():
     """Pinned host updates are streamed by the kernel directly (no staging copy): bitwise."""
     O = _oracle()
@@ -498,6 +514,7 @@ def test_zero_copy_pinned_host_clients():
     S.assert_bitwise("zerocopy", S.to_cpu(out), {"x": exp})
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("where", ["bytes", "pinned", "cache_hbm", "cache_host", "cache_slab"])
 def test_ingest_wire_payloads_to_fedavg(where):
     """Channel payloads (cloudpickle, channel.py:203-218) -> ingest.decode (zero-copy) ->
@@ -542,6 +559,7 @@ def _slab_model(g):
             "mat": torch.randn(33, 65, generator=g), "nbt": torch.tensor(7, dtype=torch.int64)}
 
 
+@pytest.mark.oracle
 def test_slab_tiled_fedavg_bitwise_and_slot_reuse():
     """Updates in the tiled UpdateSlab (client_tile_stride path) == oracle, bitwise; slots
     released after the round are reused by the next one."""
@@ -575,6 +593,7 @@ def test_slab_tiled_fedavg_bitwise_and_slot_reuse():
         assert len(slab._free) == 40, "slots must return after the round"
 
 
+@pytest.mark.oracle
 def test_slab_fedopt_and_fedbuff_tiled():
     from flame_amd.slab import UpdateSlab
     O = _oracle()
@@ -610,6 +629,7 @@ def test_slab_fedopt_and_fedbuff_tiled():
     S.assert_bitwise("slab fedbuff", S.to_cpu(aa), ao)
 
 
+@pytest.mark.oracle
 def test_registered_shared_memory_payloads_zero_copy():
     """Payloads in a registered mmap (stand-in for the LIFL shm segment) are decoded in
     place and read by the kernel over PCIe: no host copy anywhere, result bitwise."""
@@ -644,6 +664,7 @@ def test_registered_shared_memory_payloads_zero_copy():
         del cache, msg
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_fedopt_fused_reduced_precision_vs_reference_ops(sort, dtype):
@@ -693,6 +714,7 @@ def _dyn_update(g, tmpl, i, scale=1e-2):
             else torch.tensor(i, dtype=v.dtype) for k, v in tmpl.items()}
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("placement,order,history", [
     ("hbm", "sorted", "rows"), ("slab", "sorted", "rows"), ("hbm", "shuffled", "rows"), ("slab", "shuffled", "rows"),
     ("hbm", "sorted", "pingpong"), ("slab", "shuffled", "pingpong"), ("slab", "shuffled", "pingpong_rows")])
@@ -742,6 +764,7 @@ def test_feddyn_vs_oracle_partial_participation(placement, order, history):
             S.assert_bitwise(f"feddyn/{placement}/hist/{e}", S.to_cpu(amd.local_param_dict[e]), h)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("history", ["pingpong", "pingpong_rows"])
 def test_feddyn_pingpong_key_leaves_and_returns(history):
     """under history="pingpong" a key whose arrival comes in another dtype takes the
@@ -787,6 +810,7 @@ def test_feddyn_pingpong_key_leaves_and_returns(history):
         wa, wo = amd.cld_model, ora.cld_model
 
 
+@pytest.mark.oracle
 def test_scaffold_vs_oracle_rounds():
     """SCAFFOLD drop-in == oracle bitwise: c_glob (HBM-resident, updated in place) and the
     model over 3 rounds, including an int buffer whose control variate arrives as fp32, and
@@ -830,6 +854,7 @@ def test_scaffold_vs_oracle_rounds():
         assert all(t.is_cuda for t in amd.c_glob.values())
 
 
+@pytest.mark.oracle
 def test_f16_product_keeps_two_roundings():
     """torch computes an fp16 `v * rate` as fp32 product -> fp16 (two roundings).  Inputs are
     chosen where one rounding of the exact product differs (what v_fma_mixlo_f16 would give),
@@ -854,6 +879,7 @@ def test_f16_product_keeps_two_roundings():
     S.assert_bitwise("f16 product torch", {"x": out}, {"x": torch.zeros_like(vs) + vs * rate})
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_middle_group_flush_and_scale_add_many(dtype):
     """Co-located middle aggregators: flush_aggregates + scale_add_many (FLAME_AGG_SEG_RATES,
@@ -907,6 +933,7 @@ def test_middle_group_flush_and_scale_add_many(dtype):
         S.assert_bitwise(f"oracle base m{m}", S.to_cpu(gb[m]), ob)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("placement", ["slab", "tensors", "mixed"])
 @pytest.mark.parametrize("top_start", ["none", "existing"])
@@ -990,6 +1017,7 @@ def test_hierarchy_round_one_pass(dtype, placement, top_start, M, path, monkeypa
     S.assert_bitwise("oracle top w", fused[3], tw)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("placement", ["slab", "tensors"])
 @pytest.mark.parametrize("start", ["none", "existing"])
@@ -1042,6 +1070,7 @@ def test_fedbuff_do_arrivals_equals_per_do(dtype, placement, start, defer):
         S.assert_bitwise(f"do_arrivals/{lbl}", a, b)
 
 
+@pytest.mark.oracle
 def test_hierarchy_round_from_batched_arrivals_vs_fixture(golden):
     """The reference-generated 2 x 3 hierarchy (hier_fedbuff_small.npz) with each middle's
     arrivals handed over in ONE FedBuff.do_arrivals call, then one hierarchy_round launch:
@@ -1174,6 +1203,7 @@ def test_metric_collector_receives_kernel_metrics():
     assert sd["fedadam.flame_fedopt_reduce_adapt.hbm_GBps"] > 0
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("where", ["zero_copy", "device_cache"])
 def test_shm_receiver_registered_segment_to_fedavg(where):
     """LIFL SHM receive without host copies (flame_amd.ingest.ShmReceiver): each sender's
@@ -1213,6 +1243,7 @@ def test_shm_receiver_registered_segment_to_fedavg(where):
             seg.unlink()
 
 
+@pytest.mark.oracle
 def test_golden_nonfinite(golden):
     """nonfinite.npz, generated by the reference: the HIP path puts NaN and +-inf where the
     reference's torch-CPU ops do (FedAvg, FedBuff aggregate, FedBuff scale_add; f32 / bf16 /
@@ -1224,6 +1255,7 @@ def test_golden_nonfinite(golden):
     assert n == 12
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 def test_nonfinite_updates_match_oracle(dtype):
     """A diverged trainer (NaN, +-inf, overflowing sums): FedAvg and FedBuff + scale_add put
@@ -1256,6 +1288,7 @@ def test_nonfinite_updates_match_oracle(dtype):
     S.assert_same_nonfinite(f"fedbuff {dtype}", w["w"], ow["w"])
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("with_delta,slab", [(True, False), (False, False), (True, True)])
 def test_sync_hierarchy_golden(golden, with_delta, slab):
     """sync_hierarchy_round (one FLAME_HIER_SYNC launch per float dtype; the int64 key
@@ -1273,6 +1306,7 @@ def test_sync_hierarchy_golden(golden, with_delta, slab):
     assert sum(1 for ev in launches if ev[0] == "flame_hier_fedbuff") == 3 * 2   # f32, bf16, f16 x 2 rounds
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("M", [8, 20])
 @pytest.mark.parametrize("path", ["argmeta", "table"])
 def test_sync_hierarchy_vs_oracle_readonly_middles(M, path, monkeypatch):
@@ -1380,6 +1414,7 @@ def test_sharded_fedadam_two_ranks_one_gpu():
     assert res == {0: True, 1: True}, res
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("variant", ["fedadam", "fedyogi", "fedadagrad"])
 def test_c4_full_size_every_element(variant):
     """Config 4 at full size (FedAdam / FedYogi / FedAdaGrad, 1024 x 25M fp32 in a tiled slab, round 1
@@ -1449,6 +1484,7 @@ def test_c4_full_size_every_element(variant):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.oracle
 def test_c5_full_size_hierarchy_every_element():
     """Config 5's per-GPU shard at full size (64 middles x 64 arrivals x 15.625M bf16 = 128 GB
     in a tiled slab, staleness 0..3): ONE hierarchy_round launch; EVERY element of every
@@ -1528,6 +1564,7 @@ def test_mnist_example_config1():
     assert mod.run(rounds=3, verbose=False)
 
 
+@pytest.mark.oracle
 def test_integration_ctypes_stub_runs():
     """The reference-side ctypes stub printed in INTEGRATION.md §2 works as written
     (library path substituted) and equals the oracle's FedAvg, bitwise."""
@@ -1554,6 +1591,7 @@ def test_integration_ctypes_stub_runs():
     S.assert_bitwise("ctypes stub", {"x": dev_agg}, {"x": exp})
 
 
+@pytest.mark.oracle
 def test_empty_and_tiny_keys_every_path():
     """Models with 0-element and 1-element tensors between ordinary ones: FedAvg, FedAdam,
     FedBuff (fused scale_add), FedDyn and the sync hierarchy all match the oracle, bitwise
@@ -1624,6 +1662,7 @@ def test_empty_and_tiny_keys_every_path():
     S.assert_bitwise("sync top", S.to_cpu(top), exp_top)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64])
 def test_argmeta_launch_equals_device_table_launch(dtype):
     """Small launches pass the metadata as a kernel argument (flame_agg_reduce_argmeta); the
@@ -1665,6 +1704,7 @@ def test_argmeta_launch_equals_device_table_launch(dtype):
         S.assert_bitwise(f"oracle/{dtype}/{j}", {"x": results[True][0][j]}, {"x": exp})
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_many_clients_one_launch(dtype):
     """The largest flat reduction the BASELINE configs imply: all 4096 clients of config 5
@@ -1714,22 +1754,30 @@ def test_many_clients_one_launch(dtype):
     S.assert_bitwise(f"fedbuff {m} arrivals {dtype}", {k: agg[k] for k in shapes}, exp)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_fedopt_argmeta_equals_device_table(sort, dtype):
     """Small FedOPT rounds pass their metadata as a kernel argument
-    (flame_fedopt_reduce_adapt_argmeta): three rounds (passthrough, zero state, running
-    state) equal the device-table launches bitwise."""
+    (flame_fedopt_reduce_adapt_argmeta); with engine.ARGMETA off they take the device-table
+    launch (flame_fedopt_reduce_adapt, one chunk per workgroup).  Three rounds (passthrough,
+    zero state, running state): the two launches equal each other bitwise, and each round of
+    both equals OracleFedOPT.do (fedopt.py:58-129) from the same state at the round's start --
+    the average bitwise, current / m / v within the §8(c) contract (fp32) or one ulp (bf16)."""
     from flame_amd import engine
+    O = _oracle()
     g = torch.Generator().manual_seed(17)
     shapes = {"w": (300, 7), "b": (7,), "e": (0,), "t": (4099,)}
     w0 = {k: torch.randn(s, generator=g, dtype=torch.float64).to(dtype) for k, s in shapes.items()}
     rounds = [[({k: (w0[k].double() + torch.randn(s, generator=g, dtype=torch.float64) * 1e-2).to(dtype)
                  for k, s in shapes.items()}, int(c)) for c in torch.randint(1, 500, (5,), generator=g)]
               for _ in range(3)]
+    from flame_amd import _native
+    dt = {torch.float32: "f32", torch.bfloat16: "bf16"}[dtype]
     results = {}
     for argmeta in (True, False):
         engine.ARGMETA = argmeta
+        before = _native.launch_branch_counts()
         try:
             opt = make_amd(sort)
             w = {k: v.to(DEV) for k, v in w0.items()}
@@ -1739,12 +1787,49 @@ def test_fedopt_argmeta_equals_device_table(sort, dtype):
                 for i, (u, c) in enumerate(arrivals):
                     cache[f"{i:03d}"] = S.TR({k: v.to(DEV) for k, v in u.items()}, c)
                 w = opt.do({k: v.clone() for k, v in w.items()}, cache, total=sum(c for _, c in arrivals))
-                outs.append({k: v.cpu() for k, v in w.items()})
+                outs.append([S.to_cpu(dict(x)) if x is not None else None
+                             for x in (w, opt.agg_weights, opt.m_t, opt.v_t)])
             results[argmeta] = outs
         finally:
             engine.ARGMETA = True
+        after = _native.launch_branch_counts()
+        hits = {k: after[k] - before.get(k, 0) for k in after
+                if after[k] != before.get(k, 0) and k.startswith("flame_fedopt")}
+        want = f"flame_fedopt_reduce_adapt{'_argmeta' if argmeta else ''}/{dt}/{sort}"
+        assert hits == {want: 2}, hits          # rounds 2 and 3 (round 1 is the passthrough)
     for r, (a, b) in enumerate(zip(results[True], results[False])):
-        S.assert_bitwise(f"{sort}/{dtype}/round{r}", a, b)
+        for lbl, x, y in zip(("cur", "avg", "m", "v"), a, b):
+            if y is not None:
+                S.assert_bitwise(f"{sort}/{dtype}/round{r}/{lbl}", x, y)
+    ulp = 2.0 ** -7
+    for argmeta, outs in results.items():
+        ora = O.OracleFedOPT(sort)
+        prev = {k: v.clone() for k, v in w0.items()}
+        for r, arrivals in enumerate(rounds):
+            if r >= 1:
+                ora.current_weights = {k: v.clone() for k, v in outs[r - 1][0].items()}
+            if r >= 2:
+                ora.m_t = {k: v.clone() for k, v in outs[r - 1][2].items()}
+                ora.v_t = {k: v.clone() for k, v in outs[r - 1][3].items()}
+            cache = S.SortedCache()
+            for i, (u, c) in enumerate(arrivals):
+                cache[f"{i:03d}"] = S.TR({k: v.clone() for k, v in u.items()}, c)
+            exp = ora.do({k: v.clone() for k, v in prev.items()}, cache, total=sum(c for _, c in arrivals))
+            cur, avg, m, v = outs[r]
+            lbl = f"oracle/{sort}/{dtype}/argmeta={argmeta}/round{r}"
+            S.assert_bitwise(f"{lbl}/avg", avg, ora.agg_weights)
+            for name, x, y in (("cur", cur, exp), ("m", m, ora.m_t), ("v", v, ora.v_t)):
+                if r == 0 and name != "cur":
+                    assert x is None and y is None, (lbl, name)
+                    continue
+                if dtype == torch.float32:
+                    S.assert_close_fedopt(f"{lbl}/{name}", x, y)
+                else:
+                    for k in y:
+                        gg, ee = x[k].double(), y[k].double()
+                        bad = ((gg - ee).abs() > ee.abs() * ulp + 1e-30).nonzero().flatten()
+                        assert bad.numel() == 0, f"{lbl}/{name}/{k}: {bad.numel()} beyond one ulp"
+            prev = {k: t.clone() for k, t in cur.items()}
 
 
 @pytest.mark.parametrize("sort", ["fedadam", "fedyogi", "fedadagrad"])
@@ -1788,6 +1873,7 @@ def test_fedopt_split_launch_equals_fused(sort, case):
             S.assert_bitwise(f"{sort}/{case}/round{r}/{lbl}", x, y)
 
 
+@pytest.mark.oracle
 def test_key_subset_arrivals():
     """Updates carrying a SUBSET of the model's keys (fedavg.py:93 / fedbuff.py:143 add
     ``for k, v in tres.weights.items()``: a key a client did not send keeps its value).
@@ -1868,6 +1954,7 @@ def test_key_subset_arrivals():
             S.assert_close_fedopt(f"fedadam subsets r{r}", cur, ecur, elementwise=r == 1)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("sort", ["fedadam", "fedyogi"])
 def test_fedopt_multichunk_multikey(sort):
     """FedOPT launches large enough for the 8-chunks-per-workgroup build (>= 16,384 fp32

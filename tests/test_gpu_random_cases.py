@@ -238,6 +238,7 @@ def _run_fedopt_eager(rng, keys, placement, n, label):
         wa, wo = oa, oo
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("case", range(N_CASES))
 def test_random_case_vs_oracle(case):
     rng, sort, keys, placement, n = _draw_case(case)
@@ -393,6 +394,7 @@ def _run_hier_sync(rng, keys, arrivals, placement, label):
             S.assert_bitwise(f"{label}/delta{m}", S.to_cpu(deltas[m]), odeltas[m])
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("case", range(N_HIER))
 def test_random_hierarchy_vs_oracle(case, monkeypatch):
     """The co-located hierarchies (flame_hier_fedbuff: async FedBuff middles + top, and the
@@ -511,6 +513,7 @@ def _run_scaffold(rng, label):
         S.assert_bitwise(f"{label}/r{r}/c_glob", S.to_cpu(amd.c_glob), ora.c_glob)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("case", range(N_STATEFUL))
 def test_random_stateful_vs_oracle(case):
     """FedDyn (partial participation, ends leaving and returning, an unlisted end, the channel's

@@ -71,6 +71,7 @@ def _run(consume):
         snd.close()
 
 
+@pytest.mark.oracle
 def test_fedbuff_deferred_arrival_survives_segment_rewrite():
     from oracle import oracle as Ora
     opt = S_make("fedbuff")
@@ -86,6 +87,7 @@ def test_fedbuff_deferred_arrival_survives_segment_rewrite():
     S.assert_bitwise("fedbuff/shm", got, exp)
 
 
+@pytest.mark.oracle
 def test_fedavg_zero_copy_read_finishes_before_do_returns():
     from oracle import oracle as Ora
     g = torch.Generator().manual_seed(3)
@@ -103,6 +105,7 @@ def test_fedavg_zero_copy_read_finishes_before_do_returns():
     S.assert_bitwise("fedavg/shm", got, exp)
 
 
+@pytest.mark.oracle
 @pytest.mark.parametrize("placement", ["slab", "hbm", "host"])
 def test_device_update_cache_copy_completes_before_setitem_returns(placement):
     from flame_amd import ingest

@@ -148,6 +148,7 @@ def test_slab_write_entry_points_direct():
     assert b"dst_tile_stride" in L.flame_last_error()
 
 
+@pytest.mark.oracle
 def test_decoded_payloads_one_transfer_each_and_pinned_ring():
     """Channel payloads decoded zero-copy (ingest.decode) into a slab-placed DeviceUpdateCache:
     each update's tensors -- views into one pageable payload -- cross PCIe as ONE span, staged

@@ -5,6 +5,7 @@ No GPU: this pins the restatement the GPU tests compare against."""
 import pytest
 import torch
 
+from oracle import consult
 from oracle import oracle as O
 
 DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32,
@@ -22,6 +23,8 @@ def _rand(g, dt, n, scale):
 
 
 def _reference(acc, v, rate):
+    """The reference's add (fedavg.py:93-104) in torch CPU ops: a checker (consult.py)."""
+    consult.note()
     tmp = v * rate
     tmp = tmp.to(dtype=v.dtype) if tmp.dtype != v.dtype else tmp
     acc += tmp

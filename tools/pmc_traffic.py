@@ -42,6 +42,9 @@ def main():
                     help="bench.py workload the passes ran (part of the entry's key: FedAdam / FedYogi / "
                          "FedAdaGrad share a kernel name)")
     ap.add_argument("--itemsize", type=int, default=4, help="bytes per element (bf16: 2)")
+    ap.add_argument("--source", default=None,
+                    help="where the counters came from (committed CSVs under profiles/ + run id); bench.py "
+                         "copies it into roofline.traffic_source")
     ap.add_argument("--extra-arrays", type=int, default=2,
                     help="P-sized arrays besides the N clients in the algorithmic bytes (FedAvg 2, FedOPT 8)")
     a = ap.parse_args()
@@ -62,6 +65,7 @@ def main():
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": (read_b + write_b) / algo,
         "correction": "read = 2*FETCH_SIZE KiB (gfx950 half-count on 16B/lane streams), write = WRITE_SIZE KiB",
+        "source": a.source or f"rocprofv3 --pmc FETCH_SIZE: {a.fetch}; --pmc WRITE_SIZE: {a.write}",
     }
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     # the file holds one entry per (kernel, clients, params, layout); replace ours
