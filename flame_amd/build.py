@@ -17,6 +17,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "fedagg.hip")
 HDR = os.path.join(ROOT, "include", "flame_amd.h")
+DEPS = (SRC, HDR, os.path.join(PKG, "csrc", "fastmath.h"))
 LIB = os.path.join(PKG, "libflame_amd.so")
 # The kernel source WITH its compile-time sweep switches (default-off variants, diagnostics that
 # skip work): tools/kernel_sweep.py / hier_sweep.py build it into build/variants, never into LIB.
@@ -44,7 +45,7 @@ def stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR))
+    return any(os.path.getmtime(p) > t for p in DEPS)
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:

@@ -1,0 +1,52 @@
+// fastmath.h -- correctly rounded fp32 sqrt / reciprocal / divide for the operands the FedOPT
+// step meets in practice (adapt_vec in fedagg.hip), cheaper than the general sequences LLVM
+// emits for __builtin_sqrtf / __fdiv_rn, which also cover denormal, tiny, huge, inf and NaN
+// operands (16 and 13 instructions, two of them quarter-rate, and none of them packable).
+//
+// Each function returns the SAME bits as the general sequence on the operands its admission
+// predicate accepts; the caller takes the general sequence for a wave where any lane's operand
+// is not admitted.  tools/fp_probe.py checks the equality on the MI355X: exhaustively for sqrt_rn
+// (every admitted x) and rcp_rn (every admitted b), and on 2^39 counter-drawn admitted pairs for
+// div_rn (profiles/r05_fp_probe.log).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace flame_fm {
+
+// RN(sqrt(x)) for x = +0 or 2^-96 <= x <= 2^78: from v_rsq_f32, s = x*y, h = y/2 and one
+// Newton step on the root with the residual x - s*s exact by fma.  (v_sqrt_f32 alone is one ulp
+// off on 15 % of the normals.)  rsq(+0) = +inf is clamped so that +0 maps to +0.
+__device__ __forceinline__ bool sqrt_admits(float x) {
+    return (__float_as_uint(x) == 0u) | ((x >= 0x1p-96f) & (x <= 0x1p78f));
+}
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+    const float s = x * y;
+    const float h = 0.5f * y;
+    const float r = __builtin_fmaf(-s, s, x);
+    return __builtin_fmaf(r, h, s);
+}
+
+// RN(1/b) for 2^-20 <= b <= 2^40: the 1-ulp v_rcp_f32 and one Markstein correction.
+__device__ __forceinline__ float rcp_rn(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y0, 1.0f);
+    return __builtin_fmaf(e, y0, y0);
+}
+
+// RN(a/b) for 2^-20 <= b <= 2^40 and a = +-0 or 2^-85 <= |a| <= 2^100 (Markstein's theorem:
+// y = RN(1/b), q0 = RN(a*y) within one ulp, the residual b*q0 - a exact, q = RN(q0 - r*y);
+// 1/b, q0 and q are normal there).  The residual is taken negated so that a = +-0 gives +-0
+// with a's sign, as IEEE division does.
+__device__ __forceinline__ bool div_admits(float a) {
+    const float aa = __builtin_fabsf(a);
+    return (aa == 0.f) | ((aa >= 0x1p-85f) & (aa <= 0x1p100f));
+}
+__device__ __forceinline__ float div_rn(float a, float b) {
+    const float y = rcp_rn(b);
+    const float q0 = a * y;
+    const float rn = __builtin_fmaf(b, q0, -a);
+    return __builtin_fmaf(-rn, y, q0);
+}
+
+}  // namespace flame_fm

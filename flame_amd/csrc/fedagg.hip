@@ -34,46 +34,112 @@
 #include <type_traits>
 
 #include "../../include/flame_amd.h"
+#include "fastmath.h"
 
 namespace {
 
-// Tunables: fixed for the shipped build (each chosen by an interleaved A/B sweep on MI355X,
-// DESIGN.md §4).  The sweep source tools/sweep/fedagg_sweep.hip exposes them -- and the
-// variants measured no faster, which this file no longer carries -- as -D switches.
+// Tunables, each chosen by an interleaved A/B sweep on MI355X.  The product build
+// (flame_amd/build.py) passes no -D: these defaults ARE the shipped kernel.  The sweep tools
+// (tools/hier_sweep.py, tools/chain_sweep.py, ...) build variants of THIS source with -DFLAME_T_*
+// overrides into build/, so a sweep always measures the shipped code with one knob moved.
 constexpr int kBlock = 256;          // lanes per workgroup of the reduction kernels
 constexpr int kVPT = 1;              // 16-byte vectors per lane per client
-constexpr int kClientUnroll = 8;     // clients whose loads are issued together per lane (full residency)
-constexpr int kClientUnroll16 = 8;   // the same for 16-bit dtypes (8 elements per lane vector)
+#ifndef FLAME_T_CLIENT_UNROLL
+#define FLAME_T_CLIENT_UNROLL 8
+#endif
+constexpr int kClientUnroll = FLAME_T_CLIENT_UNROLL;     // clients whose loads are issued together per lane (full residency)
+#ifndef FLAME_T_CLIENT_UNROLL16
+#define FLAME_T_CLIENT_UNROLL16 8
+#endif
+constexpr int kClientUnroll16 = FLAME_T_CLIENT_UNROLL16;   // the same for 16-bit dtypes (8 elements per lane vector)
 // flame_agg_reduce, launches of >= kLoMinClients clients over >= kLoMinChunks chunks: 2 workgroups
 // per CU (kLoLds of dynamic LDS, unused) with a client unroll of 3 (16-bit: 4) -- fewer loads in
 // flight read HBM faster (C3: 14.90 -> 14.18 ms, 99 % of a region probe at that residency;
 // profiles/r03ze_c3_sweep.log, r03zf_c3_sweep.log, r03zf_c3_bf16_sweep.log)
-constexpr int kLoUnroll = 3;
-constexpr int kLoUnroll16 = 4;
-constexpr int kLoLds = 65536;
-constexpr int kLoMinClients = 64;    // 64 x 100M fp32: 4.04 -> 3.90 ms (profiles/r03zn_c64_lomin.log)
-constexpr int64_t kLoMinChunks = 4096;
+#ifndef FLAME_T_LO_UNROLL
+#define FLAME_T_LO_UNROLL 3
+#endif
+constexpr int kLoUnroll = FLAME_T_LO_UNROLL;
+#ifndef FLAME_T_LO_UNROLL16
+#define FLAME_T_LO_UNROLL16 4
+#endif
+constexpr int kLoUnroll16 = FLAME_T_LO_UNROLL16;
+#ifndef FLAME_T_LO_LDS
+#define FLAME_T_LO_LDS 65536
+#endif
+constexpr int kLoLds = FLAME_T_LO_LDS;
+#ifndef FLAME_T_LO_MIN_CLIENTS
+#define FLAME_T_LO_MIN_CLIENTS 64
+#endif
+constexpr int kLoMinClients = FLAME_T_LO_MIN_CLIENTS;    // 64 x 100M fp32: 4.04 -> 3.90 ms (profiles/r03zn_c64_lomin.log)
+#ifndef FLAME_T_LO_MIN_CHUNKS
+#define FLAME_T_LO_MIN_CHUNKS 4096
+#endif
+constexpr int64_t kLoMinChunks = FLAME_T_LO_MIN_CHUNKS;
 // FedOPT (fp32, >= 8 x 256 x kOptWGC chunks): kOptWGC chunks per workgroup, their avg/m/v/cur
 // blocks held in LDS (16 KiB per chunk -> 2 workgroups per CU) and stored in one burst at the end,
 // client unroll kOptUnroll (profiles/r02_fedopt_wgc_sweep.log, r03zf_c4_sweep.log, r03zg_c4_sweep.log)
-constexpr int kOptWGC = 4;
-constexpr int kOptUnroll = 3;
+#ifndef FLAME_T_OPT_WGC
+#define FLAME_T_OPT_WGC 4
+#endif
+constexpr int kOptWGC = FLAME_T_OPT_WGC;
+#ifndef FLAME_T_OPT_UNROLL
+#define FLAME_T_OPT_UNROLL 3
+#endif
+constexpr int kOptUnroll = FLAME_T_OPT_UNROLL;
 // hierarchy kernel: register store groups of kHB middles (16-bit client unroll kHierUnroll16);
 // launches of >= kHLdsMinMids middles hold store groups of kHBL middles in LDS (4 KiB each per
 // workgroup, 2 workgroups per CU) with a 16-bit unroll of kHierLdsUnroll16 (C5 shard 20.99 ->
 // 19.51 ms, profiles/r02_hier_lds_sweep.log); one middle over >= 64 arrivals and >= 4,096 chunks
 // (a FedBuff aggregator's fused scale_add): low residency, unroll 3 (profiles/r03zv_fedbuff_*.log)
-constexpr int kHB = 8;
-constexpr int kHierUnroll16 = 4;
-constexpr int kHBL = 16;
-constexpr int kHierLdsUnroll16 = 6;
-constexpr int kHLdsMinMids = 16;
-constexpr int kHLoUnroll = 3;
-constexpr int kHLoMinClients = 64;
-constexpr int64_t kHLoMinChunks = 4096;
-constexpr int kHLoLdsF32 = 65536;    // 2 workgroups per CU
-constexpr int kHLoLds16 = 53248;     // 3 workgroups per CU
-constexpr int kDynUnroll = 4;        // FedDyn kernel: program steps whose loads are issued together
+#ifndef FLAME_T_HB
+#define FLAME_T_HB 8
+#endif
+constexpr int kHB = FLAME_T_HB;
+#ifndef FLAME_T_HIER_UNROLL16
+#define FLAME_T_HIER_UNROLL16 4
+#endif
+constexpr int kHierUnroll16 = FLAME_T_HIER_UNROLL16;
+#ifndef FLAME_T_HBL
+#define FLAME_T_HBL 16
+#endif
+constexpr int kHBL = FLAME_T_HBL;
+#ifndef FLAME_T_HIER_LDS_UNROLL16
+#define FLAME_T_HIER_LDS_UNROLL16 6
+#endif
+constexpr int kHierLdsUnroll16 = FLAME_T_HIER_LDS_UNROLL16;
+#ifndef FLAME_T_HLDS_MIN_MIDS
+#define FLAME_T_HLDS_MIN_MIDS 16
+#endif
+constexpr int kHLdsMinMids = FLAME_T_HLDS_MIN_MIDS;
+#ifndef FLAME_T_HIER_WS
+#define FLAME_T_HIER_WS 0
+#endif
+constexpr bool kHierWS = FLAME_T_HIER_WS;   // >= kHLdsMinMids async middles: a fifth wave runs the epilogues
+#ifndef FLAME_T_HLO_UNROLL
+#define FLAME_T_HLO_UNROLL 3
+#endif
+constexpr int kHLoUnroll = FLAME_T_HLO_UNROLL;
+#ifndef FLAME_T_HLO_MIN_CLIENTS
+#define FLAME_T_HLO_MIN_CLIENTS 64
+#endif
+constexpr int kHLoMinClients = FLAME_T_HLO_MIN_CLIENTS;
+#ifndef FLAME_T_HLO_MIN_CHUNKS
+#define FLAME_T_HLO_MIN_CHUNKS 4096
+#endif
+constexpr int64_t kHLoMinChunks = FLAME_T_HLO_MIN_CHUNKS;
+#ifndef FLAME_T_HLO_LDS_F32
+#define FLAME_T_HLO_LDS_F32 65536
+#endif
+constexpr int kHLoLdsF32 = FLAME_T_HLO_LDS_F32;    // 2 workgroups per CU
+#ifndef FLAME_T_HLO_LDS16
+#define FLAME_T_HLO_LDS16 53248
+#endif
+constexpr int kHLoLds16 = FLAME_T_HLO_LDS16;     // 3 workgroups per CU
+#ifndef FLAME_T_DYN_UNROLL
+#define FLAME_T_DYN_UNROLL 4
+#endif
+constexpr int kDynUnroll = FLAME_T_DYN_UNROLL;        // FedDyn kernel: program steps whose loads are issued together
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -444,12 +510,11 @@ template <int DT> __device__ __forceinline__ float rnd(float x) {
     else return x;
 }
 
-// One element of fedopt.py:106-129 (+ the _delta_v variants), each torch op rounded in the
-// tensor's dtype.  `tau` arrives pre-rounded to the dtype for bf16/fp16 (torch-CPU rounds a
-// Python scalar to a reduced-precision tensor's dtype before + and -, not before * and /).
+// fedopt.py:106-129 (+ the _delta_v variants) up to the square root: d, the new m and v, and
+// the numerator eta * m, each torch op rounded in the tensor's dtype.
 template <int DT, int VARIANT>
-__device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float& v, float& cur_out,
-                                           float b1, float omb1, float b2, float omb2, float eta, float tau) {
+__device__ __forceinline__ void adapt_moments(float avg, float cur, float& m, float& v, float& num, float b1,
+                                              float omb1, float b2, float omb2, float eta) {
     const float d = rnd<DT>(__fsub_rn(avg, cur));
     const float mn = rnd<DT>(__fadd_rn(rnd<DT>(__fmul_rn(b1, m)), rnd<DT>(__fmul_rn(omb1, d))));
     const float d2 = rnd<DT>(__fmul_rn(d, d));
@@ -462,12 +527,56 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
     } else {
         vn = rnd<DT>(__fadd_rn(v, d2));
     }
-    // __builtin_sqrtf is correctly rounded; the __fsqrt_rn builtin lowers to the 1-ulp v_sqrt_f32
-    const float den = rnd<DT>(__fadd_rn(rnd<DT>(__builtin_sqrtf(vn)), tau));
-    const float q = rnd<DT>(__fdiv_rn(rnd<DT>(__fmul_rn(eta, mn)), den));
     m = mn;
     v = vn;
-    cur_out = rnd<DT>(__fadd_rn(cur, q));
+    num = rnd<DT>(__fmul_rn(eta, mn));
+}
+
+// One element of fedopt.py:106-129, each torch op rounded in the tensor's dtype.  `tau` arrives
+// pre-rounded to the dtype for bf16/fp16 (torch-CPU rounds a Python scalar to a reduced-precision
+// tensor's dtype before + and -, not before * and /).  The general correctly rounded sqrt and
+// divide (__builtin_sqrtf is correctly rounded; the __fsqrt_rn builtin lowers to the 1-ulp
+// v_sqrt_f32): the scalar tail path, and adapt_vec's fallback.
+template <int DT, int VARIANT>
+__device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float& v, float& cur_out,
+                                           float b1, float omb1, float b2, float omb2, float eta, float tau) {
+    float num;
+    adapt_moments<DT, VARIANT>(avg, cur, m, v, num, b1, omb1, b2, omb2, eta);
+    const float den = rnd<DT>(__fadd_rn(rnd<DT>(__builtin_sqrtf(v)), tau));
+    cur_out = rnd<DT>(__fadd_rn(cur, rnd<DT>(__fdiv_rn(num, den))));
+}
+
+// A lane's EPT elements of one adaptive step (cur_is_avg: current IS the average, d = 0).  When
+// every lane of the wave has its operands in the range fastmath.h admits -- v = +0 or
+// [2^-96, 2^78], eta*m = +-0 or 2^-85 <= |.| <= 2^100, tau in [2^-20, 2^38] (so sqrt(v) + tau is
+// in [2^-20, 2^40]) -- the square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp
+// seeds, packed fma), else the general sequences.  Both give the same bits (tools/fp_probe.py),
+// so which one a wave takes never shows in the results.
+template <int DT, int VARIANT, int EPT>
+__device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (&cur)[EPT], bool cur_is_avg,
+                                          float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
+                                          float omb1, float b2, float omb2, float eta, float tau) {
+    float c[EPT], num[EPT];
+    bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f);
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        c[j] = cur_is_avg ? avg[j] : cur[j];
+        adapt_moments<DT, VARIANT>(avg[j], c[j], m[j], v[j], num[j], b1, omb1, b2, omb2, eta);
+        ok = ok & flame_fm::sqrt_admits(v[j]) & flame_fm::div_admits(num[j]);
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {     // wave-uniform
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const float den = rnd<DT>(__fadd_rn(rnd<DT>(flame_fm::sqrt_rn(v[j])), tau));
+            cur_out[j] = rnd<DT>(__fadd_rn(c[j], rnd<DT>(flame_fm::div_rn(num[j], den))));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const float den = rnd<DT>(__fadd_rn(rnd<DT>(__builtin_sqrtf(v[j])), tau));
+            cur_out[j] = rnd<DT>(__fadd_rn(c[j], rnd<DT>(__fdiv_rn(num[j], den))));
+        }
+    }
 }
 
 // One chunk of a FedOPT round.  held != nullptr: a full-vector chunk leaves its avg / m / v /
@@ -516,15 +625,20 @@ __device__ __forceinline__ bool fedopt_chunk(const flame_segment* __restrict__ s
                 unpack<T, EPT>(ld_v(mp + v * VS), m_t);
                 unpack<T, EPT>(ld_v(vp + v * VS), v_t);
             }
+            float cf[EPT], mf[EPT], vf[EPT], co[EPT];
 #pragma unroll
             for (int j = 0; j < EPT; ++j) {
-                float mj = zero_state ? 0.f : X::ld(m_t[j]), vj = zero_state ? 0.f : X::ld(v_t[j]), cj;
-                adapt_elem<DT, VARIANT>(acc[v][j], cur_avg ? acc[v][j] : X::ld(cur_t[j]), mj, vj, cj, b1, omb1, b2,
-                                        omb2, eta, tau);
+                cf[j] = cur_avg ? 0.f : X::ld(cur_t[j]);
+                mf[j] = zero_state ? 0.f : X::ld(m_t[j]);
+                vf[j] = zero_state ? 0.f : X::ld(v_t[j]);
+            }
+            adapt_vec<DT, VARIANT, EPT>(acc[v], cf, cur_avg, mf, vf, co, b1, omb1, b2, omb2, eta, tau);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
                 avg_o[j] = X::st(acc[v][j]);
-                m_o[j] = X::st(mj);
-                v_o[j] = X::st(vj);
-                c_o[j] = X::st(cj);
+                m_o[j] = X::st(mf[j]);
+                v_o[j] = X::st(vf[j]);
+                c_o[j] = X::st(co[j]);
             }
             if (held) {
                 V16* h = held + v * kBlock + threadIdx.x;
@@ -659,6 +773,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
+    static_assert(kVPT == 1, "fedopt_chain_kernel: a lane handles one 16-byte vector of its chunk");
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_segment sg = segs[s];
@@ -688,7 +803,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
 #pragma unroll
         for (int j = 0; j < EPT; ++j) x[j] = X::ld(t[j]);
     };
-    float b[EPT], c[EPT], m[EPT], v[EPT];
+    float b[EPT], c[EPT] = {}, m[EPT], v[EPT];
     load_f(bp, b);
     if (!aliased) load_f(curp, c);
     if (zero_state) {
@@ -706,12 +821,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
 #pragma unroll
         for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
         if (step_end[i]) {     // uniform: one do() call ends here
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) {
-                float cn;
-                adapt_elem<DT, VARIANT>(b[j], aliased ? b[j] : c[j], m[j], v[j], cn, b1, omb1, b2, omb2, eta, tau);
-                c[j] = cn;
-            }
+            adapt_vec<DT, VARIANT, EPT>(b, c, aliased, m, v, c, b1, omb1, b2, omb2, eta, tau);
             aliased = false;
         }
     };
@@ -835,6 +945,84 @@ __global__ __launch_bounds__(kEwBlock) void scale_add_kernel(const flame_segment
 //   a = w_m + tmp(c_{m,0}, r_{m,0}) + ...;  w_m' = a;  d_m = w_m' - w_m
 // and the top's FedAvg adds tmp(d_m, top_rates[m]) to the top weights (top_agg_in).
 template <int DT> __device__ __forceinline__ float rnd(float x);
+// The element-wise hierarchy (segment tails, misaligned views): the same op sequence as the
+// vector paths, one element at a time.
+template <int DT, bool SYNC, typename MP>
+__device__ __forceinline__ void hier_tail(const flame_hier_segment& sg, int64_t e0, int64_t coff,
+                                          const uint64_t* __restrict__ wrow, const uint64_t* __restrict__ drow,
+                                          const uint64_t* __restrict__ crow, MP mid_ptr, int n_mids, int n_clients,
+                                          const float* __restrict__ mid_rates, const float* __restrict__ mid_goal,
+                                          const float* __restrict__ top_rates, float top_goal, unsigned flags) {
+    using X = Tr<DT>;
+    using S = SA<DT>;
+    using T = typename X::T;
+    using A = typename X::A;
+    constexpr int EPT = X::EPT;
+    constexpr int64_t VS = static_cast<int64_t>(kBlock) * EPT;
+    (void)wrow;
+    A top[kVPT][EPT];
+    bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
+    const T* tin = reinterpret_cast<const T*>(sg.top_agg_in) + e0;
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int64_t o = v * VS + j;
+            if (have_top && e0 + o < sg.numel) top[v][j] = X::ld(ld1(tin + o));
+        }
+#pragma unroll 1
+    for (int m = 0; m < n_mids; ++m) {
+        A acc[kVPT][EPT];
+        T* wp = mid_ptr(m);
+        if constexpr (SYNC) {
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int j = 0; j < EPT; ++j)
+                    acc[v][j] = (e0 + v * VS + j < sg.numel) ? X::ld(ld1(wp + v * VS + j)) : A(0);
+        }
+        reduce_clients<DT, 1, false>(acc, !SYNC, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+                                     mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel, coff);
+        T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
+        const float g = mid_goal[m], rt = top_rates[m];
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                const int64_t o = v * VS + j;
+                if (e0 + o >= sg.numel) continue;
+                T w = ld1(wp + o), d;
+                if constexpr (SYNC) {
+                    const T wn = X::st(acc[v][j]);
+                    d = X::st(rnd<DT>(__fsub_rn(X::ld(wn), X::ld(w))));
+                    w = wn;
+                } else {
+                    S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
+                }
+                if (!(flags & FLAME_HIER_MID_READONLY)) st1(wp + o, w);
+                if (dp) st1(dp + o, d);
+                const A t = X::tmp(d, rt, 0.0);
+                top[v][j] = have_top ? X::add(top[v][j], t) : t;
+            }
+        have_top = true;
+    }
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int64_t o = v * VS + j;
+            if (e0 + o >= sg.numel) continue;
+            const T t = X::st(top[v][j]);
+            if (sg.top_agg_out) st1(reinterpret_cast<T*>(sg.top_agg_out) + e0 + o, t);
+            if (flags & FLAME_HIER_TOP_APPLY) {
+                T* gp = reinterpret_cast<T*>(sg.top_w) + e0 + o;
+                T gw = ld1(gp);
+                S::op(gw, t, top_goal, static_cast<double>(top_goal), nullptr);
+                st1(gp, gw);
+            }
+        }
+}
+
 // (HL instantiations: the middle loop stays rolled -- its group lives in LDS, not registers)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wpass-failed"
@@ -967,65 +1155,8 @@ __device__ __forceinline__ void hier_fedbuff_body(const flame_hier_segment* __re
         }
         return;
     }
-    // tails / misaligned views: element-wise, same op sequence
-#pragma unroll
-    for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) {
-            const int64_t o = v * VS + j;
-            if (have_top && e0 + o < sg.numel) top[v][j] = X::ld(ld1(tin + o));
-        }
-#pragma unroll 1
-    for (int m = 0; m < n_mids; ++m) {
-        A acc[kVPT][EPT];
-        T* wp = mid_ptr(m);
-        if constexpr (SYNC) {
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-                for (int j = 0; j < EPT; ++j)
-                    acc[v][j] = (e0 + v * VS + j < sg.numel) ? X::ld(ld1(wp + v * VS + j)) : A(0);
-        }
-        reduce_clients<DT, 1, false>(acc, !SYNC, crow + static_cast<int64_t>(m) * n_clients, n_clients,
-                                     mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel, coff);
-        T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + e0 : nullptr;
-        const float g = mid_goal[m], rt = top_rates[m];
-#pragma unroll
-        for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) {
-                const int64_t o = v * VS + j;
-                if (e0 + o >= sg.numel) continue;
-                T w = ld1(wp + o), d;
-                if constexpr (SYNC) {
-                    const T wn = X::st(acc[v][j]);
-                    d = X::st(rnd<DT>(__fsub_rn(X::ld(wn), X::ld(w))));
-                    w = wn;
-                } else {
-                    S::op(w, X::st(acc[v][j]), g, static_cast<double>(g), &d);
-                }
-                if (!(flags & FLAME_HIER_MID_READONLY)) st1(wp + o, w);
-                if (dp) st1(dp + o, d);
-                const A t = X::tmp(d, rt, 0.0);
-                top[v][j] = have_top ? X::add(top[v][j], t) : t;
-            }
-        have_top = true;
-    }
-#pragma unroll
-    for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) {
-            const int64_t o = v * VS + j;
-            if (e0 + o >= sg.numel) continue;
-            const T t = X::st(top[v][j]);
-            if (sg.top_agg_out) st1(reinterpret_cast<T*>(sg.top_agg_out) + e0 + o, t);
-            if (flags & FLAME_HIER_TOP_APPLY) {
-                T* gp = reinterpret_cast<T*>(sg.top_w) + e0 + o;
-                T gw = ld1(gp);
-                S::op(gw, t, top_goal, static_cast<double>(top_goal), nullptr);
-                st1(gp, gw);
-            }
-        }
+    hier_tail<DT, SYNC>(sg, e0, coff, wrow, drow, crow, mid_ptr, n_mids, n_clients, mid_rates, mid_goal, top_rates,
+                        top_goal, flags);
 }
 
 template <int DT, int CU, bool SYNC, int HB, bool HL>
@@ -1057,6 +1188,162 @@ __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel_argmeta(const ArgM
                                     reinterpret_cast<const float*>(w + o_top_rates), top_goal, flags);
 }
 #pragma clang diagnostic pop
+
+// The asynchronous (FedBuff-mode) hierarchy of >= kHLdsMinMids middles with a workgroup of
+// kBlock + 64 lanes: waves 0-3 stream the middles' arrival reductions without a break; the fifth
+// wave runs every middle's epilogue (its weights -- prefetched one middle ahead -- scale_add,
+// delta, the top's accumulate, the LDS-held store group and its burst) while the four stream the
+// next middle.  The sums change hands through a double-buffered LDS block and one barrier per
+// middle.  Same op sequence, same bits as hier_fedbuff_body; chunks that are not whole and
+// aligned take hier_tail (the fifth wave has no elements there).
+template <int DT, int CU, int HB>
+__device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restrict__ segs, int n_segs, int n_mids,
+                                             int n_clients, const uint64_t* __restrict__ mid_w,
+                                             const uint64_t* __restrict__ mid_delta,
+                                             const uint64_t* __restrict__ clients,
+                                             const float* __restrict__ mid_rates,
+                                             const float* __restrict__ mid_goal,
+                                             const float* __restrict__ top_rates, float top_goal, unsigned flags) {
+    using X = Tr<DT>;
+    using S = SA<DT>;
+    using T = typename X::T;
+    using A = typename X::A;
+    constexpr int EPT = X::EPT;
+    constexpr int NV = kBlock / 64;                       // elements blocks per epilogue lane
+    static_assert(kVPT == 1 && sizeof(A) * EPT % 16 == 0, "hier_ws_body: one 16-byte vector per lane");
+    constexpr int AV = sizeof(A) * EPT / 16;              // 16-byte words of a lane's sums
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_hier_segment sg = segs[s];
+    const int64_t cbase = (chunk - sg.chunk_begin) * chunk_elems<DT>();
+    const bool epi = threadIdx.x >= kBlock;
+    const uint64_t* wrow = mid_w + static_cast<int64_t>(s) * n_mids;
+    const uint64_t* drow = mid_delta ? mid_delta + static_cast<int64_t>(s) * n_mids : nullptr;
+    const uint64_t* crow = clients + static_cast<int64_t>(s) * n_mids * n_clients;
+    auto woff = [&](int vl) {     // byte offset of lane vl's elements in every middle's weights
+        return sg.mid_tile_stride
+            ? (chunk - sg.chunk_begin) * sg.mid_tile_stride + static_cast<int64_t>(vl) * EPT * sizeof(T)
+            : (cbase + static_cast<int64_t>(vl) * EPT) * static_cast<int64_t>(sizeof(T));
+    };
+    if (cbase + chunk_elems<DT>() > sg.numel || (sg.flags & FLAME_SEG_UNALIGNED)) {
+        if (epi) return;
+        const int64_t e0 = cbase + static_cast<int64_t>(threadIdx.x) * EPT;
+        if (e0 >= sg.numel) return;
+        const int64_t wo = woff(threadIdx.x);
+        auto mid_ptr = [&](int m) { return reinterpret_cast<T*>(reinterpret_cast<char*>(wrow[m]) + wo); };
+        hier_tail<DT, false>(sg, e0, client_offset<DT>(sg, chunk), wrow, drow, crow, mid_ptr, n_mids, n_clients,
+                             mid_rates, mid_goal, top_rates, top_goal, flags);
+        return;
+    }
+    __shared__ V16 sums[2][AV][kBlock];     // the streamers' sums of a middle, double-buffered
+    __shared__ V16 held[HB * kBlock];       // the epilogue's store group
+    if (!epi) {
+        const int64_t e0 = cbase + static_cast<int64_t>(threadIdx.x) * EPT;
+        const int64_t coff = client_offset<DT>(sg, chunk);
+#pragma unroll 1
+        for (int m = 0; m < n_mids; ++m) {
+            A acc[kVPT][EPT];
+            reduce_clients<DT, CU, true>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
+                                         mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
+                                         coff);
+            V16 w[AV];
+            __builtin_memcpy(w, acc[0], sizeof(w));
+#pragma unroll
+            for (int a = 0; a < AV; ++a) sums[m & 1][a][threadIdx.x] = w[a];
+            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1
+        }
+        return;
+    }
+    const int lane = threadIdx.x - kBlock;
+    int64_t wo[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) wo[k] = woff(lane + 64 * k);
+    auto mid_ptr = [&](int m, int k) { return reinterpret_cast<T*>(reinterpret_cast<char*>(wrow[m]) + wo[k]); };
+    A top[NV][EPT];
+    bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
+    if (have_top) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            T b[EPT];
+            unpack<T, EPT>(ld_v(reinterpret_cast<const T*>(sg.top_agg_in) + cbase + (lane + 64 * k) * EPT), b);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) top[k][j] = X::ld(b[j]);
+        }
+    }
+    V16 wnext[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) wnext[k] = ld_v(mid_ptr(0, k));
+#pragma unroll 1
+    for (int m = 0; m < n_mids; ++m) {
+        V16 wcur[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) wcur[k] = wnext[k];
+        if (m + 1 < n_mids) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) wnext[k] = ld_v(mid_ptr(m + 1, k));
+        }
+        __syncthreads();                    // middle m's sums are in sums[m & 1]
+        T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + cbase : nullptr;
+        const float g = mid_goal[m], rt = top_rates[m];
+        const int u = m % HB;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int vl = lane + 64 * k;
+            V16 sw[AV];
+#pragma unroll
+            for (int a = 0; a < AV; ++a) sw[a] = sums[m & 1][a][vl];
+            A acc[EPT];
+            __builtin_memcpy(acc, sw, sizeof(acc));
+            T w[EPT], d[EPT];
+            unpack<T, EPT>(wcur[k], w);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                S::op(w[j], X::st(acc[j]), g, static_cast<double>(g), &d[j]);
+                const A t = X::tmp(d[j], rt, 0.0);
+                top[k][j] = have_top ? X::add(top[k][j], t) : t;
+            }
+            held[u * kBlock + vl] = pack<T, EPT>(w);
+            if (dp) st_v(dp + vl * EPT, pack<T, EPT>(d));
+        }
+        have_top = true;
+        if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {
+#pragma unroll 1
+            for (int uu = 0; uu <= u; ++uu)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) st_v(mid_ptr(m - u + uu, k), held[uu * kBlock + lane + 64 * k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int64_t e = cbase + (lane + 64 * k) * EPT;
+        T o[EPT];
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) o[j] = X::st(top[k][j]);
+        if (sg.top_agg_out) st_v(reinterpret_cast<T*>(sg.top_agg_out) + e, pack<T, EPT>(o));
+        if (flags & FLAME_HIER_TOP_APPLY) {
+            T* gp = reinterpret_cast<T*>(sg.top_w) + e;
+            T gw[EPT];
+            unpack<T, EPT>(ld_v(gp), gw);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) S::op(gw[j], o[j], top_goal, static_cast<double>(top_goal), nullptr);
+            st_v(gp, pack<T, EPT>(gw));
+        }
+    }
+}
+
+template <int DT, int CU, int HB>
+__global__ __launch_bounds__(kBlock + 64) void hier_ws_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
+                                                              int n_mids, int n_clients,
+                                                              const uint64_t* __restrict__ mid_w,
+                                                              const uint64_t* __restrict__ mid_delta,
+                                                              const uint64_t* __restrict__ clients,
+                                                              const float* __restrict__ mid_rates,
+                                                              const float* __restrict__ mid_goal,
+                                                              const float* __restrict__ top_rates, float top_goal,
+                                                              unsigned flags) {
+    hier_ws_body<DT, CU, HB>(segs, n_segs, n_mids, n_clients, mid_w, mid_delta, clients, mid_rates, mid_goal,
+                             top_rates, top_goal, flags);
+}
 
 // ---------------------------------------------------------------- FedDyn server round
 // One pass over a FedDyn aggregation round (optimizer/feddyn.py:90-113,125-139), driven
@@ -1682,6 +1969,9 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
 #define FLAME_HIER_LAUNCH(DT, CUV, CUL, LOLDS)                                                                  \
     if (lds) {                                                                                                 \
         if (sync) FLAME_HIER_GO(DT, CUL, true, kHBL, true, 0);                                                 \
+        else if (kHierWS)                                                                                      \
+            hipLaunchKernelGGL((hier_ws_kernel<DT, CUL, kHBL>), grid, dim3(kBlock + 64), 0, st, segs, n_segs,  \
+                               n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);  \
         else FLAME_HIER_GO(DT, CUL, false, kHBL, true, 0);                                                     \
         br = BR_HIER_LDS + DT * 2 + sync;                                                                      \
     } else if (lo) {                                                                                           \
@@ -1775,8 +2065,12 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
     const void* f = nullptr;
     // the instantiation flame_hier_fedbuff picks for these arguments (the one-middle low-residency
     // launch aside, which depends on the launch size)
+    int block = kBlock;
 #define FLAME_HIER_PICK(DT, CUV, CUL)                                                                          \
-    if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)          \
+    if (lds && !sync && kHierWS) {                                                                             \
+        f = reinterpret_cast<const void*>(hier_ws_kernel<DT, CUL, kHBL>);                                      \
+        block = kBlock + 64;                                                                                   \
+    } else if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)   \
                       : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, false, kHBL, true>);        \
     else f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, true, kHB, false>)              \
                   : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, false, kHB, false>);
@@ -1789,7 +2083,7 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
         return -set_err(FLAME_ENOTSUP, "flame_hier_resident_per_cu: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     int blocks = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, kBlock, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, block, 0);
     if (e != hipSuccess) return -set_err(FLAME_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
     return blocks < 1 ? 1 : blocks;
 }

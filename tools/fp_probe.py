@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Exhaustive / randomized bit checks of flame_amd/csrc/fastmath.h on the MI355X (see
+tools/fp_probe.hip).  Prints one line per check with the mismatch count and the first
+mismatching operands; exits non-zero when a variant the product uses mismatches.
+
+    python tools/fp_probe.py --build          # here (hipcc, gfx950)
+    python tools/fp_probe.py [--div-pairs N]  # on the GPU box
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "build", "diag", "libfp_probe.so")
+
+NORMAL_LO, INF = 0x00800000, 0x7F800000
+
+
+def f2b(x):
+    import struct
+    return struct.unpack("<I", struct.pack("<f", x))[0]
+
+
+def build():
+    from flame_amd import build as B
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-o", LIB, os.path.join(ROOT, "tools", "fp_probe.hip")])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--div-pairs", type=float, default=2 ** 36)
+    a = ap.parse_args()
+    if a.build:
+        return build()
+    import torch
+    L = ctypes.CDLL(LIB)
+    out = torch.zeros(5, dtype=torch.int64, device="cuda")
+    p = ctypes.c_void_p(out.data_ptr())
+    u64 = ctypes.c_uint64
+    bad = 0
+
+    def show(name, rc, must_be_exact):
+        nonlocal bad
+        o = out.cpu().tolist()
+        ok = rc == 0 and (o[0] == 0 or not must_be_exact)
+        bad += not ok
+        first = "" if o[0] == 0 else f"; first: x={o[1]:#010x} y={o[2]:#010x} got={o[3]:#010x} want={o[4]:#010x}"
+        print(f"{name}: rc={rc} mismatches={o[0]}{first}{'' if ok else '  <-- FAIL'}", flush=True)
+
+    t = time.time()
+    # sqrt: the admitted operands (+0, [2^-96, 2^78]) must match; the rest is informational
+    SQ_LO, SQ_HI = f2b(2.0 ** -96), f2b(2.0 ** 78) + 1
+    for v, nm in ((0, "sqrt_rn"), (1, "v_sqrt_f32 alone"), (2, "sqrt_fix"), (3, "sqrt_rsq2")):
+        show(f"{nm} on +0", L.probe_sqrt(u64(0), u64(1), v, p), v == 0)
+        show(f"{nm} on every x in [2^-96, 2^78]", L.probe_sqrt(u64(SQ_LO), u64(SQ_HI), v, p), v == 0)
+        show(f"{nm} on every other normal", L.probe_sqrt(u64(NORMAL_LO), u64(SQ_LO), v, p), False)
+        if v == 0:
+            show(f"{nm} on (2^78, inf]", L.probe_sqrt(u64(SQ_HI), u64(INF + 1), v, p), False)
+            show(f"{nm} on the subnormals", L.probe_sqrt(u64(1), u64(NORMAL_LO), v, p), False)
+    for v, nm in ((0, "rcp v_rcp_f32 alone"), (1, "rcp_rn")):
+        show(f"{nm} on every b in [2^-20, 2^40]", L.probe_rcp(u64(f2b(2.0 ** -20)), u64(f2b(2.0 ** 40) + 1), v, p),
+             v == 1)
+        show(f"{nm} on every normal b", L.probe_rcp(u64(NORMAL_LO), u64(INF), v, p), False)
+    n = int(a.div_pairs)
+    for seed in (1, 2):
+        show(f"div_rn {n} admitted pairs (seed {seed})", L.probe_div(u64(seed), u64(n), 0, p), True)
+    show(f"div_rn {n // 4} pairs over every finite a, b in [2^-60, 2^66] (outside the admitted range)",
+         L.probe_div(u64(3), u64(n // 4), 1, p), False)
+    print(f"fp_probe: {time.time() - t:.1f} s, {bad} failing check(s)", flush=True)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

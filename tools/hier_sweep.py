@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """Interleaved A/B sweep of compile-time variants of flame_hier_fedbuff (config 5 shard).
 
-Each variant is a separate build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) loaded side by side with
+Each variant is a build of the PRODUCT source (flame_amd/csrc/fedagg.hip) with -DFLAME_T_*
+overrides of its tunables (the defaults are the shipped kernel), loaded side by side with
 ctypes; all run in ONE process on the same device-resident tiled slab (64 middles x 64
 arrivals x 15.6M bf16 by default), rounds interleaved; outputs (middle weights, top
 aggregate, top weights) are checked bitwise against the first variant from identical state.
+A name containing "/" is a library path instead (e.g. flame_amd/libflame_amd.so).
 
-    python tools/hier_sweep.py --build            # here (hipcc cross-compiles)
-    python tools/hier_sweep.py --rounds 4         # on the GPU
+    python tools/hier_sweep.py --build --variants base,ws    # here (hipcc cross-compiles)
+    python tools/hier_sweep.py --variants base,ws --rounds 4 # on the GPU
 """
 import argparse
 import ctypes
@@ -18,92 +20,16 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "hvariants")
+VDIR = os.path.join(ROOT, "build", "diag", "hier")   # travels to the GPU box with the tree
 
+# Round-2/3 sweeps of the store grouping, unroll, residency (LDS groups of 12 = 3 workgroups per
+# CU), prefetch and pipelining variants are in profiles/r02_hier_*.log, r03z*_hier_sweep.log.
 VARIANTS = {
     "base": {},
-    "nolds": {"FLAME_HLDS": 0},                        # before the LDS-held store groups (round 2 first half)
-    "r01": {"FLAME_HBATCH": 1, "FLAME_HCU16": 8},     # round 1's kernel: stores per middle, unroll 8
-    "hcu4": {"FLAME_HCU16": 4},
-    "hcu2": {"FLAME_HCU16": 2},
-    "pf": {"FLAME_HPF": 1},
-    "hcu4pf": {"FLAME_HCU16": 4, "FLAME_HPF": 1},
-    "wpe8": {"FLAME_HWPE": 8},
-    "hcu4wpe8": {"FLAME_HCU16": 4, "FLAME_HWPE": 8},
-    "hcu4wpe6": {"FLAME_HCU16": 4, "FLAME_HWPE": 6},
-    "hst0": {"FLAME_HST": 0},
-    "hst1": {"FLAME_HST": 1},
-    "hst2": {"FLAME_HST": 2},
-    "hst3": {"FLAME_HST": 3},
-    "hst5": {"FLAME_HST": 5},
-    "hb2": {"FLAME_HBATCH": 2},
-    "hb4": {"FLAME_HBATCH": 4},
-    "hb8": {"FLAME_HBATCH": 8},
-    "hb8cu4": {"FLAME_HBATCH": 8, "FLAME_HCU16": 4},
-    "hb8wpe5": {"FLAME_HBATCH": 8, "FLAME_HWPE": 5},
-    "hb4cu4": {"FLAME_HBATCH": 4, "FLAME_HCU16": 4},
-    "hb6": {"FLAME_HBATCH": 6},
-    "hb4hst0": {"FLAME_HBATCH": 4, "FLAME_HST": 0},
-    "lds16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16},
-    "lds24": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 24},
-    "lds32": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32},
-    "lds16cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 8},
-    "lds32cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32, "FLAME_HLDS_CU16": 8},
-    "lds32cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 32, "FLAME_HLDS_CU16": 16},
-    "lds8cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 8},
-    "lds12cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 8},
-    "lds20cu8": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 8},
-    "lds16cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 16},
-    "lds16cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 6},
-    "lds20cu16": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 16},
-    "lds16cu4": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 4},
-    "lds16cu5": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 5},
-    "lds16cu7": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 16, "FLAME_HLDS_CU16": 7},
-    "lds20cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 20, "FLAME_HLDS_CU16": 6},
-    "lds18cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 18, "FLAME_HLDS_CU16": 6},
-    "lds14cu6": {"FLAME_HLDS": 1, "FLAME_HLDS_BATCH": 14, "FLAME_HLDS_CU16": 6},
-    # round 3: the next client batch's loads issued before the current one is combined (a
-    # wave's loads in flight stay between CU and 2 CU instead of dropping to 0 while it computes)
-    "pipe3": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 3},
-    "pipe4": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 4},
-    "pipe6": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 6},
-    "pipe2": {"FLAME_PIPE": 1, "FLAME_HLDS_CU16": 2},
-    # round 3: whole batches only (the init-first arrival with the first batch, the remainder together)
-    "tailb": {"FLAME_TAILB": 1},
-    "tailbpf": {"FLAME_TAILB": 1, "FLAME_HPF": 1},
-    "tailbcu5": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 5},
-    "tailbcu7": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 7},
-    "tailbcu8": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 8},
-    "tailbcu4": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 4},
-    "tailbcu3": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 3},
-    "tailbcu2": {"FLAME_TAILB": 1, "FLAME_HLDS_CU16": 2},
-    # round 3: cheaper bf16 arithmetic (the kernel issues ~13x the VALU instructions of C3's per
-    # launch, SQ counters r03zj): one-instruction rounding, packed-fp32 multiply / add
-    "bhi": {"FLAME_BF16_HI": 1},
-    "bpk": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1},
-    "bpkcu4": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 4},
-    "bpkcu5": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 5},
-    "bpkcu8": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_HLDS_CU16": 8},
-    # round 3: one double-buffered arrival stream across the middles (no drain at middle boundaries)
-    "hxp2": {"FLAME_HXP": 2},
-    "hxp4": {"FLAME_HXP": 4},
-    "hxp8": {"FLAME_HXP": 8},
-    "hxp16": {"FLAME_HXP": 16},
-    "spf": {"FLAME_SPF": 1},
-    "spf2": {"FLAME_SPF": 2},          # pointers AND rates prefetched one batch ahead, whole batches
-    "spf2cu5": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 5},
-    "spf2cu4": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 4},
-    "spf2cu8": {"FLAME_SPF": 2, "FLAME_HLDS_CU16": 8},
-    "spfcu5": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 5},
-    "spfcu8": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 8},
-    "spfcu4": {"FLAME_SPF": 1, "FLAME_HLDS_CU16": 4},
-    "hcu3": {"FLAME_HLDS_CU16": 3},
-    "lds12cu3": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 3},
-    "lds12cu4": {"FLAME_HLDS_BATCH": 12, "FLAME_HLDS_CU16": 4},
-    "lds8cu3": {"FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 3},
-    "lds8cu2": {"FLAME_HLDS_BATCH": 8, "FLAME_HLDS_CU16": 2},
-    "hdiag1": {"FLAME_HDIAG": 1},   # diagnostic: middle weights not stored (output not checked)
-    "hdiag2": {"FLAME_HDIAG": 2},   # diagnostic: middle weights neither loaded nor stored
+    "ws": {"FLAME_T_HIER_WS": 1},                              # a fifth wave runs the epilogues
+    "ws_cu8": {"FLAME_T_HIER_WS": 1, "FLAME_T_HIER_LDS_UNROLL16": 8},
+    "ws_cu4": {"FLAME_T_HIER_WS": 1, "FLAME_T_HIER_LDS_UNROLL16": 4},
+    "hbl12cu4": {"FLAME_T_HBL": 12, "FLAME_T_HIER_LDS_UNROLL16": 4},   # 3 workgroups per CU
 }
 
 
@@ -113,7 +39,7 @@ def build_variants(names):
     for name in names:
         defs = [f"-D{k}={v}" for k, v in VARIANTS[name].items()]
         out = os.path.join(VDIR, f"lib_{name}.so")
-        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SWEEP_SRC])
+        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SRC])
         print("built", out, flush=True)
 
 
@@ -130,7 +56,7 @@ def load(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
-    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--variants", default="base,ws")
     ap.add_argument("--mids", type=int, default=64)
     ap.add_argument("--clients", type=int, default=64, help="arrivals per middle")
     ap.add_argument("--params", type=int, default=125_000_000 // 8)
@@ -142,7 +68,7 @@ def main():
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
-        build_variants(sorted({n.split(":")[0] for n in names if n not in ("probe", "rprobe")}))
+        build_variants(sorted({n.split(":")[0] for n in names if n not in ("probe", "rprobe") and "/" not in n}))
         return
 
     import torch
