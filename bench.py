@@ -810,9 +810,14 @@ def _fracs(args, shard, default=None):
 
 
 def _collective_note(plan, world, itemsize):
+    from flame_amd import shard
     recv = sum((s.g1 - s.g0) - (s.hi - s.lo) for s in plan.subs if not s.tail) * itemsize
     return {"kind": "in-place all_gather_into_tensor per wave (RCCL over xGMI)" if world > 1 else "none (world 1)",
             "waves": plan.n_waves, "bytes_received_per_rank": recv,
+            # which torch.distributed calls the gathers took (flame_amd.shard.GATHER_STATS): "async" =
+            # the public all_gather_into_tensor per piece, "coalesced" = torch's _coalescing_manager group
+            # (a wave of several same-dtype pieces), "host_staged" = gloo with CUDA tensors
+            "gather_calls": dict(shard.GATHER_STATS),
             "wave_elements_per_rank": [sum(s.hi - s.lo for s in plan.subs if s.wave == w and not s.tail)
                                        for w in range(plan.n_waves)],
             "replicated_tail_elements": sum(s.hi - s.lo for s in plan.subs if s.tail)}

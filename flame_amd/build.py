@@ -19,9 +19,9 @@ SRC = os.path.join(PKG, "csrc", "fedagg.hip")
 HDR = os.path.join(ROOT, "include", "flame_amd.h")
 DEPS = (SRC, HDR, os.path.join(PKG, "csrc", "fastmath.h"))
 LIB = os.path.join(PKG, "libflame_amd.so")
-# The kernel source WITH its compile-time sweep switches (default-off variants, diagnostics that
-# skip work): tools/kernel_sweep.py / hier_sweep.py build it into build/variants, never into LIB.
-SWEEP_SRC = os.path.join(ROOT, "tools", "sweep", "fedagg_sweep.hip")
+# Sweep builds (tools/kernel_sweep.py, hier_sweep.py) compile SRC itself with -DFLAME_T_* overrides
+# of its tunables into build/diag; diagnostic stamps are inserted into a copy by
+# tools/sweep/htime.py.  Neither ever writes LIB.
 ARCH = os.environ.get("FLAME_AMD_ARCH", "gfx950")
 # host side: the restricted pickle VM of flame_amd.ingest (a CPython extension, plain gcc)
 VM_SRC = os.path.join(PKG, "csrc", "pickle_vm.c")

@@ -2,12 +2,12 @@
 """Interleaved A/B of compile-time variants for the async FedBuff aggregator's round
 (asyncfl/top_aggregator.py:85-110: aggGoal arrivals, one per do(), then the fused
 scale_add -- or a middle's scale_add + upload delta, --delta), in ONE process: each variant
-is a build in build/variants (tools/kernel_sweep.py --build), swapped in as the engine's
+is a build in build/diag/variants (tools/kernel_sweep.py --build), swapped in as the engine's
 native library round by round; kernel time from HIP events; the model (and deltas) checked
 bitwise across variants every round.
 
-    python tools/kernel_sweep.py --build --variants base,hsm1     # here
-    python tools/fedbuff_sweep.py --variants base,hsm1 --rounds 6  # on the GPU
+    python tools/kernel_sweep.py --build --variants base,lo_cu4     # here
+    python tools/fedbuff_sweep.py --variants base,lo_cu4 --rounds 6  # on the GPU
 """
 import argparse
 import os
@@ -18,7 +18,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "build", "diag", "variants")   # built by tools/kernel_sweep.py --build
 
 
 class Cache(dict):

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Interleaved A/B of compile-time variants of flame_feddyn_round through the FedDyn drop-in,
-in ONE process: each variant is a build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) in build/variants
-(tools/kernel_sweep.py --build), swapped in as the engine's native library round by round;
+in ONE process: each variant is a build of the product source with -DFLAME_T_* overrides in
+build/diag/variants (tools/kernel_sweep.py --build), swapped in as the engine's native library
+round by round;
 the same slab-resident arrivals drive one FedDyn instance per variant; kernel time from HIP
 events; cld_model checked bitwise across variants every round.
 
-    python tools/kernel_sweep.py --build --variants base,dynlds16   # here
-    python tools/feddyn_sweep.py --variants base,dynlds16 --rounds 5 # on the GPU
+    python tools/kernel_sweep.py --build --variants base,dyncu8   # here
+    python tools/feddyn_sweep.py --variants base,dyncu8 --rounds 5 # on the GPU
 """
 import argparse
 import os
@@ -17,7 +18,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "build", "diag", "variants")   # built by tools/kernel_sweep.py --build
 
 
 class Cache(dict):

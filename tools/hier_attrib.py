@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Where config 5's hierarchy kernel spends its time, per workgroup.
 
-A diagnostic build of tools/sweep/fedagg_sweep.hip (-DFLAME_HTIME=1) has wave 0 of every
-workgroup stamp s_memrealtime (100 MHz) at: start, each middle's reduction end, each
+A diagnostic build of the product source with stamps inserted by tools/sweep/htime.py has wave 0
+of every workgroup stamp s_memrealtime (100 MHz) at: start, each middle's reduction end, each
 middle's epilogue end (scale_add + delta into the top, weights into the LDS store group),
 each LDS store burst's end, and the end (top scale_add).  Run on the C5 shard (64 middles x
 64 arrivals x 15.6M bf16, tiled middles, FedBuff mode with the top applied) next to the
@@ -29,17 +29,20 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag")   # uploaded to the box (not in .gpurunignore)
-SLOTS = 256
+VDIR = os.path.join(ROOT, "build", "diag", "attrib")   # uploaded to the box (not in .gpurunignore)
+SLOTS = 288
 
 
 def build():
     from flame_amd import build as B
+    sys.path.insert(0, os.path.join(ROOT, "tools", "sweep"))
+    import htime
     os.makedirs(VDIR, exist_ok=True)
-    for nm, defs in (("base", []), ("htime", ["-DFLAME_HTIME=1"]), ("hnx", ["-DFLAME_HNX=1"]),
-                     ("htime_hnx", ["-DFLAME_HTIME=1", "-DFLAME_HNX=1"])):
-        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", os.path.join(VDIR, f"lib_{nm}.so"),
-                               B.SWEEP_SRC])
+    stamped = htime.generate(os.path.join(VDIR, "fedagg_htime.hip"))
+    ws = ["-DFLAME_T_HIER_WS=1"]
+    for nm, defs, src in (("base", [], B.SRC), ("htime", [], stamped), ("ws", ws, B.SRC), ("htime_ws", ws, stamped)):
+        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", os.path.join(VDIR, f"lib_{nm}.so"), src])
+        print("built", nm, flush=True)
 
 
 def load(nm):
@@ -64,7 +67,7 @@ def main():
     ap.add_argument("--params", type=int, default=125_000_000 // 8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variant", default="", help="'' = base / htime, 'hnx' = hnx / htime_hnx")
+    ap.add_argument("--variant", default="", help="'' = base / htime, 'ws' = ws / htime_ws (FLAME_T_HIER_WS)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -95,7 +98,7 @@ def main():
     dm = torch.from_numpy(p.meta).to(dev)
     b = dm.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    plain, stamped = ("hnx", "htime_hnx") if a.variant == "hnx" else ("base", "htime")
+    plain, stamped = ("ws", "htime_ws") if a.variant == "ws" else ("base", "htime")
     libs = {"base": load(plain), "htime": load(stamped)}
     ts = torch.zeros(p.n_chunks * SLOTS, dtype=torch.int64, device=dev)
     assert libs["htime"].flame_sweep_htime(ts.data_ptr(), SLOTS) == 0
@@ -171,6 +174,23 @@ def main():
         "wg_bytes": M * C * T * isz + 2 * M * T * isz + 2 * T * isz,
     }
     res["streaming_GBps_per_wg_while_streaming"] = (M * C * T * isz) / (float(np.median(red_t.sum(1))) * tick_ns)
+    if a.variant == "ws":
+        # the streamers (waves 0-3): each middle's reduction, and the wait at its barrier (the epilogue
+        # wave still busy with the previous middle); the epilogue wave: per middle, its work after the
+        # sums arrive, and its idle wait for them
+        o = 3 + 2 * M + nb
+        s_red = t[:, o:o + 2 * M:2]                 # reduction m done (streamers)
+        s_bar = t[:, o + 1:o + 1 + 2 * M:2]         # past barrier m
+        s_prev = np.concatenate([start[:, None], s_bar[:, :-1]], axis=1)
+        e_got, e_done = t[:, 3:3 + 2 * M:2], t[:, 4:4 + 2 * M:2]
+        res["ws"] = {
+            "streamer_reduction_us": float(np.median(s_red - s_prev)) * tick_ns / 1e3,
+            "streamer_barrier_wait_us": float(np.median(s_bar - s_red)) * tick_ns / 1e3,
+            "streamer_barrier_wait_share": float((s_bar - s_red).sum()) / float((s_bar - start[:, None])[:, -1].sum()),
+            "epilogue_work_us": float(np.median(e_done - e_got)) * tick_ns / 1e3,
+            "epilogue_work_us_p95": float(np.percentile(e_done - e_got, 95)) * tick_ns / 1e3,
+            "epilogue_busy_share": float((e_done - e_got).sum()) / float((end - start).sum()),
+        }
     print(json.dumps(res, indent=1), flush=True)
     if a.out:
         with open(a.out, "w") as f:

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B sweep of compile-time variants of flame_agg_reduce (fp32).
 
-Each variant is a separate build of tools/sweep/fedagg_sweep.hip (the kernel source with every sweep switch) (FLAME_BLOCK,
-FLAME_CU, FLAME_VPT, FLAME_PIPE, FLAME_NT) loaded side by side with ctypes;
+Each variant is a build of the product source (flame_amd/csrc/fedagg.hip) with -DFLAME_T_*
+overrides of its tunables, loaded side by side with ctypes;
 all run in ONE process on the same device-resident 1024 x 25M slab, rounds
 interleaved (cdna_hip_programming.md §5.4 rule 24), outputs checked bitwise
 against the first variant.
@@ -20,129 +20,25 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "build", "diag", "variants")   # travels to the GPU box with the tree
 
+# Knobs of the PRODUCT source (flame_amd/csrc/fedagg.hip's FLAME_T_* defaults are the shipped
+# kernel).  Variants of rounds 1-4 that were measured no faster and are no longer in the source
+# (block size, vectors per lane, pipelining, store policies, buffer loads, FedDyn LDS bursts, ...)
+# are recorded in profiles/r0*_sweep*.log and DESIGN.md §4.
 VARIANTS = {
     "base": {},
-    "nt0": {"FLAME_NT": 0},
-    "cu4": {"FLAME_CU": 4},
-    "cu16": {"FLAME_CU": 16},
-    "vpt2": {"FLAME_VPT": 2},
-    "vpt2cu4": {"FLAME_VPT": 2, "FLAME_CU": 4},
-    "pipe8": {"FLAME_PIPE": 1},
-    "pipe4": {"FLAME_PIPE": 1, "FLAME_CU": 4},
-    "b512": {"FLAME_BLOCK": 512},
-    "b128": {"FLAME_BLOCK": 128},
-    "b64": {"FLAME_BLOCK": 64},
-    "optpf": {"FLAME_OPT_PREFETCH": 1},
-    "c16_4": {"FLAME_CU16": 4},
-    "c16_2": {"FLAME_CU16": 2},
-    "c16_4v2": {"FLAME_CU16": 4, "FLAME_VPT": 2},
-    "cu16b128": {"FLAME_CU": 16, "FLAME_BLOCK": 128},
-    "stplain": {"FLAME_ST_NT": 0},
-    "stnt": {"FLAME_ST_NT": 1},
-    "nostore": {"FLAME_NOSTORE": 1},   # diagnostic: output not written (not checked)
-    "stsc1": {"FLAME_ST_NT": 2},
-    "stsc01": {"FLAME_ST_NT": 3},
-    "stsc01nt": {"FLAME_ST_NT": 4},
-    "wgc2": {"FLAME_WGC": 2},
-    "wgc4": {"FLAME_WGC": 4},
-    "wgc2d": {"FLAME_WGC": 2, "FLAME_DEFER_ST": 1},
-    "wgc4d": {"FLAME_WGC": 4, "FLAME_DEFER_ST": 1},
-    "wgc8d": {"FLAME_WGC": 8, "FLAME_DEFER_ST": 1},
-    # FedDyn round kernel (bench.py --workload feddyn with FLAME_AMD_LIB=build/variants/lib_<name>.so)
-    # FedOPT: several chunks per workgroup, outputs held in LDS and stored in one burst
-    "optwgc1": {"FLAME_OPT_WGC": 1},      # round 1's FedOPT kernel (one chunk per workgroup)
-    "optwgc2": {"FLAME_OPT_WGC": 2},
-    "optwgc3": {"FLAME_OPT_WGC": 3},
-    "optwgc4": {"FLAME_OPT_WGC": 4},
-    "optwgc6": {"FLAME_OPT_WGC": 6},
-    "optwgc8": {"FLAME_OPT_WGC": 8},
-    "optwgc4cu16": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 16},
-    "optwgc6cu16": {"FLAME_OPT_WGC": 6, "FLAME_OPT_CU": 16},
-    "optwgc3cu16": {"FLAME_OPT_WGC": 3, "FLAME_OPT_CU": 16},
-    "optwgc5": {"FLAME_OPT_WGC": 5},
-    "optwgc7": {"FLAME_OPT_WGC": 7},
-    "optwgc10": {"FLAME_OPT_WGC": 10},
-    "optwgc8cu16": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 16},
-    "optwgc8cu4": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 4},
-    "dynxcd0": {"FLAME_DYN_XCD": 0},       # round-robin chunk order (before)
-    "dyncu2": {"FLAME_DYN_CU": 2},
-    # updated histories held in LDS, stored G steps at a time (tools/feddyn_sweep.py)
-    "dynlds8": {"FLAME_DYN_LDS": 8},
-    "dynlds16": {"FLAME_DYN_LDS": 16},
-    "dynlds32": {"FLAME_DYN_LDS": 32},
-    "dynlds16cu8": {"FLAME_DYN_LDS": 16, "FLAME_DYN_CU": 8},
-    "dynlds24cu8": {"FLAME_DYN_LDS": 24, "FLAME_DYN_CU": 8},
-    "dynlds12cu6": {"FLAME_DYN_LDS": 12, "FLAME_DYN_CU": 6},
-    "dyncu8": {"FLAME_DYN_CU": 8},
-    "dynst0": {"FLAME_DYN_ST": 0},
-    "dynst1": {"FLAME_DYN_ST": 1},
-    "dynst2": {"FLAME_DYN_ST": 2},
-    # resident workgroups per CU capped by dynamic LDS (reduction + hierarchy kernels)
-    "occ3": {"FLAME_OCC_LDS": 53248},
-    "occ4": {"FLAME_OCC_LDS": 40960},
-    "occ5": {"FLAME_OCC_LDS": 32768},
-    "occ6": {"FLAME_OCC_LDS": 27136},
-    "xcd": {"FLAME_XCD_SWIZZLE": 1},
-    # round 3: fewer loads in flight per CU (tools/occ_probe.py: reads peak at 2 workgroups per CU
-    # with 6 x 16-B loads per lane, above the full-occupancy configurations)
-    "occ2cu6": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 6},
-    "occ2cu8": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 8},
-    "occ2cu4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4},
-    "occ2cu12": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 12},
-    "occ3cu4": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 4},
-    "occ3cu6": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 6},
-    "occ4cu4": {"FLAME_OCC_LDS": 40960, "FLAME_CU": 4},
-    "occ2pipe3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3, "FLAME_PIPE": 1},
-    "occ2pipe4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_PIPE": 1},
-    "occ2cu3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3},
-    "occ2cu2": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 2},
-    "occ2cu5": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 5},
-    "occ3cu3": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 3},
-    "occ3cu2": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 2},
-    "tailb": {"FLAME_TAILB": 1},
-    "occ2cu4tb": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_TAILB": 1},
-    "occ2cu6tb": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 6, "FLAME_TAILB": 1},
-    "optwgc4cu6": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 6},
-    "optwgc8cu12": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 12},
-    "lo0": {"FLAME_LO_CU": 0},        # flame_agg_reduce before the low-occupancy path (full occupancy, unroll 8)
-    "lo4": {"FLAME_LO_CU": 4},
-    "lo2occ3": {"FLAME_LO_CU": 2, "FLAME_LO_LDS": 53248},
-    "lo3occ3": {"FLAME_LO_CU": 3, "FLAME_LO_LDS": 53248},
-    "optwgc4cu3": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 3},
-    "optwgc4cu4": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 4},
-    "bpk": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1},   # cheaper bf16 arithmetic (hier_sweep.py)
-    "bpklo3": {"FLAME_BF16_HI": 1, "FLAME_BF16_PK": 1, "FLAME_LO_CU16": 3},
-    "spf": {"FLAME_SPF": 1},          # next batch's client pointers prefetched behind the current loads
-    "spflo4": {"FLAME_SPF": 1, "FLAME_LO_CU": 4},
-    "spf2": {"FLAME_SPF": 2},
-    # FedDyn (2 reads : 1 write) and mid-size reductions at lower residency (tools/feddyn_sweep.py)
-    "dynocc2": {"FLAME_DYN_OCC_LDS": 65536},
-    "dynocc2cu2": {"FLAME_DYN_OCC_LDS": 65536, "FLAME_DYN_CU": 2},
-    "dynocc2cu3": {"FLAME_DYN_OCC_LDS": 65536, "FLAME_DYN_CU": 3},
-    "dynocc3cu2": {"FLAME_DYN_OCC_LDS": 53248, "FLAME_DYN_CU": 2},
-    "dynocc4cu2": {"FLAME_DYN_OCC_LDS": 40960, "FLAME_DYN_CU": 2},
-    "lomin32": {"FLAME_LO_MIN_CLIENTS": 32},
-    # the single-middle hierarchy launch (FedBuff's fused scale_add, tools/fedbuff_sweep.py) capped at
-    # 2 / 3 workgroups per CU with fewer loads in flight (FLAME_CU: fp32 unroll of every full-residency path)
-    "hocc2cu3": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 3, "FLAME_HCU16": 4},
-    "hocc2cu4": {"FLAME_OCC_LDS": 65536, "FLAME_CU": 4, "FLAME_HCU16": 4},
-    "hocc3cu3": {"FLAME_OCC_LDS": 53248, "FLAME_CU": 3, "FLAME_HCU16": 3},         # FLAME_SPF >= 2 builds differ only by name (second version: rates too)
-    "lo16_3": {"FLAME_LO_CU16": 3},
-    "lo16_6": {"FLAME_LO_CU16": 6},
-    "optwgc4cu2": {"FLAME_OPT_WGC": 4, "FLAME_OPT_CU": 2},
-    "optwgc8cu3": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 3},
-    "optwgc8cu4": {"FLAME_OPT_WGC": 8, "FLAME_OPT_CU": 4},
-    "optwgc6cu3": {"FLAME_OPT_WGC": 6, "FLAME_OPT_CU": 3},
-    "optwgc3cu3": {"FLAME_OPT_WGC": 3, "FLAME_OPT_CU": 3},
-    "optwgc2cu3": {"FLAME_OPT_WGC": 2, "FLAME_OPT_CU": 3},
-    # client loads as buffer loads with an explicit cache policy (sc0 1, nt 2, sc1 16; value - 1)
-    "bl_none": {"FLAME_BUFLD": 1},
-    "bl_nt": {"FLAME_BUFLD": 3},
-    "bl_sc1nt": {"FLAME_BUFLD": 19},
-    "bl_sc01nt": {"FLAME_BUFLD": 20},
-    "bl_sc0nt": {"FLAME_BUFLD": 4},
+    "cu4": {"FLAME_T_CLIENT_UNROLL": 4},
+    "cu16": {"FLAME_T_CLIENT_UNROLL": 16},
+    "lo_cu2": {"FLAME_T_LO_UNROLL": 2},
+    "lo_cu4": {"FLAME_T_LO_UNROLL": 4},
+    "lo_occ3": {"FLAME_T_LO_LDS": 53248},
+    "optwgc2": {"FLAME_T_OPT_WGC": 2},
+    "optwgc8": {"FLAME_T_OPT_WGC": 8},
+    "optcu4": {"FLAME_T_OPT_UNROLL": 4},
+    "dyncu2": {"FLAME_T_DYN_UNROLL": 2},
+    "dyncu8": {"FLAME_T_DYN_UNROLL": 8},
+    "chaincu4": {"FLAME_T_CLIENT_UNROLL": 4},
 }
 
 
@@ -152,7 +48,7 @@ def build_variants(names):
     for name in names:
         defs = [f"-D{k}={v}" for k, v in VARIANTS[name].items()]
         out = os.path.join(VDIR, f"lib_{name}.so")
-        cmd = [B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SWEEP_SRC]
+        cmd = [B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", out, B.SRC]
         subprocess.check_call(cmd)
         print("built", out, flush=True)
 
