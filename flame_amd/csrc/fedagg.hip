@@ -557,12 +557,12 @@ __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
                                           float omb1, float b2, float omb2, float eta, float tau) {
     float c[EPT], num[EPT];
-    bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f);
+    unsigned ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f);       // no short-circuit branches
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         c[j] = cur_is_avg ? avg[j] : cur[j];
         adapt_moments<DT, VARIANT>(avg[j], c[j], m[j], v[j], num[j], b1, omb1, b2, omb2, eta);
-        ok = ok & flame_fm::sqrt_admits(v[j]) & flame_fm::div_admits(num[j]);
+        ok &= static_cast<unsigned>(flame_fm::sqrt_admits(v[j])) & static_cast<unsigned>(flame_fm::div_admits(num[j]));
     }
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) {     // wave-uniform
 #pragma unroll
@@ -763,26 +763,28 @@ __global__ __launch_bounds__(kBlock) void fedopt_kernel_argmeta(const ArgMeta me
 // of every arrival's launch reading and writing all four.  Bitwise equal to those launches: every
 // value held in registers between steps is already rounded to the dtype (each op rounds), so it
 // equals what the per-arrival launches store and reload.
-template <int DT, int VARIANT, int CU>
-__global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segment* __restrict__ segs, int n_segs,
-                                                              const uint64_t* __restrict__ clients, int n_clients,
-                                                              const float* __restrict__ r32,
-                                                              const uint8_t* __restrict__ step_end, unsigned flags,
-                                                              float b1, float omb1, float b2, float omb2, float eta,
-                                                              float tau) {
+// step_end[i] through a SCALAR load: the aligned dword holding byte i (never outside the page
+// that holds it), so the per-step test is an s_load + scalar branch, not a vector byte load whose
+// s_waitcnt vmcnt(0) would also wait for the batch's client loads in flight.
+__device__ __forceinline__ bool step_ends(const uint8_t* __restrict__ step_end, int i) {
+    using kptr = const __attribute__((address_space(4))) uint32_t*;    // constant: scalar loads
+    const uintptr_t a = reinterpret_cast<uintptr_t>(step_end) + static_cast<uintptr_t>(i);
+    const uint32_t w = *reinterpret_cast<kptr>(a & ~static_cast<uintptr_t>(3));
+    return ((w >> ((a & 3u) * 8u)) & 0xffu) != 0u;
+}
+
+// VEC: the workgroup's whole chunk is inside the segment and aligned, so every lane's loads are
+// unconditional 16-byte vectors and the batch's loads are waited for one by one
+// (s_waitcnt vmcnt(CU - 1 - u)) instead of all at once.
+template <int DT, int VARIANT, int CU, bool VEC>
+__device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64_t e0, const uint64_t* __restrict__ cp,
+                                                  int64_t coff, int n_clients, const float* __restrict__ r32,
+                                                  const uint8_t* __restrict__ step_end, unsigned flags, float b1,
+                                                  float omb1, float b2, float omb2, float eta, float tau) {
     using X = Tr<DT>;
     using T = typename X::T;
     constexpr int EPT = X::EPT;
-    static_assert(kVPT == 1, "fedopt_chain_kernel: a lane handles one 16-byte vector of its chunk");
-    const int64_t chunk = blockIdx.x;
-    const int s = find_segment(segs, n_segs, chunk);
-    const flame_segment sg = segs[s];
-    const int64_t e0 = (chunk - sg.chunk_begin) * chunk_elems<DT>() + static_cast<int64_t>(threadIdx.x) * EPT;
-    if (e0 >= sg.numel) return;
-    const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
-    const int64_t coff = client_offset<DT>(sg, chunk);
-    const bool vec = (e0 + EPT <= sg.numel) && !(sg.flags & FLAME_SEG_UNALIGNED);
-    const int nv = vec ? EPT : static_cast<int>(sg.numel - e0 < EPT ? sg.numel - e0 : EPT);
+    const int nv = VEC ? EPT : static_cast<int>(sg.numel - e0 < EPT ? sg.numel - e0 : EPT);
     bool aliased = (sg.flags & FLAME_SEG_CUR_IS_AVG) != 0;
     const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
     const T* bp = reinterpret_cast<const T*>(sg.in) + e0;
@@ -790,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
     T* mp = reinterpret_cast<T*>(sg.m) + e0;
     T* vp = reinterpret_cast<T*>(sg.v) + e0;
     auto load_t = [&](const T* p, T (&x)[EPT], bool nt) {
-        if (vec) {
+        if constexpr (VEC) {
             unpack<T, EPT>(nt ? ld_nt(p) : ld_v(p), x);
         } else {
 #pragma unroll
@@ -820,9 +822,13 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
         const float r = r32[i];
 #pragma unroll
         for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
-        if (step_end[i]) {     // uniform: one do() call ends here
-            adapt_vec<DT, VARIANT, EPT>(b, c, aliased, m, v, c, b1, omb1, b2, omb2, eta, tau);
-            aliased = false;
+        if (step_ends(step_end, i)) {     // uniform: one do() call ends here
+            if (__builtin_expect(aliased, 0)) {   // the first step after the passthrough: current IS base
+#pragma unroll
+                for (int j = 0; j < EPT; ++j) c[j] = b[j];
+                aliased = false;
+            }
+            adapt_vec<DT, VARIANT, EPT>(b, c, false, m, v, c, b1, omb1, b2, omb2, eta, tau);
         }
     };
     int i = 0;
@@ -849,12 +855,36 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
         T t[EPT];
 #pragma unroll
         for (int j = 0; j < EPT; ++j) t[j] = X::st(vals[o][j]);
-        if (vec) {
+        if constexpr (VEC) {
             st_v(outs[o], pack<T, EPT>(t));
         } else {
             for (int j = 0; j < nv; ++j) st1(outs[o] + j, t[j]);
         }
     }
+}
+
+template <int DT, int VARIANT, int CU>
+__global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segment* __restrict__ segs, int n_segs,
+                                                              const uint64_t* __restrict__ clients, int n_clients,
+                                                              const float* __restrict__ r32,
+                                                              const uint8_t* __restrict__ step_end, unsigned flags,
+                                                              float b1, float omb1, float b2, float omb2, float eta,
+                                                              float tau) {
+    static_assert(kVPT == 1, "fedopt_chain_kernel: a lane handles one 16-byte vector of its chunk");
+    const int64_t chunk = blockIdx.x;
+    const int s = find_segment(segs, n_segs, chunk);
+    const flame_segment sg = segs[s];
+    const int64_t c0 = (chunk - sg.chunk_begin) * chunk_elems<DT>();
+    const int64_t e0 = c0 + static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
+    if (e0 >= sg.numel) return;
+    const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
+    const int64_t coff = client_offset<DT>(sg, chunk);
+    if (c0 + chunk_elems<DT>() <= sg.numel && !(sg.flags & FLAME_SEG_UNALIGNED))    // workgroup-uniform
+        fedopt_chain_body<DT, VARIANT, CU, true>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2,
+                                                 omb2, eta, tau);
+    else
+        fedopt_chain_body<DT, VARIANT, 1, false>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2,
+                                                 omb2, eta, tau);
 }
 
 // ---------------------------------------------------------------- FedBuff scale-add (+delta)
@@ -1210,8 +1240,7 @@ __device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restric
     using A = typename X::A;
     constexpr int EPT = X::EPT;
     constexpr int NV = kBlock / 64;                       // elements blocks per epilogue lane
-    static_assert(kVPT == 1 && sizeof(A) * EPT % 16 == 0, "hier_ws_body: one 16-byte vector per lane");
-    constexpr int AV = sizeof(A) * EPT / 16;              // 16-byte words of a lane's sums
+    static_assert(kVPT == 1, "hier_ws_body: one 16-byte vector per lane");
     const int64_t chunk = blockIdx.x;
     const int s = find_segment(segs, n_segs, chunk);
     const flame_hier_segment sg = segs[s];
@@ -1235,8 +1264,15 @@ __device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restric
                              mid_rates, mid_goal, top_rates, top_goal, flags);
         return;
     }
-    __shared__ V16 sums[2][AV][kBlock];     // the streamers' sums of a middle, double-buffered
-    __shared__ V16 held[HB * kBlock];       // the epilogue's store group
+    // Dynamic LDS (hier_ws_lds_bytes): [2][kBlock] the streamers' sums of a middle, double-
+    // buffered, in the dtype (every partial sum is already rounded to it by X::add, so the 16-byte
+    // vector holds it exactly), then [HB][kBlock] the epilogue's store group.  Dynamic, so that
+    // the compiler does not size the registers for the occupancy a static LDS footprint implies
+    // (it rounds the allocation up to 136 VGPRs, 3 waves per SIMD, and two 5-wave workgroups
+    // then rarely fit on a CU).
+    extern __shared__ V16 ws_lds[];
+    V16 (*sums)[kBlock] = reinterpret_cast<V16 (*)[kBlock]>(ws_lds);
+    V16* held = ws_lds + 2 * kBlock;
     if (!epi) {
         const int64_t e0 = cbase + static_cast<int64_t>(threadIdx.x) * EPT;
         const int64_t coff = client_offset<DT>(sg, chunk);
@@ -1246,10 +1282,10 @@ __device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restric
             reduce_clients<DT, CU, true>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
                                          mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
                                          coff);
-            V16 w[AV];
-            __builtin_memcpy(w, acc[0], sizeof(w));
+            T w[EPT];
 #pragma unroll
-            for (int a = 0; a < AV; ++a) sums[m & 1][a][threadIdx.x] = w[a];
+            for (int j = 0; j < EPT; ++j) w[j] = X::st(acc[0][j]);
+            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);
             __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1
         }
         return;
@@ -1289,16 +1325,12 @@ __device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restric
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             const int vl = lane + 64 * k;
-            V16 sw[AV];
-#pragma unroll
-            for (int a = 0; a < AV; ++a) sw[a] = sums[m & 1][a][vl];
-            A acc[EPT];
-            __builtin_memcpy(acc, sw, sizeof(acc));
-            T w[EPT], d[EPT];
+            T sm[EPT], w[EPT], d[EPT];
+            unpack<T, EPT>(sums[m & 1][vl], sm);
             unpack<T, EPT>(wcur[k], w);
 #pragma unroll
             for (int j = 0; j < EPT; ++j) {
-                S::op(w[j], X::st(acc[j]), g, static_cast<double>(g), &d[j]);
+                S::op(w[j], sm[j], g, static_cast<double>(g), &d[j]);
                 const A t = X::tmp(d[j], rt, 0.0);
                 top[k][j] = have_top ? X::add(top[k][j], t) : t;
             }
@@ -1329,6 +1361,19 @@ __device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restric
             st_v(gp, pack<T, EPT>(gw));
         }
     }
+}
+
+template <int HB> constexpr int hier_ws_lds_bytes() { return (2 + HB) * kBlock * static_cast<int>(sizeof(V16)); }
+
+// Lift a WS instantiation's dynamic-LDS ceiling to what it uses (above the 64 KiB default);
+// false (and a flame_last_error message) if the runtime refuses.
+bool ws_lds_ok(const void* f) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, hier_ws_lds_bytes<kHBL>());
+    if (e != hipSuccess) {
+        set_err(FLAME_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s", hipGetErrorString(e));
+        return false;
+    }
+    return true;
 }
 
 template <int DT, int CU, int HB>
@@ -1969,8 +2014,9 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
 #define FLAME_HIER_LAUNCH(DT, CUV, CUL, LOLDS)                                                                  \
     if (lds) {                                                                                                 \
         if (sync) FLAME_HIER_GO(DT, CUL, true, kHBL, true, 0);                                                 \
-        else if (kHierWS)                                                                                      \
-            hipLaunchKernelGGL((hier_ws_kernel<DT, CUL, kHBL>), grid, dim3(kBlock + 64), 0, st, segs, n_segs,  \
+        else if (kHierWS && ws_lds_ok(reinterpret_cast<const void*>(hier_ws_kernel<DT, CUL, kHBL>)))             \
+            hipLaunchKernelGGL((hier_ws_kernel<DT, CUL, kHBL>), grid, dim3(kBlock + 64),                       \
+                               hier_ws_lds_bytes<kHBL>(), st, segs, n_segs,                                    \
                                n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);  \
         else FLAME_HIER_GO(DT, CUL, false, kHBL, true, 0);                                                     \
         br = BR_HIER_LDS + DT * 2 + sync;                                                                      \
@@ -2083,7 +2129,8 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
         return -set_err(FLAME_ENOTSUP, "flame_hier_resident_per_cu: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     int blocks = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, block, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, block,
+                                                                       block > kBlock ? hier_ws_lds_bytes<kHBL>() : 0);
     if (e != hipSuccess) return -set_err(FLAME_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
     return blocks < 1 ? 1 : blocks;
 }

@@ -75,10 +75,10 @@ EDITS = [
      "                st_v(gp, pack<T, EPT>(gw));\n            }\n        }\n"
      f"        FLAME_HT({W0}, 1);\n        return;\n    }}\n    hier_tail<DT, SYNC>("),
     # hier_ws_body: streamers
-    ("#pragma unroll\n            for (int a = 0; a < AV; ++a) sums[m & 1][a][threadIdx.x] = w[a];\n"
+    ("            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);\n"
      "            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1\n",
      f"            FLAME_HT({W0}, 3 + 2 * n_mids + {NB} + 2 * m);\n"
-     "#pragma unroll\n            for (int a = 0; a < AV; ++a) sums[m & 1][a][threadIdx.x] = w[a];\n"
+     "            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);\n"
      "            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1\n"
      f"            FLAME_HT({W0}, 4 + 2 * n_mids + {NB} + 2 * m);\n"),
     # hier_ws_body: the epilogue wave
@@ -97,10 +97,9 @@ EDITS = [
      "#pragma unroll 1\n            for (int uu = 0; uu <= u; ++uu)\n#pragma unroll\n"
      "                for (int k = 0; k < NV; ++k) st_v(mid_ptr(m - u + uu, k), held[uu * kBlock + lane + 64 * k]);\n"
      "        }\n        if (u == HB - 1 || m == n_mids - 1) FLAME_HT(lane == 0, 3 + 2 * n_mids + m / HB);\n"),
-    ("            st_v(gp, pack<T, EPT>(gw));\n        }\n    }\n}\n\ntemplate <int DT, int CU, int HB>\n"
-     "__global__ __launch_bounds__(kBlock + 64) void hier_ws_kernel(",
+    ("            st_v(gp, pack<T, EPT>(gw));\n        }\n    }\n}\n\ntemplate <int HB> constexpr int hier_ws_lds_bytes()",
      "            st_v(gp, pack<T, EPT>(gw));\n        }\n    }\n    FLAME_HT(lane == 0, 1);\n}\n\n"
-     "template <int DT, int CU, int HB>\n__global__ __launch_bounds__(kBlock + 64) void hier_ws_kernel("),
+     "template <int HB> constexpr int hier_ws_lds_bytes()"),
 ]
 
 
