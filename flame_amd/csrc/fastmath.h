@@ -11,6 +11,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef FLAME_T_SQRT_NUDGE
+#define FLAME_T_SQRT_NUDGE 0
+#endif
+
 namespace flame_fm {
 
 // RN(sqrt(x)) for x = +0 or 2^-96 <= x <= 2^78: from v_rsq_f32, s = x*y, h = y/2 and one
@@ -20,7 +24,13 @@ __device__ __forceinline__ bool sqrt_admits(float x) {
     return (__float_as_uint(x) == 0u) | ((x >= 0x1p-96f) & (x <= 0x1p78f));
 }
 __device__ __forceinline__ float sqrt_rn(float x) {
+#if FLAME_T_SQRT_NUDGE
+    // +0 nudged to the smallest subnormal for the seed only (a normal x is unchanged by the add):
+    // one packed add per pair instead of a min per element
+    const float y = __builtin_amdgcn_rsqf(x + 0x1p-149f);
+#else
     const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+#endif
     const float s = x * y;
     const float h = 0.5f * y;
     const float r = __builtin_fmaf(-s, s, x);
@@ -47,6 +57,27 @@ __device__ __forceinline__ float div_rn(float a, float b) {
     const float q0 = a * y;
     const float rn = __builtin_fmaf(b, q0, -a);
     return __builtin_fmaf(-rn, y, q0);
+}
+
+// The same admission for a lane's n elements at once, with four compares in all (per-element
+// compares cost six VALU instructions and five scalar ones each): every v +0 or in
+// [2^-96, 2^78] -- unsigned min of bits-1 (0 wraps to the top) and max of bits (a sign, an inf or
+// a NaN is above the bound) -- and every num +-0 or 2^-85 <= |num| <= 2^100 -- unsigned min of
+// 2*bits-2 (drops the sign; +-0 wraps to the top) and the max of |num| (a NaN num passes it: the
+// quotient is NaN on either path, and NaN bits are not part of the contract).
+template <int N>
+__device__ __forceinline__ bool admits(const float (&v)[N], const float (&num)[N]) {
+    uint32_t vlo = 0xffffffffu, vhi = 0u, nlo = 0xffffffffu;
+    float nhi = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const uint32_t vb = __float_as_uint(v[j]), nb = __float_as_uint(num[j]);
+        vlo = min(vlo, vb - 1u);
+        vhi = max(vhi, vb);
+        nlo = min(nlo, (nb << 1) - 2u);
+        nhi = fmaxf(nhi, __builtin_fabsf(num[j]));
+    }
+    return (vlo >= 0x0f800000u - 1u) & (vhi <= 0x66800000u) & (nlo >= (0x15000000u << 1) - 2u) & (nhi <= 0x1p100f);
 }
 
 }  // namespace flame_fm

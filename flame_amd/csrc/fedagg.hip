@@ -139,7 +139,22 @@ constexpr int kHLoLds16 = FLAME_T_HLO_LDS16;     // 3 workgroups per CU
 #ifndef FLAME_T_DYN_UNROLL
 #define FLAME_T_DYN_UNROLL 4
 #endif
-constexpr int kDynUnroll = FLAME_T_DYN_UNROLL;        // FedDyn kernel: program steps whose loads are issued together
+constexpr int kDynUnroll = FLAME_T_DYN_UNROLL;
+#ifndef FLAME_T_CHAIN_UNROLL
+#define FLAME_T_CHAIN_UNROLL 16
+#endif
+constexpr int kChainUnroll = FLAME_T_CHAIN_UNROLL;     // eager FedOPT chain: client loads in flight per lane
+#ifndef FLAME_T_CHAIN_UNROLL16
+#define FLAME_T_CHAIN_UNROLL16 8
+#endif
+constexpr int kChainUnroll16 = FLAME_T_CHAIN_UNROLL16;
+// fp32 chain: 16 client loads in flight per lane at 3 workgroups per CU (dynamic LDS as the cap):
+// 1.453 -> 1.358 ms per 64 x 25M round against 8 at full residency, one process, bitwise
+// (profiles/r05g_chain_ab.log); 16-bit chains keep 8 at full residency
+#ifndef FLAME_T_CHAIN_LDS
+#define FLAME_T_CHAIN_LDS 53248
+#endif
+constexpr int kChainLds = FLAME_T_CHAIN_LDS;           // dynamic LDS per fp32 workgroup (a residency cap)        // FedDyn kernel: program steps whose loads are issued together
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -557,13 +572,12 @@ __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
                                           float omb1, float b2, float omb2, float eta, float tau) {
     float c[EPT], num[EPT];
-    unsigned ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f);       // no short-circuit branches
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         c[j] = cur_is_avg ? avg[j] : cur[j];
         adapt_moments<DT, VARIANT>(avg[j], c[j], m[j], v[j], num[j], b1, omb1, b2, omb2, eta);
-        ok &= static_cast<unsigned>(flame_fm::sqrt_admits(v[j])) & static_cast<unsigned>(flame_fm::div_admits(num[j]));
     }
+    const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & flame_fm::admits<EPT>(v, num);
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) {     // wave-uniform
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
@@ -818,11 +832,10 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
     auto load_client = [&](int i, T (&x)[EPT]) {
         load_t(reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[i]) + coff), x, true);
     };
-    auto arrive = [&](int i, const T (&x)[EPT]) {
-        const float r = r32[i];
+    auto arrive = [&](const T (&x)[EPT], float r, bool ends) {
 #pragma unroll
         for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
-        if (step_ends(step_end, i)) {     // uniform: one do() call ends here
+        if (ends) {     // uniform: one do() call ends here
             if (__builtin_expect(aliased, 0)) {   // the first step after the passthrough: current IS base
 #pragma unroll
                 for (int j = 0; j < EPT; ++j) c[j] = b[j];
@@ -834,15 +847,22 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
     int i = 0;
     for (; i + CU <= n_clients; i += CU) {
         T x[CU][EPT];
+        float rr[CU];
+        bool ends[CU];
 #pragma unroll
         for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
 #pragma unroll
-        for (int u = 0; u < CU; ++u) arrive(i + u, x[u]);
+        for (int u = 0; u < CU; ++u) {     // the batch's scalar loads issued together, one wait
+            rr[u] = r32[i + u];
+            ends[u] = step_ends(step_end, i + u);
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) arrive(x[u], rr[u], ends[u]);
     }
     for (; i < n_clients; ++i) {
         T x[EPT];
         load_client(i, x);
-        arrive(i, x);
+        arrive(x, r32[i], step_ends(step_end, i));
     }
     if (aliased) {             // no step closed: current is still the base
 #pragma unroll
@@ -1889,15 +1909,17 @@ int flame_fedopt_chain(int dtype, int variant, unsigned flags, const flame_segme
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
 #define FLAME_CHAIN_LAUNCH(DT, V, CUV)                                                                              \
-    hipLaunchKernelGGL((fedopt_chain_kernel<DT, V, CUV>), grid, block, 0, st, segs, n_segs, cl, n_clients, rates32, \
+    hipLaunchKernelGGL((fedopt_chain_kernel<DT, V, CUV>), grid, block, DT == FLAME_F32 ? kChainLds : 0, st, segs,   \
+                       n_segs, cl, n_clients,                                                                       \
+                       rates32,                                                                                     \
                        step_end, flags, b1, omb1, b2, omb2, eta, tau)
 #define FLAME_CHAIN_VARIANTS(DT, CUV)                                                  \
     if (variant == FLAME_FEDADAM) FLAME_CHAIN_LAUNCH(DT, FLAME_FEDADAM, CUV);          \
     else if (variant == FLAME_FEDYOGI) FLAME_CHAIN_LAUNCH(DT, FLAME_FEDYOGI, CUV);     \
     else FLAME_CHAIN_LAUNCH(DT, FLAME_FEDADAGRAD, CUV);
-    if (dtype == FLAME_F32) { FLAME_CHAIN_VARIANTS(FLAME_F32, kClientUnroll) }
-    else if (dtype == FLAME_BF16) { FLAME_CHAIN_VARIANTS(FLAME_BF16, kClientUnroll16) }
-    else { FLAME_CHAIN_VARIANTS(FLAME_F16, kClientUnroll16) }
+    if (dtype == FLAME_F32) { FLAME_CHAIN_VARIANTS(FLAME_F32, kChainUnroll) }
+    else if (dtype == FLAME_BF16) { FLAME_CHAIN_VARIANTS(FLAME_BF16, kChainUnroll16) }
+    else { FLAME_CHAIN_VARIANTS(FLAME_F16, kChainUnroll16) }
 #undef FLAME_CHAIN_VARIANTS
 #undef FLAME_CHAIN_LAUNCH
     return launched(BR_CHAIN + dtype * 3 + variant, "flame_fedopt_chain");

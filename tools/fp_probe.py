@@ -28,18 +28,23 @@ def f2b(x):
 def build():
     from flame_amd import build as B
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-o", LIB, os.path.join(ROOT, "tools", "fp_probe.hip")])
+    src = os.path.join(ROOT, "tools", "fp_probe.hip")
+    subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-o", LIB, src])
+    # the FLAME_T_SQRT_NUDGE variant of sqrt_rn (a sweep knob of fastmath.h)
+    subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-DFLAME_T_SQRT_NUDGE=1", "-o",
+                           LIB.replace(".so", "_nudge.so"), src])
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--div-pairs", type=float, default=2 ** 36)
+    ap.add_argument("--lib", default=LIB)
     a = ap.parse_args()
     if a.build:
         return build()
     import torch
-    L = ctypes.CDLL(LIB)
+    L = ctypes.CDLL(a.lib)
     out = torch.zeros(5, dtype=torch.int64, device="cuda")
     p = ctypes.c_void_p(out.data_ptr())
     u64 = ctypes.c_uint64

@@ -38,7 +38,18 @@ VARIANTS = {
     "optcu4": {"FLAME_T_OPT_UNROLL": 4},
     "dyncu2": {"FLAME_T_DYN_UNROLL": 2},
     "dyncu8": {"FLAME_T_DYN_UNROLL": 8},
-    "chaincu4": {"FLAME_T_CLIENT_UNROLL": 4},
+    "chain_cu8_full": {"FLAME_T_CHAIN_UNROLL": 8, "FLAME_T_CHAIN_LDS": 0},     # round 4's configuration
+    "sqrt_nudge": {"FLAME_T_SQRT_NUDGE": 1},
+    "chain_cu4": {"FLAME_T_CHAIN_UNROLL": 4},
+    "chain_cu16": {"FLAME_T_CHAIN_UNROLL": 16},
+    "chain_occ4": {"FLAME_T_CHAIN_LDS": 40960},     # 4 workgroups per CU
+    "chain_occ3": {"FLAME_T_CHAIN_LDS": 53248},
+    "chain_occ2": {"FLAME_T_CHAIN_LDS": 65536},
+    "chain_cu16_occ3": {"FLAME_T_CHAIN_UNROLL": 16, "FLAME_T_CHAIN_LDS": 53248},
+    "chain_cu16_occ4": {"FLAME_T_CHAIN_UNROLL": 16, "FLAME_T_CHAIN_LDS": 40960},
+    "chain_cu12_occ3": {"FLAME_T_CHAIN_UNROLL": 12, "FLAME_T_CHAIN_LDS": 53248},
+    "chain_cu32": {"FLAME_T_CHAIN_UNROLL": 32},
+    "chain_cu24_occ3": {"FLAME_T_CHAIN_UNROLL": 24, "FLAME_T_CHAIN_LDS": 53248},
 }
 
 
