@@ -11,10 +11,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#ifndef FLAME_T_SQRT_NUDGE
-#define FLAME_T_SQRT_NUDGE 0
-#endif
-
 namespace flame_fm {
 
 // RN(sqrt(x)) for x = +0 or 2^-96 <= x <= 2^78: from v_rsq_f32, s = x*y, h = y/2 and one
@@ -24,13 +20,9 @@ __device__ __forceinline__ bool sqrt_admits(float x) {
     return (__float_as_uint(x) == 0u) | ((x >= 0x1p-96f) & (x <= 0x1p78f));
 }
 __device__ __forceinline__ float sqrt_rn(float x) {
-#if FLAME_T_SQRT_NUDGE
-    // +0 nudged to the smallest subnormal for the seed only (a normal x is unchanged by the add):
-    // one packed add per pair instead of a min per element
-    const float y = __builtin_amdgcn_rsqf(x + 0x1p-149f);
-#else
+    // (a cheaper alternative, the seed of x + 2^-149 -- a packed add instead of a min -- fails at
+    // +0: v_rsq_f32 flushes the subnormal, profiles/r05h_fp_probe_nudge.log)
     const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
-#endif
     const float s = x * y;
     const float h = 0.5f * y;
     const float r = __builtin_fmaf(-s, s, x);

@@ -562,11 +562,11 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
 }
 
 // A lane's EPT elements of one adaptive step (cur_is_avg: current IS the average, d = 0).  When
-// every lane of the wave has its operands in the range fastmath.h admits -- v = +0 or
-// [2^-96, 2^78], eta*m = +-0 or 2^-85 <= |.| <= 2^100, tau in [2^-20, 2^38] (so sqrt(v) + tau is
-// in [2^-20, 2^40]) -- the square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp
+// the lane's operands are all in the range fastmath.h admits -- v = +0 or [2^-96, 2^78],
+// eta*m = +-0 or 2^-85 <= |.| <= 2^100, tau in [2^-20, 2^38] (so sqrt(v) + tau is in
+// [2^-20, 2^40]) -- the square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp
 // seeds, packed fma), else the general sequences.  Both give the same bits (tools/fp_probe.py),
-// so which one a wave takes never shows in the results.
+// so which one a lane takes never shows in the results.
 template <int DT, int VARIANT, int EPT>
 __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (&cur)[EPT], bool cur_is_avg,
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
@@ -578,7 +578,7 @@ __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (
         adapt_moments<DT, VARIANT>(avg[j], c[j], m[j], v[j], num[j], b1, omb1, b2, omb2, eta);
     }
     const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & flame_fm::admits<EPT>(v, num);
-    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {     // wave-uniform
+    if (ok) {         // per lane (exec-masked; a wave whose lanes all agree runs one side only)
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const float den = rnd<DT>(__fadd_rn(rnd<DT>(flame_fm::sqrt_rn(v[j])), tau));

@@ -1,9 +1,9 @@
 """GPU: the FedOPT step's fast correctly rounded sqrt / divide (flame_amd/csrc/fastmath.h) and its
-wave-uniform fallback (adapt_vec), against the C oracle, bit for bit.
+per-lane fallback (adapt_vec), against the C oracle, bit for bit.
 
-adapt_vec takes sqrt_rn / div_rn for a wave only when every lane's v is +0 or in [2^-96, 2^78]
-and every eta*m is +-0 or in [2^-85, 2^100]; any other operand sends the whole wave through the
-general sequences.  Both are correctly rounded, as the C oracle's sqrtf and division are
+adapt_vec takes sqrt_rn / div_rn for a lane only when each of its elements' v is +0 or in
+[2^-96, 2^78] and each eta*m is +-0 or in [2^-85, 2^100]; any other operand sends that lane through
+the general sequences (the rest of its wave stays on the fast path).  Both are correctly rounded, as the C oracle's sqrtf and division are
 (oracle/fedagg_oracle.c:191-220, fedopt.py:102-129), so fp32 results equal the oracle's bitwise
 -- on either side of every admission boundary.  The model below puts one boundary case in each of
 a run of waves (a wave = 64 lanes x 4 fp32 elements), the rest of them ordinary, and runs the

@@ -30,9 +30,6 @@ def build():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     src = os.path.join(ROOT, "tools", "fp_probe.hip")
     subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-o", LIB, src])
-    # the FLAME_T_SQRT_NUDGE variant of sqrt_rn (a sweep knob of fastmath.h)
-    subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-DFLAME_T_SQRT_NUDGE=1", "-o",
-                           LIB.replace(".so", "_nudge.so"), src])
 
 
 def main():

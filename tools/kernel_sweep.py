@@ -39,7 +39,6 @@ VARIANTS = {
     "dyncu2": {"FLAME_T_DYN_UNROLL": 2},
     "dyncu8": {"FLAME_T_DYN_UNROLL": 8},
     "chain_cu8_full": {"FLAME_T_CHAIN_UNROLL": 8, "FLAME_T_CHAIN_LDS": 0},     # round 4's configuration
-    "sqrt_nudge": {"FLAME_T_SQRT_NUDGE": 1},
     "chain_cu4": {"FLAME_T_CHAIN_UNROLL": 4},
     "chain_cu16": {"FLAME_T_CHAIN_UNROLL": 16},
     "chain_occ4": {"FLAME_T_CHAIN_LDS": 40960},     # 4 workgroups per CU
