@@ -513,6 +513,33 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
         }), flush=True)
 
 
+def traffic_lookup(path, **match):
+    """HBM bytes per launch from the PMC-derived table (tools/pmc_traffic.py writes it from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs): the LAST entry whose fields equal ``match``
+    (``None`` in ``match`` = the field is absent or anything; a missing entry field counts as its
+    given default), with where the bytes came from -- a lookup, not this run's counters."""
+    try:
+        entries = json.load(open(path))
+        entries = entries["entries"] if "entries" in entries else [entries]
+    except Exception:  # noqa: BLE001
+        return None, None
+    hit = None
+    for tr in entries:
+        if all(v is None or tr.get(k, _TRAFFIC_DEFAULTS.get(k)) == v for k, v in match.items()):
+            hit = tr
+    if hit is None:
+        return None, None
+    return hit["hbm_bytes_per_launch"], {
+        "kind": "lookup", "file": os.path.relpath(path, ROOT),
+        "entry": {k: hit.get(k) for k in ("kernel", "clients", "params", "layout", "workload")},
+        "counters": hit.get("source", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (source not recorded in "
+                                      "this entry)"),
+        "traffic_over_algorithmic": hit.get("traffic_over_algorithmic")}
+
+
+_TRAFFIC_DEFAULTS = {"layout": "row", "middle_weights": "own"}
+
+
 def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     """The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) on
     device-resident updates: base = deepcopy(weights), then one do() per arrival with the
@@ -562,13 +589,7 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
-        traffic = None
-        try:
-            for tr in json.load(open(args.traffic))["entries"]:
-                if tr.get("kernel") == kname and tr.get("clients") == n and tr.get("params") == P:
-                    traffic = tr["hbm_bytes_per_launch"]
-        except Exception:  # noqa: BLE001
-            pass
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P)
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -580,10 +601,12 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
+                         "traffic_source": traffic_source,
                          "bytes_per_client_param": k_bytes / (n * P * 4),
                          **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
-                                     "element (~41 VALU ops each, the correctly rounded sqrt and divide "
-                                     "among them): VALU-bound near its HBM time (DESIGN.md §4)"}
+                                     "element (~20 VALU instructions each with the fast correctly rounded "
+                                     "sqrt and divide, 2 of them quarter-rate transcendentals): VALU and "
+                                     "HBM both ~70-75 % busy (DESIGN.md §4)"}
                             if fedopt and defer else {})},
         }), flush=True)
 
@@ -709,23 +732,8 @@ def main():
     ks = kernel_stats(events, name)
 
     if rank == 0:
-        traffic, traffic_source = None, None
-        try:
-            doc = json.load(open(args.traffic))
-            for tr in (doc["entries"] if "entries" in doc else [doc]):
-                if (tr.get("kernel") == name and tr.get("clients") == n and tr.get("params") == P
-                        and tr.get("layout", "row") == args.layout
-                        and tr.get("workload", args.workload) == args.workload):
-                    traffic = tr["hbm_bytes_per_launch"]
-                    # a LOOKUP, not this run's counters: PMC passes run in their own processes
-                    # (rocprofv3 --pmc, tools/pmc_traffic.py); name where the bytes came from
-                    traffic_source = {"kind": "lookup", "file": os.path.relpath(args.traffic, ROOT),
-                                      "entry": {k: tr.get(k) for k in ("kernel", "clients", "params", "layout")},
-                                      "counters": tr.get("source", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
-                                                         "(source not recorded in this entry)"),
-                                      "traffic_over_algorithmic": tr.get("traffic_over_algorithmic")}
-        except Exception:  # noqa: BLE001
-            pass
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=name, clients=n, params=P, layout=args.layout,
+                                                 workload=args.workload)
         cpu = None
         if world == 1 and args.cpu_clients > 0 and args.workload == "fedavg":
             cpu = cpu_baseline(host_row, n, P, base0, counts, args.cpu_clients, args.cpu_rounds)
@@ -1240,14 +1248,8 @@ def bench_fedbuff(args, world, rank, dev):
 
     elapsed, events = timed(world, args.steps, args.warmup, step)
     if rank == 0:
-        traffic = None
-        try:
-            for tr in json.load(open(args.traffic))["entries"]:
-                if (tr.get("kernel") == "flame_hier_fedbuff" and tr.get("workload") == "fedbuff"
-                        and tr.get("clients") == K and tr.get("params") == P):
-                    traffic = tr["hbm_bytes_per_launch"]
-        except Exception:  # noqa: BLE001
-            pass
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel="flame_hier_fedbuff", workload="fedbuff",
+                                                 clients=K, params=P)
         kst = {nm: kernel_stats(events, nm) for nm in sorted({e[0] for e in events})}
         k_time = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         k_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kst.values()) / args.steps
@@ -1260,7 +1262,7 @@ def bench_fedbuff(args, world, rank, dev):
                        "fuse_scale_add": args.fedbuff_fuse},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel_ms_per_step": k_time * 1e3,
-                         "algorithmic_bytes_per_step": k_bytes, "traffic": traffic,
+                         "algorithmic_bytes_per_step": k_bytes, "traffic": traffic, "traffic_source": traffic_source,
                          "bytes_per_client_param": k_bytes / (K * P * 4)},
             "kernels": kst, "launch_branches": br,
         }), flush=True)
@@ -1408,15 +1410,10 @@ def bench_hier(args, world, rank, dev):
     names = tuple(seen) if seen and seen[0] == first else (first,)
     kst = {nm: kernel_stats(events, nm) for nm in seen}
     red = kst.get(names[0]) or next(iter(kst.values()))
-    traffic = None
+    traffic, traffic_source = None, None
     if rank == 0 and args.hier_mode == "fused":
-        try:
-            for tr in json.load(open(args.traffic))["entries"]:
-                if (tr.get("kernel") == names[0] and tr.get("clients") == M * C and tr.get("params") == P
-                        and tr.get("middle_weights", "own") == args.hier_middles):
-                    traffic = tr["hbm_bytes_per_launch"]
-        except Exception:  # noqa: BLE001
-            pass
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=names[0], clients=M * C, params=P,
+                                                 middle_weights=args.hier_middles)
     if rank == 0:
         per_step_kernel = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         sync = args.hier_mode.startswith("sync")
@@ -1431,7 +1428,7 @@ def bench_hier(args, world, rank, dev):
                                         "middles": args.hier_mode, "middle_weights": args.hier_middles,
                                         "arrivals": args.hier_arrivals},
             "roofline": {"bound": "hbm", "achieved": red["achieved_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic,
+                         "frac": red["achieved_GBps"] / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_source,
                          "kernel": names[0], "kernel_ms": red["avg_s"] * 1e3,
                          "algorithmic_bytes": red["bytes_per_launch"],
                          "measured_read_ceiling_GBps": ceiling, "read_probes_GBps": probes,
