@@ -4,10 +4,11 @@
 // operands (16 and 13 instructions, two of them quarter-rate, and none of them packable).
 //
 // Each function returns the SAME bits as the general sequence on the operands its admission
-// predicate accepts; the caller takes the general sequence for a wave where any lane's operand
-// is not admitted.  tools/fp_probe.py checks the equality on the MI355X: exhaustively for sqrt_rn
-// (every admitted x) and rcp_rn (every admitted b), and on 2^39 counter-drawn admitted pairs for
-// div_rn (profiles/r05_fp_probe.log).
+// predicate accepts, or (admits: v below 2^-96) bits that cannot change the step's results; the
+// caller takes the general sequence for a lane where any operand is not admitted.
+// tools/fp_probe.py checks this on the MI355X: exhaustively for sqrt_rn (every admitted x, and
+// every v below 2^-96 through sqrt(v) + tau) and rcp_rn (every admitted b), and on counter-drawn
+// admitted pairs for div_rn.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -51,25 +52,32 @@ __device__ __forceinline__ float div_rn(float a, float b) {
     return __builtin_fmaf(-rn, y, q0);
 }
 
-// The same admission for a lane's n elements at once, with four compares in all (per-element
-// compares cost six VALU instructions and five scalar ones each): every v +0 or in
-// [2^-96, 2^78] -- unsigned min of bits-1 (0 wraps to the top) and max of bits (a sign, an inf or
-// a NaN is above the bound) -- and every num +-0 or 2^-85 <= |num| <= 2^100 -- unsigned min of
-// 2*bits-2 (drops the sign; +-0 wraps to the top) and the max of |num| (a NaN num passes it: the
-// quotient is NaN on either path, and NaN bits are not part of the contract).
+// What a lane's n elements need for sqrt_rn / div_rn to give adapt_vec's results bit for bit,
+// with tau in [2^-20, 2^38] (checked by the caller), in three reductions:
+//  * every v in [+0, 2^78] (the unsigned max of the bits; a sign, an inf or a NaN is above it).
+//    On [2^-96, 2^78] and at +0 sqrt_rn is correctly rounded.  Below 2^-96 it is not, but only
+//    den = RN(sqrt(v) + tau) uses it: both roots are under 2^-47 there (sqrt_rn's seed is
+//    clamped at 2^64, so even a subnormal v that v_rsq_f32 flushes stays under 2^-60), far
+//    below half an ulp of tau >= 2^-20, so den = tau either way -- and no lower bound on v costs
+//    a compare;
+//  * every eta*m +-0 or 2^-85 <= |num| <= 2^100: unsigned min of 2*bits-2 (drops the sign; +-0
+//    wraps to the top) and the max of |num| (a NaN num passes it: the quotient is NaN on either
+//    path, and NaN bits are not part of the contract).
+// (A tiny eta*m could be admitted too while every current weight is >= 2^-30 -- c + q rounds to
+// c for either quotient -- but that reduction adds 3-7 VALU instructions to the ~77 of a lane's
+// 4-element step (ISA count), and only a weight whose average stays exactly equal to it decays m
+// that far.)
 template <int N>
 __device__ __forceinline__ bool admits(const float (&v)[N], const float (&num)[N]) {
-    uint32_t vlo = 0xffffffffu, vhi = 0u, nlo = 0xffffffffu;
+    uint32_t vhi = 0u, nlo = 0xffffffffu;
     float nhi = 0.f;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        const uint32_t vb = __float_as_uint(v[j]), nb = __float_as_uint(num[j]);
-        vlo = min(vlo, vb - 1u);
-        vhi = max(vhi, vb);
-        nlo = min(nlo, (nb << 1) - 2u);
+        vhi = max(vhi, __float_as_uint(v[j]));
+        nlo = min(nlo, (__float_as_uint(num[j]) << 1) - 2u);
         nhi = fmaxf(nhi, __builtin_fabsf(num[j]));
     }
-    return (vlo >= 0x0f800000u - 1u) & (vhi <= 0x66800000u) & (nlo >= (0x15000000u << 1) - 2u) & (nhi <= 0x1p100f);
+    return (vhi <= 0x66800000u) & (nhi <= 0x1p100f) & (nlo >= (0x15000000u << 1) - 2u);
 }
 
 }  // namespace flame_fm

@@ -154,7 +154,7 @@ constexpr int kChainUnroll16 = FLAME_T_CHAIN_UNROLL16;
 #ifndef FLAME_T_CHAIN_LDS
 #define FLAME_T_CHAIN_LDS 53248
 #endif
-constexpr int kChainLds = FLAME_T_CHAIN_LDS;           // dynamic LDS per fp32 workgroup (a residency cap)        // FedDyn kernel: program steps whose loads are issued together
+constexpr int kChainLds = FLAME_T_CHAIN_LDS;           // dynamic LDS per fp32 workgroup (a residency cap)
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -562,11 +562,11 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
 }
 
 // A lane's EPT elements of one adaptive step (cur_is_avg: current IS the average, d = 0).  When
-// the lane's operands are all in the range fastmath.h admits -- v = +0 or [2^-96, 2^78],
-// eta*m = +-0 or 2^-85 <= |.| <= 2^100, tau in [2^-20, 2^38] (so sqrt(v) + tau is in
-// [2^-20, 2^40]) -- the square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp
-// seeds, packed fma), else the general sequences.  Both give the same bits (tools/fp_probe.py),
-// so which one a lane takes never shows in the results.
+// the lane's operands are all in the range fastmath.h admits -- v in [+0, 2^78], eta*m = +-0 or
+// 2^-85 <= |.| <= 2^100, tau in [2^-20, 2^38] (so sqrt(v) + tau is in [2^-20, 2^40]) -- the
+// square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp seeds, packed fma), else
+// the general sequences.  Both give the same m, v and current (tools/fp_probe.py), so which one a
+// lane takes never shows in the results.
 template <int DT, int VARIANT, int EPT>
 __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (&cur)[EPT], bool cur_is_avg,
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
@@ -844,20 +844,30 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
             adapt_vec<DT, VARIANT, EPT>(b, c, false, m, v, c, b1, omb1, b2, omb2, eta, tau);
         }
     };
+    auto load_batch = [&](int i0, T (&x)[CU][EPT], float (&rr)[CU], bool (&ends)[CU]) {
+#pragma unroll
+        for (int u = 0; u < CU; ++u) load_client(i0 + u, x[u]);
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {     // the batch's scalar loads issued together, one wait
+            rr[u] = r32[i0 + u];
+            ends[u] = step_ends(step_end, i0 + u);
+        }
+    };
+    auto run_batch = [&](const T (&x)[CU][EPT], const float (&rr)[CU], const bool (&ends)[CU]) {
+#pragma unroll
+        for (int u = 0; u < CU; ++u) arrive(x[u], rr[u], ends[u]);
+    };
     int i = 0;
+    // (Two register batches -- the next batch's loads issued before this one's steps -- run no
+    // faster: 1.294 vs 1.287 ms at 8 loads per batch, 1.457 at 12, 3.40 at 16 (two 64-register
+    // batches); one process, bitwise, profiles/r05k_chain_pipe_ab.log.  Three resident
+    // workgroups of the plain batch loop already overlap one another's loads and arithmetic.)
     for (; i + CU <= n_clients; i += CU) {
         T x[CU][EPT];
         float rr[CU];
         bool ends[CU];
-#pragma unroll
-        for (int u = 0; u < CU; ++u) load_client(i + u, x[u]);
-#pragma unroll
-        for (int u = 0; u < CU; ++u) {     // the batch's scalar loads issued together, one wait
-            rr[u] = r32[i + u];
-            ends[u] = step_ends(step_end, i + u);
-        }
-#pragma unroll
-        for (int u = 0; u < CU; ++u) arrive(x[u], rr[u], ends[u]);
+        load_batch(i, x, rr, ends);
+        run_batch(x, rr, ends);
     }
     for (; i < n_clients; ++i) {
         T x[EPT];

@@ -1,14 +1,16 @@
 """GPU: the FedOPT step's fast correctly rounded sqrt / divide (flame_amd/csrc/fastmath.h) and its
 per-lane fallback (adapt_vec), against the C oracle, bit for bit.
 
-adapt_vec takes sqrt_rn / div_rn for a lane only when each of its elements' v is +0 or in
-[2^-96, 2^78] and each eta*m is +-0 or in [2^-85, 2^100]; any other operand sends that lane through
-the general sequences (the rest of its wave stays on the fast path).  Both are correctly rounded, as the C oracle's sqrtf and division are
-(oracle/fedagg_oracle.c:191-220, fedopt.py:102-129), so fp32 results equal the oracle's bitwise
--- on either side of every admission boundary.  The model below puts one boundary case in each of
-a run of waves (a wave = 64 lanes x 4 fp32 elements), the rest of them ordinary, and runs the
-per-call fused kernel (three rounds: passthrough, zero state, running state) and the deferred
-eager chain against OracleFedOPT.  NaN / inf positions are checked separately (their payloads
+adapt_vec takes sqrt_rn / div_rn for a lane only when each of its elements' v is in [+0, 2^78]
+and each eta*m is +-0 or in [2^-85, 2^100]; any other operand sends that lane through the general
+sequences (the rest of its wave stays on the fast path).  On [2^-96, 2^78] both are correctly
+rounded, as the C oracle's sqrtf and division are (oracle/fedagg_oracle.c:191-220,
+fedopt.py:102-129); below 2^-96 sqrt_rn is not, but sqrt(v) + tau is tau either way
+(fastmath.h).  So fp32 results equal the oracle's bitwise -- on either side of every admission
+boundary.  A tiny eta (1e-25) puts every eta*m below 2^-85: all lanes on the general divide.
+The model below puts one boundary case in each of a run of waves (a wave = 64 lanes x 4 fp32
+elements), the rest of them ordinary, and runs the per-call fused kernel (three rounds:
+passthrough, zero state, running state) and the deferred eager chain against OracleFedOPT.  NaN / inf positions are checked separately (their payloads
 are not part of the contract).
 """
 import copy
@@ -22,6 +24,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.oracle]
 
 DEV = "cuda:0"
 SORTS = ["fedadam", "fedyogi", "fedadagrad"]
+ETAS = [None, 1e-25]    # None: the optimizer's default; 1e-25: every eta*m below 2^-85
 WAVE = 256          # fp32 elements per wave of the FedOPT kernels (64 lanes x 4)
 
 # One element per case: its current weight is 0 and every client sends the same value d, so the
@@ -80,13 +83,18 @@ def _bits_equal_or_both_nan(label, got, exp):
                                   f"{et[keep][bad[:4]].tolist()}")
 
 
+def _kw(eta):
+    return {} if eta is None else {"eta": eta}
+
+
+@pytest.mark.parametrize("eta", ETAS)
 @pytest.mark.parametrize("sort", SORTS)
-def test_fused_step_admission_boundaries_bitwise(sort):
+def test_fused_step_admission_boundaries_bitwise(sort, eta):
     from oracle import oracle as O
     from flame_amd.optimizers import optimizer_provider
     cur = _model()
     g = torch.Generator().manual_seed(5)
-    amd, ora = optimizer_provider.get(sort), O.OracleFedOPT(sort)
+    amd, ora = optimizer_provider.get(sort, **_kw(eta)), O.OracleFedOPT(sort, **_kw(eta))
     wa, wo = {"w": cur.to(DEV)}, {"w": cur.clone()}
     for r in range(3):
         ups = _updates(cur.numel(), 4, g)
@@ -104,8 +112,9 @@ def test_fused_step_admission_boundaries_bitwise(sort):
             _bits_equal_or_both_nan(f"{sort}/r{r}/v", S.to_cpu(amd.v_t), ora.v_t)
 
 
+@pytest.mark.parametrize("eta", ETAS)
 @pytest.mark.parametrize("sort", SORTS)
-def test_chain_admission_boundaries_bitwise(sort):
+def test_chain_admission_boundaries_bitwise(sort, eta):
     """The eager round through FedOPT(defer=True) (one flame_fedopt_chain launch per round): 6
     arrivals per round, two rounds, every returned current, m_t and v_t == the oracle's
     per-call sequence, bitwise."""
@@ -114,7 +123,7 @@ def test_chain_admission_boundaries_bitwise(sort):
     cur = _model()
     g = torch.Generator().manual_seed(9)
     rounds = [[(u, 2 + 3 * i) for i, u in enumerate(_updates(cur.numel(), 6, g))] for _ in range(2)]
-    opt, ora = optimizer_provider.get(sort, defer=True), O.OracleFedOPT(sort)
+    opt, ora = optimizer_provider.get(sort, defer=True, **_kw(eta)), O.OracleFedOPT(sort, **_kw(eta))
     wa, wo = {"w": cur.to(DEV)}, {"w": cur.clone()}
     for r, arrivals in enumerate(rounds):
         ba, bo = copy.deepcopy(wa), copy.deepcopy(wo)
@@ -132,3 +141,4 @@ def test_chain_admission_boundaries_bitwise(sort):
         _bits_equal_or_both_nan(f"chain/{sort}/r{r}/cur", S.to_cpu(wa), wo)
         _bits_equal_or_both_nan(f"chain/{sort}/r{r}/m", S.to_cpu(opt.m_t), ora.m_t)
         _bits_equal_or_both_nan(f"chain/{sort}/r{r}/v", S.to_cpu(opt.v_t), ora.v_t)
+

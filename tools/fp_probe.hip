@@ -6,6 +6,7 @@
 //                               v_sqrt_f32 alone, 2 sqrt_fix, 3 sqrt_rsq2 -- vs __builtin_sqrtf
 //   probe_rcp(lo, hi, v, out):  every b in [lo, hi): v=0 v_rcp_f32, v=1 rcp_rn -- vs __fdiv_rn(1, b)
 //   probe_div(seed, n, w, out): n counter-drawn (a, b) pairs: div_rn vs __fdiv_rn(a, b)
+//   probe_den(lo, hi, tau, out): every v in [lo, hi): RN(sqrt_rn(v) + tau) vs RN(sqrtf(v) + tau)
 // out[0] = mismatches, out[1..2] = the first mismatching operands (bits), out[3..4] = results.
 // Built by tools/fp_probe.py (hipcc, same flags as the product library).
 #include <hip/hip_runtime.h>
@@ -105,6 +106,18 @@ __global__ void div_kernel(uint64_t seed, uint64_t n, int wide, unsigned long lo
     }
 }
 
+// The denominator adapt_vec forms from a v below sqrt_rn's exact range: sqrt(v) + tau.
+__global__ void den_kernel(uint64_t lo, uint64_t hi, float tau, unsigned long long* out) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = lo + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < hi; i += stride) {
+        const float v = __uint_as_float(static_cast<uint32_t>(i));
+        const float want = __fadd_rn(__builtin_sqrtf(v), tau);
+        const float got = __fadd_rn(flame_fm::sqrt_rn(v), tau);
+        if (__float_as_uint(got) != __float_as_uint(want))
+            report(out, static_cast<uint32_t>(i), __float_as_uint(tau), __float_as_uint(got), __float_as_uint(want));
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -124,6 +137,12 @@ int probe_rcp(uint64_t lo, uint64_t hi, int variant, unsigned long long* out) {
 int probe_div(uint64_t seed, uint64_t n, int wide, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
     div_kernel<<<8192, 256>>>(seed, n, wide, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_den(uint64_t lo, uint64_t hi, float tau, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    den_kernel<<<8192, 256>>>(lo, hi, tau, out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
 

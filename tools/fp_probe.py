@@ -74,6 +74,10 @@ def main():
         show(f"div_rn {n} admitted pairs (seed {seed})", L.probe_div(u64(seed), u64(n), 0, p), True)
     show(f"div_rn {n // 4} pairs over every finite a, b in [2^-60, 2^66] (outside the admitted range)",
          L.probe_div(u64(3), u64(n // 4), 1, p), False)
+    # adapt_vec admits v below 2^-96 too: it only reaches sqrt(v) + tau (tau >= 2^-20)
+    L.probe_den.argtypes = [u64, u64, ctypes.c_float, ctypes.c_void_p]
+    for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):
+        show(f"sqrt_rn(v) + {tau:g} on every v in [+0, 2^-96)", L.probe_den(0, SQ_LO, tau, p), True)
     print(f"fp_probe: {time.time() - t:.1f} s, {bad} failing check(s)", flush=True)
     return 1 if bad else 0
 
