@@ -112,10 +112,6 @@ constexpr int kHierLdsUnroll16 = FLAME_T_HIER_LDS_UNROLL16;
 #define FLAME_T_HLDS_MIN_MIDS 16
 #endif
 constexpr int kHLdsMinMids = FLAME_T_HLDS_MIN_MIDS;
-#ifndef FLAME_T_HIER_WS
-#define FLAME_T_HIER_WS 0
-#endif
-constexpr bool kHierWS = FLAME_T_HIER_WS;   // >= kHLdsMinMids async middles: a fifth wave runs the epilogues
 #ifndef FLAME_T_HLO_UNROLL
 #define FLAME_T_HLO_UNROLL 3
 #endif
@@ -1249,177 +1245,6 @@ __global__ __launch_bounds__(kBlock) void hier_fedbuff_kernel_argmeta(const ArgM
 }
 #pragma clang diagnostic pop
 
-// The asynchronous (FedBuff-mode) hierarchy of >= kHLdsMinMids middles with a workgroup of
-// kBlock + 64 lanes: waves 0-3 stream the middles' arrival reductions without a break; the fifth
-// wave runs every middle's epilogue (its weights -- prefetched one middle ahead -- scale_add,
-// delta, the top's accumulate, the LDS-held store group and its burst) while the four stream the
-// next middle.  The sums change hands through a double-buffered LDS block and one barrier per
-// middle.  Same op sequence, same bits as hier_fedbuff_body; chunks that are not whole and
-// aligned take hier_tail (the fifth wave has no elements there).
-template <int DT, int CU, int HB>
-__device__ __forceinline__ void hier_ws_body(const flame_hier_segment* __restrict__ segs, int n_segs, int n_mids,
-                                             int n_clients, const uint64_t* __restrict__ mid_w,
-                                             const uint64_t* __restrict__ mid_delta,
-                                             const uint64_t* __restrict__ clients,
-                                             const float* __restrict__ mid_rates,
-                                             const float* __restrict__ mid_goal,
-                                             const float* __restrict__ top_rates, float top_goal, unsigned flags) {
-    using X = Tr<DT>;
-    using S = SA<DT>;
-    using T = typename X::T;
-    using A = typename X::A;
-    constexpr int EPT = X::EPT;
-    constexpr int NV = kBlock / 64;                       // elements blocks per epilogue lane
-    static_assert(kVPT == 1, "hier_ws_body: one 16-byte vector per lane");
-    const int64_t chunk = blockIdx.x;
-    const int s = find_segment(segs, n_segs, chunk);
-    const flame_hier_segment sg = segs[s];
-    const int64_t cbase = (chunk - sg.chunk_begin) * chunk_elems<DT>();
-    const bool epi = threadIdx.x >= kBlock;
-    const uint64_t* wrow = mid_w + static_cast<int64_t>(s) * n_mids;
-    const uint64_t* drow = mid_delta ? mid_delta + static_cast<int64_t>(s) * n_mids : nullptr;
-    const uint64_t* crow = clients + static_cast<int64_t>(s) * n_mids * n_clients;
-    auto woff = [&](int vl) {     // byte offset of lane vl's elements in every middle's weights
-        return sg.mid_tile_stride
-            ? (chunk - sg.chunk_begin) * sg.mid_tile_stride + static_cast<int64_t>(vl) * EPT * sizeof(T)
-            : (cbase + static_cast<int64_t>(vl) * EPT) * static_cast<int64_t>(sizeof(T));
-    };
-    if (cbase + chunk_elems<DT>() > sg.numel || (sg.flags & FLAME_SEG_UNALIGNED)) {
-        if (epi) return;
-        const int64_t e0 = cbase + static_cast<int64_t>(threadIdx.x) * EPT;
-        if (e0 >= sg.numel) return;
-        const int64_t wo = woff(threadIdx.x);
-        auto mid_ptr = [&](int m) { return reinterpret_cast<T*>(reinterpret_cast<char*>(wrow[m]) + wo); };
-        hier_tail<DT, false>(sg, e0, client_offset<DT>(sg, chunk), wrow, drow, crow, mid_ptr, n_mids, n_clients,
-                             mid_rates, mid_goal, top_rates, top_goal, flags);
-        return;
-    }
-    // Dynamic LDS (hier_ws_lds_bytes): [2][kBlock] the streamers' sums of a middle, double-
-    // buffered, in the dtype (every partial sum is already rounded to it by X::add, so the 16-byte
-    // vector holds it exactly), then [HB][kBlock] the epilogue's store group.  Dynamic, so that
-    // the compiler does not size the registers for the occupancy a static LDS footprint implies
-    // (it rounds the allocation up to 136 VGPRs, 3 waves per SIMD, and two 5-wave workgroups
-    // then rarely fit on a CU).
-    extern __shared__ V16 ws_lds[];
-    V16 (*sums)[kBlock] = reinterpret_cast<V16 (*)[kBlock]>(ws_lds);
-    V16* held = ws_lds + 2 * kBlock;
-    if (!epi) {
-        const int64_t e0 = cbase + static_cast<int64_t>(threadIdx.x) * EPT;
-        const int64_t coff = client_offset<DT>(sg, chunk);
-#pragma unroll 1
-        for (int m = 0; m < n_mids; ++m) {
-            A acc[kVPT][EPT];
-            reduce_clients<DT, CU, true>(acc, true, crow + static_cast<int64_t>(m) * n_clients, n_clients,
-                                         mid_rates + static_cast<int64_t>(m) * n_clients, nullptr, e0, sg.numel,
-                                         coff);
-            T w[EPT];
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) w[j] = X::st(acc[0][j]);
-            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);
-            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1
-        }
-        return;
-    }
-    const int lane = threadIdx.x - kBlock;
-    int64_t wo[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) wo[k] = woff(lane + 64 * k);
-    auto mid_ptr = [&](int m, int k) { return reinterpret_cast<T*>(reinterpret_cast<char*>(wrow[m]) + wo[k]); };
-    A top[NV][EPT];
-    bool have_top = (flags & FLAME_HIER_TOP_ACCUM) != 0;
-    if (have_top) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            T b[EPT];
-            unpack<T, EPT>(ld_v(reinterpret_cast<const T*>(sg.top_agg_in) + cbase + (lane + 64 * k) * EPT), b);
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) top[k][j] = X::ld(b[j]);
-        }
-    }
-    V16 wnext[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) wnext[k] = ld_v(mid_ptr(0, k));
-#pragma unroll 1
-    for (int m = 0; m < n_mids; ++m) {
-        V16 wcur[NV];
-#pragma unroll
-        for (int k = 0; k < NV; ++k) wcur[k] = wnext[k];
-        if (m + 1 < n_mids) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) wnext[k] = ld_v(mid_ptr(m + 1, k));
-        }
-        __syncthreads();                    // middle m's sums are in sums[m & 1]
-        T* dp = (drow && drow[m]) ? reinterpret_cast<T*>(drow[m]) + cbase : nullptr;
-        const float g = mid_goal[m], rt = top_rates[m];
-        const int u = m % HB;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            const int vl = lane + 64 * k;
-            T sm[EPT], w[EPT], d[EPT];
-            unpack<T, EPT>(sums[m & 1][vl], sm);
-            unpack<T, EPT>(wcur[k], w);
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) {
-                S::op(w[j], sm[j], g, static_cast<double>(g), &d[j]);
-                const A t = X::tmp(d[j], rt, 0.0);
-                top[k][j] = have_top ? X::add(top[k][j], t) : t;
-            }
-            held[u * kBlock + vl] = pack<T, EPT>(w);
-            if (dp) st_v(dp + vl * EPT, pack<T, EPT>(d));
-        }
-        have_top = true;
-        if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {
-#pragma unroll 1
-            for (int uu = 0; uu <= u; ++uu)
-#pragma unroll
-                for (int k = 0; k < NV; ++k) st_v(mid_ptr(m - u + uu, k), held[uu * kBlock + lane + 64 * k]);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const int64_t e = cbase + (lane + 64 * k) * EPT;
-        T o[EPT];
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) o[j] = X::st(top[k][j]);
-        if (sg.top_agg_out) st_v(reinterpret_cast<T*>(sg.top_agg_out) + e, pack<T, EPT>(o));
-        if (flags & FLAME_HIER_TOP_APPLY) {
-            T* gp = reinterpret_cast<T*>(sg.top_w) + e;
-            T gw[EPT];
-            unpack<T, EPT>(ld_v(gp), gw);
-#pragma unroll
-            for (int j = 0; j < EPT; ++j) S::op(gw[j], o[j], top_goal, static_cast<double>(top_goal), nullptr);
-            st_v(gp, pack<T, EPT>(gw));
-        }
-    }
-}
-
-template <int HB> constexpr int hier_ws_lds_bytes() { return (2 + HB) * kBlock * static_cast<int>(sizeof(V16)); }
-
-// Lift a WS instantiation's dynamic-LDS ceiling to what it uses (above the 64 KiB default);
-// false (and a flame_last_error message) if the runtime refuses.
-bool ws_lds_ok(const void* f) {
-    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, hier_ws_lds_bytes<kHBL>());
-    if (e != hipSuccess) {
-        set_err(FLAME_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s", hipGetErrorString(e));
-        return false;
-    }
-    return true;
-}
-
-template <int DT, int CU, int HB>
-__global__ __launch_bounds__(kBlock + 64) void hier_ws_kernel(const flame_hier_segment* __restrict__ segs, int n_segs,
-                                                              int n_mids, int n_clients,
-                                                              const uint64_t* __restrict__ mid_w,
-                                                              const uint64_t* __restrict__ mid_delta,
-                                                              const uint64_t* __restrict__ clients,
-                                                              const float* __restrict__ mid_rates,
-                                                              const float* __restrict__ mid_goal,
-                                                              const float* __restrict__ top_rates, float top_goal,
-                                                              unsigned flags) {
-    hier_ws_body<DT, CU, HB>(segs, n_segs, n_mids, n_clients, mid_w, mid_delta, clients, mid_rates, mid_goal,
-                             top_rates, top_goal, flags);
-}
-
 // ---------------------------------------------------------------- FedDyn server round
 // One pass over a FedDyn aggregation round (optimizer/feddyn.py:90-113,125-139), driven
 // by a host-built step program.  Per element, in step order (every op rounded in dtype):
@@ -2046,10 +1871,6 @@ int flame_hier_fedbuff(int dtype, unsigned flags, const flame_hier_segment* segs
 #define FLAME_HIER_LAUNCH(DT, CUV, CUL, LOLDS)                                                                  \
     if (lds) {                                                                                                 \
         if (sync) FLAME_HIER_GO(DT, CUL, true, kHBL, true, 0);                                                 \
-        else if (kHierWS && ws_lds_ok(reinterpret_cast<const void*>(hier_ws_kernel<DT, CUL, kHBL>)))             \
-            hipLaunchKernelGGL((hier_ws_kernel<DT, CUL, kHBL>), grid, dim3(kBlock + 64),                       \
-                               hier_ws_lds_bytes<kHBL>(), st, segs, n_segs,                                    \
-                               n_mids, n_clients, w, d, cl, mid_rates, mid_goal, top_rates, top_goal, flags);  \
         else FLAME_HIER_GO(DT, CUL, false, kHBL, true, 0);                                                     \
         br = BR_HIER_LDS + DT * 2 + sync;                                                                      \
     } else if (lo) {                                                                                           \
@@ -2143,12 +1964,8 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
     const void* f = nullptr;
     // the instantiation flame_hier_fedbuff picks for these arguments (the one-middle low-residency
     // launch aside, which depends on the launch size)
-    int block = kBlock;
 #define FLAME_HIER_PICK(DT, CUV, CUL)                                                                          \
-    if (lds && !sync && kHierWS) {                                                                             \
-        f = reinterpret_cast<const void*>(hier_ws_kernel<DT, CUL, kHBL>);                                      \
-        block = kBlock + 64;                                                                                   \
-    } else if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)   \
+    if (lds) f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, true, kHBL, true>)          \
                       : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUL, false, kHBL, true>);        \
     else f = sync ? reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, true, kHB, false>)              \
                   : reinterpret_cast<const void*>(hier_fedbuff_kernel<DT, CUV, false, kHB, false>);
@@ -2161,8 +1978,7 @@ int flame_hier_resident_per_cu(int dtype, unsigned flags, int32_t n_mids) {
         return -set_err(FLAME_ENOTSUP, "flame_hier_resident_per_cu: dtype %d not supported (f32, bf16, f16)", dtype);
     }
     int blocks = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, block,
-                                                                       block > kBlock ? hier_ws_lds_bytes<kHBL>() : 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, kBlock, 0);
     if (e != hipSuccess) return -set_err(FLAME_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
     return blocks < 1 ? 1 : blocks;
 }

@@ -24,7 +24,7 @@ def test_htime_anchors_apply_to_the_product_source(tmp_path):
     htime = _load(os.path.join(ROOT, "tools", "sweep", "htime.py"), "htime")
     out = htime.generate(str(tmp_path / "stamped.hip"))
     text = open(out).read()
-    assert text.count("FLAME_HT(") >= 10 and "flame_sweep_htime" in text
+    assert text.count("FLAME_HT(") >= 5 and "flame_sweep_htime" in text
     # only stamps were added: the product source minus the inserted lines is unchanged
     prod = open(SRC).read()
     assert len(text) > len(prod)
@@ -32,7 +32,7 @@ def test_htime_anchors_apply_to_the_product_source(tmp_path):
 
 def test_sweep_variants_name_existing_knobs():
     knobs = set(re.findall(r"#ifndef (FLAME_T_\w+)", open(SRC).read()))
-    assert {"FLAME_T_CLIENT_UNROLL", "FLAME_T_HBL", "FLAME_T_HIER_WS", "FLAME_T_OPT_WGC"} <= knobs
+    assert {"FLAME_T_CLIENT_UNROLL", "FLAME_T_HBL", "FLAME_T_OPT_WGC"} <= knobs
     for tool in ("kernel_sweep.py", "hier_sweep.py"):
         src = open(os.path.join(ROOT, "tools", tool)).read()
         used = set(re.findall(r'"(FLAME_T_\w+)"', src))

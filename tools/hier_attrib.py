@@ -39,9 +39,8 @@ def build():
     import htime
     os.makedirs(VDIR, exist_ok=True)
     stamped = htime.generate(os.path.join(VDIR, "fedagg_htime.hip"))
-    ws = ["-DFLAME_T_HIER_WS=1"]
-    for nm, defs, src in (("base", [], B.SRC), ("htime", [], stamped), ("ws", ws, B.SRC), ("htime_ws", ws, stamped)):
-        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, *defs, "-o", os.path.join(VDIR, f"lib_{nm}.so"), src])
+    for nm, src in (("base", B.SRC), ("htime", stamped)):
+        subprocess.check_call([B.hipcc(), *B.HIPCC_FLAGS, "-o", os.path.join(VDIR, f"lib_{nm}.so"), src])
         print("built", nm, flush=True)
 
 
@@ -67,7 +66,6 @@ def main():
     ap.add_argument("--params", type=int, default=125_000_000 // 8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variant", default="", help="'' = base / htime, 'ws' = ws / htime_ws (FLAME_T_HIER_WS)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -98,7 +96,7 @@ def main():
     dm = torch.from_numpy(p.meta).to(dev)
     b = dm.data_ptr()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    plain, stamped = ("ws", "htime_ws") if a.variant == "ws" else ("base", "htime")
+    plain, stamped = "base", "htime"
     libs = {"base": load(plain), "htime": load(stamped)}
     ts = torch.zeros(p.n_chunks * SLOTS, dtype=torch.int64, device=dev)
     assert libs["htime"].flame_sweep_htime(ts.data_ptr(), SLOTS) == 0
@@ -174,23 +172,6 @@ def main():
         "wg_bytes": M * C * T * isz + 2 * M * T * isz + 2 * T * isz,
     }
     res["streaming_GBps_per_wg_while_streaming"] = (M * C * T * isz) / (float(np.median(red_t.sum(1))) * tick_ns)
-    if a.variant == "ws":
-        # the streamers (waves 0-3): each middle's reduction, and the wait at its barrier (the epilogue
-        # wave still busy with the previous middle); the epilogue wave: per middle, its work after the
-        # sums arrive, and its idle wait for them
-        o = 3 + 2 * M + nb
-        s_red = t[:, o:o + 2 * M:2]                 # reduction m done (streamers)
-        s_bar = t[:, o + 1:o + 1 + 2 * M:2]         # past barrier m
-        s_prev = np.concatenate([start[:, None], s_bar[:, :-1]], axis=1)
-        e_got, e_done = t[:, 3:3 + 2 * M:2], t[:, 4:4 + 2 * M:2]
-        res["ws"] = {
-            "streamer_reduction_us": float(np.median(s_red - s_prev)) * tick_ns / 1e3,
-            "streamer_barrier_wait_us": float(np.median(s_bar - s_red)) * tick_ns / 1e3,
-            "streamer_barrier_wait_share": float((s_bar - s_red).sum()) / float((s_bar - start[:, None])[:, -1].sum()),
-            "epilogue_work_us": float(np.median(e_done - e_got)) * tick_ns / 1e3,
-            "epilogue_work_us_p95": float(np.percentile(e_done - e_got, 95)) * tick_ns / 1e3,
-            "epilogue_busy_share": float((e_done - e_got).sum()) / float((end - start).sum()),
-        }
     print(json.dumps(res, indent=1), flush=True)
     if a.out:
         with open(a.out, "w") as f:

@@ -26,11 +26,6 @@ VDIR = os.path.join(ROOT, "build", "diag", "hier")   # travels to the GPU box wi
 # CU), prefetch and pipelining variants are in profiles/r02_hier_*.log, r03z*_hier_sweep.log.
 VARIANTS = {
     "base": {},
-    "ws": {"FLAME_T_HIER_WS": 1},                              # a fifth wave runs the epilogues
-    "ws_hbl14": {"FLAME_T_HIER_WS": 1, "FLAME_T_HBL": 14},     # 64 KiB of LDS per workgroup
-    "ws_hbl12": {"FLAME_T_HIER_WS": 1, "FLAME_T_HBL": 12},
-    "ws_hbl12cu8": {"FLAME_T_HIER_WS": 1, "FLAME_T_HBL": 12, "FLAME_T_HIER_LDS_UNROLL16": 8},
-    "ws_hbl12cu4": {"FLAME_T_HIER_WS": 1, "FLAME_T_HBL": 12, "FLAME_T_HIER_LDS_UNROLL16": 4},
     "hbl12cu4": {"FLAME_T_HBL": 12, "FLAME_T_HIER_LDS_UNROLL16": 4},   # 3 workgroups per CU
 }
 

@@ -10,9 +10,8 @@ Slots per workgroup (the layout tools/hier_attrib.py reads; M middles, NB = ceil
   hier_fedbuff_body (LDS store groups), wave 0 lane 0:
     0 start, 1 end, 2 HW_ID | XCC_ID << 32, 3 + 2m the end of middle m's reduction,
     4 + 2m the end of its epilogue, 3 + 2M + g the end of store burst g
-  hier_ws_body (FLAME_T_HIER_WS=1), the epilogue wave's lane 0 on the same slots (3 + 2m: middle
-    m's sums received, 4 + 2m: its epilogue done), and the streamers' wave 0 lane 0 at
-    3 + 2M + NB + 2m (middle m's reduction done) and 4 + 2M + NB + 2m (past its barrier)
+(Round 5's wave-specialised variant, hier_ws_body, had stamps of its own; it left the product
+source with its measurement)
 
     python tools/sweep/htime.py OUT.hip
 """
@@ -47,7 +46,6 @@ extern "C" int flame_sweep_htime(void* buf, int32_t slots) {
 '''
 
 W0 = "threadIdx.x == 0"
-NB = "((n_mids + HB - 1) / HB)"
 
 # (anchor, replacement) -- the anchor text is kept, the stamp goes before or after it
 EDITS = [
@@ -74,32 +72,6 @@ EDITS = [
      "    hier_tail<DT, SYNC>(",
      "                st_v(gp, pack<T, EPT>(gw));\n            }\n        }\n"
      f"        FLAME_HT({W0}, 1);\n        return;\n    }}\n    hier_tail<DT, SYNC>("),
-    # hier_ws_body: streamers
-    ("            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);\n"
-     "            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1\n",
-     f"            FLAME_HT({W0}, 3 + 2 * n_mids + {NB} + 2 * m);\n"
-     "            sums[m & 1][threadIdx.x] = pack<T, EPT>(w);\n"
-     "            __syncthreads();                // middle m's sums are out; the epilogue has finished m - 1\n"
-     f"            FLAME_HT({W0}, 4 + 2 * n_mids + {NB} + 2 * m);\n"),
-    # hier_ws_body: the epilogue wave
-    ("    const int lane = threadIdx.x - kBlock;\n    int64_t wo[NV];\n",
-     "    const int lane = threadIdx.x - kBlock;\n    FLAME_HT(lane == 0, 0);\n    FLAME_HW(lane == 0);\n"
-     "    int64_t wo[NV];\n"),
-    ("        __syncthreads();                    // middle m's sums are in sums[m & 1]\n",
-     "        __syncthreads();                    // middle m's sums are in sums[m & 1]\n"
-     "        FLAME_HT(lane == 0, 3 + 2 * m);\n"),
-    ("        have_top = true;\n        if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {\n"
-     "#pragma unroll 1\n            for (int uu = 0; uu <= u; ++uu)\n#pragma unroll\n"
-     "                for (int k = 0; k < NV; ++k) st_v(mid_ptr(m - u + uu, k), held[uu * kBlock + lane + 64 * k]);\n"
-     "        }\n",
-     "        have_top = true;\n        FLAME_HT(lane == 0, 4 + 2 * m);\n"
-     "        if ((u == HB - 1 || m == n_mids - 1) && !(flags & FLAME_HIER_MID_READONLY)) {\n"
-     "#pragma unroll 1\n            for (int uu = 0; uu <= u; ++uu)\n#pragma unroll\n"
-     "                for (int k = 0; k < NV; ++k) st_v(mid_ptr(m - u + uu, k), held[uu * kBlock + lane + 64 * k]);\n"
-     "        }\n        if (u == HB - 1 || m == n_mids - 1) FLAME_HT(lane == 0, 3 + 2 * n_mids + m / HB);\n"),
-    ("            st_v(gp, pack<T, EPT>(gw));\n        }\n    }\n}\n\ntemplate <int HB> constexpr int hier_ws_lds_bytes()",
-     "            st_v(gp, pack<T, EPT>(gw));\n        }\n    }\n    FLAME_HT(lane == 0, 1);\n}\n\n"
-     "template <int HB> constexpr int hier_ws_lds_bytes()"),
 ]
 
 
