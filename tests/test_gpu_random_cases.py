@@ -11,6 +11,8 @@ one element off their allocation's alignment).  FedAvg / FedBuff: every element 
 several entries); FedOPT: the first round bitwise, the adaptive rounds within the SURVEY §8(c)
 contract (fedopt.py:102-129).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -21,7 +23,11 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 SORTS = ["fedavg", "fedbuff", "fedadam", "fedyogi", "fedadagrad", "fedavg_eager", "fedopt_eager"]
-N_CASES = 7 * 40
+# A soak run draws more, different cases: FLAME_RANDOM_SCALE multiplies every case count and
+# FLAME_RANDOM_SEED_OFFSET moves every seed range (defaults: the suite's own 391 cases).
+SCALE = max(1, int(os.environ.get("FLAME_RANDOM_SCALE", "1")))
+SEED_OFFSET = int(os.environ.get("FLAME_RANDOM_SEED_OFFSET", "0"))
+N_CASES = 7 * 40 * SCALE
 FLOATS = [torch.float32, torch.bfloat16, torch.float16, torch.float64]
 INTS = [torch.int64, torch.int32]
 
@@ -47,7 +53,7 @@ def _draw_size(rng, dtype):
 
 
 def _draw_case(i):
-    rng = np.random.default_rng(7_000 + i)
+    rng = np.random.default_rng(7_000 + SEED_OFFSET + i)
     sort = SORTS[i % len(SORTS)]
     n_keys = int(rng.integers(1, 5))
     keys = []
@@ -272,12 +278,12 @@ def test_random_cases_cover_every_draw():
 
 
 # ---------------------------------------------------------------- co-located hierarchies
-N_HIER = 60
+N_HIER = 60 * SCALE
 HFLOATS = [torch.float32, torch.bfloat16, torch.float16]
 
 
 def _draw_hier(i):
-    rng = np.random.default_rng(9_000 + i)
+    rng = np.random.default_rng(9_000 + SEED_OFFSET + i)
     mode = "async" if i % 2 == 0 else "sync"
     keys = []
     for k in range(int(rng.integers(1, 4))):
@@ -416,7 +422,7 @@ def test_random_hierarchy_vs_oracle(case, monkeypatch):
 
 
 # ---------------------------------------------------------------- FedDyn / SCAFFOLD
-N_STATEFUL = 30
+N_STATEFUL = 30 * SCALE
 
 
 def _draw_model(rng, g):
@@ -520,7 +526,7 @@ def test_random_stateful_vs_oracle(case):
     order equal to the cache's or not, in-place / ping-pong / ping-pong-rows histories, HBM or
     slab updates; feddyn.py:70-139) and SCAFFOLD (random subsets, k, an int buffer with an fp32
     control variate; scaffold.py:82-150) on drawn models, every output and state bitwise."""
-    rng = np.random.default_rng(11_000 + case)
+    rng = np.random.default_rng(11_000 + SEED_OFFSET + case)
     label = f"stateful case {case}"
     if case % 2 == 0:
         _run_feddyn(rng, label + " feddyn")
@@ -529,7 +535,7 @@ def test_random_stateful_vs_oracle(case):
 
 
 # ---------------------------------------------------------------- 16-bit eager FedOPT, deferred
-N_EAGER16 = 20
+N_EAGER16 = 20 * SCALE
 
 
 @pytest.mark.parametrize("case", range(N_EAGER16))
@@ -540,7 +546,7 @@ def test_random_eager_fedopt_16bit_defer_equals_per_call(case):
     GPU paths to each other exactly)."""
     from copy import deepcopy
     from flame_amd.optimizers import optimizer_provider
-    rng = np.random.default_rng(13_000 + case)
+    rng = np.random.default_rng(13_000 + SEED_OFFSET + case)
     keys = []
     for k in range(int(rng.integers(1, 4))):
         dt = [torch.bfloat16, torch.float16, torch.float32][rng.integers(0, 3)] if k else \
