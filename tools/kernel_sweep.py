@@ -89,8 +89,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--kernel", default="agg", choices=["agg", "fedadam", "fedyogi"],
-                    help="agg: flame_agg_reduce; fedadam/fedyogi: flame_fedopt_reduce_adapt (state present)")
+    ap.add_argument("--kernel", default="agg", choices=["agg", "fedadam", "fedyogi", "fedadagrad"],
+                    help="agg: flame_agg_reduce; fedadam / fedyogi / fedadagrad: flame_fedopt_reduce_adapt (state present)")
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
@@ -171,7 +171,7 @@ def main():
             rc = libs[nm].flame_agg_reduce(code, 0, b, p.n_segs, p.n_chunks, b + p.off_clients, p.n_clients,
                                            b + p.off_r32, b + p.off_r64, stream)
         else:
-            rc = libs[nm].flame_fedopt_reduce_adapt(code, {"fedadam": 0, "fedyogi": 1}[args.kernel], 0, b, p.n_segs,
+            rc = libs[nm].flame_fedopt_reduce_adapt(code, {"fedadam": 0, "fedyogi": 1, "fedadagrad": 2}[args.kernel], 0, b, p.n_segs,
                                                     p.n_chunks, b + p.off_clients, p.n_clients, b + p.off_r32,
                                                     *[float(x) for x in hyper], stream)
         if rc:
