@@ -498,6 +498,8 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P,
+                                                 workload=args.workload)
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), {args.workload} server round",
             "value": n * P * world / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -508,7 +510,8 @@ def bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts):
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "kernel": kname,
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
-                         "algorithmic_bytes_per_step": k_bytes,
+                         "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
+                         "traffic_source": traffic_source,
                          "bytes_per_client_param": k_bytes / (n * P * 4)},
         }), flush=True)
 
@@ -537,7 +540,7 @@ def traffic_lookup(path, **match):
         "traffic_over_algorithmic": hit.get("traffic_over_algorithmic")}
 
 
-_TRAFFIC_DEFAULTS = {"layout": "row", "middle_weights": "own"}
+_TRAFFIC_DEFAULTS = {"layout": "row"}
 
 
 def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
@@ -589,7 +592,8 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
-        traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P)
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P,
+                                                 workload=None if fedopt else args.workload)
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -1413,7 +1417,8 @@ def bench_hier(args, world, rank, dev):
     traffic, traffic_source = None, None
     if rank == 0 and args.hier_mode == "fused":
         traffic, traffic_source = traffic_lookup(args.traffic, kernel=names[0], clients=M * C, params=P,
-                                                 middle_weights=args.hier_middles)
+                                                 workload="hier_fedbuff" if args.hier_middles == "own"
+                                                 else f"hier_fedbuff_{args.hier_middles}")
     if rank == 0:
         per_step_kernel = sum(k["avg_s"] * k["launches"] for k in kst.values()) / args.steps
         sync = args.hier_mode.startswith("sync")
