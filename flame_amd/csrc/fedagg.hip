@@ -68,6 +68,24 @@ constexpr int kLoUnroll16 = FLAME_T_LO_UNROLL16;
 #define FLAME_T_LO_LDS 65536
 #endif
 constexpr int kLoLds = FLAME_T_LO_LDS;
+// Below kLoBurstMaxClients clients the low-residency launch also holds kLoWGC chunks' outputs per
+// workgroup in LDS and stores them in one burst: the short client streams of such rounds pay for
+// every interleaved store.  Tiled slab, one process, bitwise (tools/kernel_sweep.py,
+// profiles/r05s_lo_wgc_*.log, r05t_lo_wgc_*.log): fp32 x 25M, 64 clients 0.964 -> 0.909 ms, 128
+// 1.843 -> 1.797, 256 3.594 -> 3.546, 512 equal, 1,024 +0.8 %; bf16 x 50M, 64 clients 1.028 ->
+// 0.969 ms, 256 3.647 -> 3.621.  (A kernel-argument launch never holds 512 clients' pointers, so
+// its low-residency launches always burst.)
+#ifndef FLAME_T_LO_WGC
+#define FLAME_T_LO_WGC 8
+#endif
+constexpr int kLoWGC = FLAME_T_LO_WGC;
+#ifndef FLAME_T_LO_BURST_MAX_CLIENTS
+#define FLAME_T_LO_BURST_MAX_CLIENTS 512
+#endif
+constexpr int kLoBurstMaxClients = FLAME_T_LO_BURST_MAX_CLIENTS;
+// the dynamic LDS that, beside the kLoWGC chunks' held outputs (4 KiB each), still makes kLoLds per workgroup
+constexpr int kLoHeld = kLoWGC > 1 ? kLoWGC * 4096 : 0;
+constexpr int kLoDynLds = kLoLds > kLoHeld ? kLoLds - kLoHeld : 0;
 #ifndef FLAME_T_LO_MIN_CLIENTS
 #define FLAME_T_LO_MIN_CLIENTS 64
 #endif
@@ -465,27 +483,58 @@ __device__ __forceinline__ int64_t xcd_slot(int64_t b, int64_t n) {
     return x * q + (x < r ? x : r) + b / 8;
 }
 
-// One chunk per workgroup (chunk = workgroup slot: the launch order, or the XCD-contiguous map).
-template <int DT, int CU>
+// G chunks per workgroup (G = 1: chunk = workgroup slot, in launch order or the XCD-contiguous
+// map).  G > 1: the workgroup reduces chunks slot*G .. slot*G+G-1 one after another, holds their
+// full output vectors in LDS and stores them in one burst at the end.
+template <int DT, int CU, int G>
 __device__ __forceinline__ void agg_reduce_body(const flame_segment* __restrict__ segs, int n_segs,
                                                 const uint64_t* __restrict__ clients, int n_clients,
                                                 const float* __restrict__ r32, const double* __restrict__ r64,
                                                 unsigned flags, int64_t n_chunks) {
     using T = typename Tr<DT>::T;
-    const int64_t chunk = (flags & FLAME_AGG_XCD_MAP) ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
-    if (chunk >= n_chunks) return;
-    V16 ov[kVPT];
-    T* op;
-    if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov, op)) store_chunk(op, ov);
+    const int64_t slot = (flags & FLAME_AGG_XCD_MAP) ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x;
+    if constexpr (G == 1) {
+        if (slot >= n_chunks) return;
+        V16 ov[kVPT];
+        T* op;
+        if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, slot, ov, op)) store_chunk(op, ov);
+    } else {
+        static_assert(G <= 32 && G * kVPT * kBlock * sizeof(V16) <= 128 * 1024, "agg_reduce_body: G chunks' outputs exceed the LDS");
+        constexpr int64_t VS = static_cast<int64_t>(kBlock) * Tr<DT>::EPT;
+        __shared__ V16 held[G * kVPT * kBlock];
+        unsigned pending = 0;
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+            const int64_t chunk = slot * G + g;
+            if (chunk >= n_chunks) break;
+            V16 ov[kVPT];
+            T* op;
+            if (reduce_chunk<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, chunk, ov, op)) {
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v) held[(g * kVPT + v) * kBlock + threadIdx.x] = ov[v];
+                pending |= 1u << g;
+            }
+        }
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+            if (!(pending >> g & 1u)) continue;
+            const int64_t chunk = slot * G + g;
+            const flame_segment& sg = segs[find_segment(segs, n_segs, chunk)];
+            T* op = reinterpret_cast<T*>(sg.out) + (chunk - sg.chunk_begin) * chunk_elems<DT>() +
+                    static_cast<int64_t>(threadIdx.x) * Tr<DT>::EPT;
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) st_v(op + v * VS, held[(g * kVPT + v) * kBlock + threadIdx.x]);
+        }
+    }
 }
 
-template <int DT, int CU>
+template <int DT, int CU, int G>
 __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                             const uint64_t* __restrict__ clients, int n_clients,
                                                             const float* __restrict__ r32,
                                                             const double* __restrict__ r64, unsigned flags,
                                                             int64_t n_chunks) {
-    agg_reduce_body<DT, CU>(segs, n_segs, clients, n_clients, r32, r64, flags, n_chunks);
+    agg_reduce_body<DT, CU, G>(segs, n_segs, clients, n_clients, r32, r64, flags, n_chunks);
 }
 
 // Small launches (few segments x few hundred clients): the whole metadata block travels as a
@@ -496,7 +545,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel(const flame_segment*
 constexpr int kArgMetaWords = 448;          // 3,584 B: kernel arguments are limited to 4 KiB
 struct ArgMeta { uint64_t w[kArgMetaWords]; };
 
-template <int DT, int CU>
+template <int DT, int CU, int G>
 __global__ __launch_bounds__(kBlock) void agg_reduce_kernel_argmeta(const ArgMeta meta, int n_segs, int n_clients,
                                                                     int off_clients, int off_r32, int off_r64,
                                                                     unsigned flags, int64_t n_chunks) {
@@ -504,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel_argmeta(const ArgMet
     // loads) -- naming the by-value parameter would copy 3.5 KB into every lane's scratch
     (void)sizeof(meta);
     const uint64_t* w = (const uint64_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    agg_reduce_body<DT, CU>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
+    agg_reduce_body<DT, CU, G>(reinterpret_cast<const flame_segment*>(w), n_segs, w + off_clients, n_clients,
                             off_r32 >= 0 ? reinterpret_cast<const float*>(w + off_r32) : nullptr,
                             off_r64 >= 0 ? reinterpret_cast<const double*>(w + off_r64) : nullptr, flags, n_chunks);
 }
@@ -1497,12 +1546,13 @@ enum : int {
     BR_HIER_LO = 52,      // + dt: one middle over a long launch, low residency (FedBuff only)
     BR_HIER_ARG = 55,     // + dt * 2 + sync: flame_hier_fedbuff_argmeta
     BR_DYN = 61,          // + dt (f32, bf16, f16, f64): flame_feddyn_round
-    BR_AGG_ARG_LO = 65,   // + dt (f32, bf16, f16): flame_agg_reduce_argmeta, 2 workgroups per CU
+    BR_AGG_ARG_LO = 65,   // + dt (f32, bf16, f16): flame_agg_reduce_argmeta, 2 workgroups per CU, output bursts
     BR_HIER_ARG_LO = 68,  // + dt: flame_hier_fedbuff_argmeta, one middle over a long launch
     BR_OPT_ARG_MULTI = 71,  // + variant: flame_fedopt_reduce_adapt_argmeta, fp32, kOptWGC chunks per workgroup
     BR_HIER_ARG_LDS = 74,   // + dt * 2 + sync: flame_hier_fedbuff_argmeta, LDS store groups
     BR_CHAIN = 80,          // + dt * 3 + variant (f32, bf16, f16): flame_fedopt_chain
-    BR_COUNT = 89
+    BR_AGG_LOB = 89,        // + dt (f32, bf16, f16): flame_agg_reduce, low residency, LDS-held output bursts
+    BR_COUNT = 92
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -1526,11 +1576,12 @@ const char* branch_name(int i) {
             else if (b < BR_HIER_ARG) snprintf(n, z, "flame_hier_fedbuff/lo/%s/fedbuff", dts[b - BR_HIER_LO]);
             else if (b < BR_DYN) snprintf(n, z, "flame_hier_fedbuff_argmeta/%s/%s", dts[(b - BR_HIER_ARG) / 2], (b - BR_HIER_ARG) % 2 ? "sync" : "fedbuff");
             else if (b < BR_AGG_ARG_LO) snprintf(n, z, "flame_feddyn_round/%s", dts[b - BR_DYN]);
-            else if (b < BR_HIER_ARG_LO) snprintf(n, z, "flame_agg_reduce_argmeta/lo/%s", dts[b - BR_AGG_ARG_LO]);
+            else if (b < BR_HIER_ARG_LO) snprintf(n, z, "flame_agg_reduce_argmeta/lo_burst/%s", dts[b - BR_AGG_ARG_LO]);
             else if (b < BR_OPT_ARG_MULTI) snprintf(n, z, "flame_hier_fedbuff_argmeta/lo/%s/fedbuff", dts[b - BR_HIER_ARG_LO]);
             else if (b < BR_HIER_ARG_LDS) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
             else if (b < BR_CHAIN) snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
-            else snprintf(n, z, "flame_fedopt_chain/%s/%s", dts[(b - BR_CHAIN) / 3], var[(b - BR_CHAIN) % 3]);
+            else if (b < BR_AGG_LOB) snprintf(n, z, "flame_fedopt_chain/%s/%s", dts[(b - BR_CHAIN) / 3], var[(b - BR_CHAIN) % 3]);
+            else snprintf(n, z, "flame_agg_reduce/lo_burst/%s", dts[b - BR_AGG_LOB]);
         }
         return true;
     }();
@@ -1596,28 +1647,37 @@ int flame_agg_reduce(int dtype, unsigned flags, const flame_segment* segs, int32
     if (dtype == FLAME_F64 ? (n_clients > 0 && !rates64) : (n_clients > 0 && !rates32))
         return set_err(FLAME_EINVAL, "rate array is NULL");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
+    const dim3 block(kBlock);
     auto cl = reinterpret_cast<const uint64_t*>(clients);
-#define FLAME_AGG_LAUNCH(DT, CUV, LDS, BR)                                                                      \
-    hipLaunchKernelGGL((agg_reduce_kernel<DT, CUV>), grid, block, LDS, st, segs, n_segs, cl, n_clients, rates32, \
-                       rates64, flags, n_chunks);                                                              \
+#define FLAME_AGG_LAUNCH(DT, CUV, G, LDS, BR)                                                                   \
+    hipLaunchKernelGGL((agg_reduce_kernel<DT, CUV, G>), dim3(static_cast<unsigned>((n_chunks + G - 1) / G)),    \
+                       block, LDS, st, segs, n_segs, cl, n_clients, rates32, rates64, flags, n_chunks);         \
     return launched(BR, "flame_agg_reduce");
-    // long-lived workgroups over many chunks: two per CU, fewer loads in flight per lane
+    // long-lived workgroups over many chunks: two per CU, fewer loads in flight per lane; below
+    // kLoBurstMaxClients clients with their outputs held in LDS and stored in bursts
     if (n_clients >= kLoMinClients && n_chunks >= kLoMinChunks) {
+        if (n_clients < kLoBurstMaxClients) {
+            switch (dtype) {
+            case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kLoUnroll, kLoWGC, kLoDynLds, BR_AGG_LOB + FLAME_F32)
+            case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kLoUnroll16, kLoWGC, kLoDynLds, BR_AGG_LOB + FLAME_BF16)
+            case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kLoUnroll16, kLoWGC, kLoDynLds, BR_AGG_LOB + FLAME_F16)
+            default: break;      // f64 / integers: the general launch below
+            }
+        }
         switch (dtype) {
-        case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kLoUnroll, kLoLds, BR_AGG_LO + FLAME_F32)
-        case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kLoUnroll16, kLoLds, BR_AGG_LO + FLAME_BF16)
-        case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kLoUnroll16, kLoLds, BR_AGG_LO + FLAME_F16)
+        case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kLoUnroll, 1, kLoLds, BR_AGG_LO + FLAME_F32)
+        case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kLoUnroll16, 1, kLoLds, BR_AGG_LO + FLAME_BF16)
+        case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kLoUnroll16, 1, kLoLds, BR_AGG_LO + FLAME_F16)
         default: break;      // f64 / integers: the general launch below
         }
     }
     switch (dtype) {
-    case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kClientUnroll, 0, BR_AGG + FLAME_F32)
-    case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kClientUnroll16, 0, BR_AGG + FLAME_BF16)
-    case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kClientUnroll16, 0, BR_AGG + FLAME_F16)
-    case FLAME_F64: FLAME_AGG_LAUNCH(FLAME_F64, kClientUnroll, 0, BR_AGG + FLAME_F64)
-    case FLAME_I64: FLAME_AGG_LAUNCH(FLAME_I64, 4, 0, BR_AGG + FLAME_I64)
-    case FLAME_I32: FLAME_AGG_LAUNCH(FLAME_I32, 4, 0, BR_AGG + FLAME_I32)
+    case FLAME_F32: FLAME_AGG_LAUNCH(FLAME_F32, kClientUnroll, 1, 0, BR_AGG + FLAME_F32)
+    case FLAME_BF16: FLAME_AGG_LAUNCH(FLAME_BF16, kClientUnroll16, 1, 0, BR_AGG + FLAME_BF16)
+    case FLAME_F16: FLAME_AGG_LAUNCH(FLAME_F16, kClientUnroll16, 1, 0, BR_AGG + FLAME_F16)
+    case FLAME_F64: FLAME_AGG_LAUNCH(FLAME_F64, kClientUnroll, 1, 0, BR_AGG + FLAME_F64)
+    case FLAME_I64: FLAME_AGG_LAUNCH(FLAME_I64, 4, 1, 0, BR_AGG + FLAME_I64)
+    case FLAME_I32: FLAME_AGG_LAUNCH(FLAME_I32, 4, 1, 0, BR_AGG + FLAME_I32)
     default:
         return set_err(FLAME_ENOTSUP, "flame_agg_reduce: unsupported dtype %d", dtype);
     }
@@ -1652,18 +1712,20 @@ int flame_agg_reduce_argmeta(int dtype, unsigned flags, const void* host_meta, i
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<unsigned>(n_chunks)), block(kBlock);
 #define FLAME_ARGMETA_LAUNCH(DT, CUV) \
-    hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV>), grid, block, 0, st, m, n_segs, n_clients, \
+    hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV, 1>), grid, block, 0, st, m, n_segs, n_clients, \
                        oc, o32, o64, flags, n_chunks)
     // a long launch with few segments (its table fits the kernel arguments): the same low-residency
     // instantiation as flame_agg_reduce's
     if (n_clients >= kLoMinClients && n_chunks >= kLoMinChunks &&
         (dtype == FLAME_F32 || dtype == FLAME_BF16 || dtype == FLAME_F16)) {
-#define FLAME_ARGMETA_LO(DT, CUV)                                                                              \
-        hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV>), grid, block, kLoLds, st, m, n_segs, n_clients, \
-                           oc, o32, o64, flags, n_chunks)
-        if (dtype == FLAME_F32) FLAME_ARGMETA_LO(FLAME_F32, kLoUnroll);
-        else if (dtype == FLAME_BF16) FLAME_ARGMETA_LO(FLAME_BF16, kLoUnroll16);
-        else FLAME_ARGMETA_LO(FLAME_F16, kLoUnroll16);
+#define FLAME_ARGMETA_LO(DT, CUV, G, LDS)                                                                      \
+        hipLaunchKernelGGL((agg_reduce_kernel_argmeta<DT, CUV, G>), dim3(static_cast<unsigned>((n_chunks + G - 1) / G)), \
+                           block, LDS, st, m, n_segs, n_clients, oc, o32, o64, flags, n_chunks)
+        static_assert((kArgMetaWords - 10) < kLoBurstMaxClients,
+                      "a kernel-argument launch can hold kLoBurstMaxClients clients: it needs the plain instantiation too");
+        if (dtype == FLAME_F32) FLAME_ARGMETA_LO(FLAME_F32, kLoUnroll, kLoWGC, kLoDynLds);
+        else if (dtype == FLAME_BF16) FLAME_ARGMETA_LO(FLAME_BF16, kLoUnroll16, kLoWGC, kLoDynLds);
+        else FLAME_ARGMETA_LO(FLAME_F16, kLoUnroll16, kLoWGC, kLoDynLds);
 #undef FLAME_ARGMETA_LO
         return launched(BR_AGG_ARG_LO + dtype, "flame_agg_reduce_argmeta");
     }

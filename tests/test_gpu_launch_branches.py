@@ -186,7 +186,7 @@ def test_fedbuff_existing_aggregate_long_round_vs_oracle(dt):
                           version=RND)
     torch.cuda.synchronize()
     hits = _diff(before, _counts())
-    assert hits == {f"flame_agg_reduce_argmeta/lo/{dt}": 1}, hits
+    assert hits == {f"flame_agg_reduce_argmeta/lo_burst/{dt}": 1}, hits
     w = {k: v.clone() for k, v in base.items()}
     before = _counts()
     _, delta = opt.scale_add_agg_weights_with_delta(w, agg, n)

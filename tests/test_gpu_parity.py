@@ -201,18 +201,27 @@ def test_reduce_vs_oracle_dtypes(dtype, numel):
     S.assert_bitwise(f"{dtype}/{numel}", out, {"x": exp})
 
 
+# (clients, extra small keys, the launch branch the round takes): the low-residency instantiation
+# with LDS-held output bursts below 512 clients and without at 512, through the kernel-argument
+# metadata (a few keys) and through the device table (more segments x clients than 3.5 KB holds)
+LO_CASES = [(64, 0, "flame_agg_reduce_argmeta/lo_burst"), (64, 7, "flame_agg_reduce/lo_burst"),
+            (512, 1, "flame_agg_reduce/lo")]
+
+
 @pytest.mark.oracle
+@pytest.mark.parametrize("case", LO_CASES, ids=[f"n{n}_k{k}" for n, k, _ in LO_CASES])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-def test_low_residency_reduction_vs_oracle(dtype):
-    """flame_agg_reduce's 2-workgroups-per-CU instantiation (FLAME_LO_CU / FLAME_LO_CU16: launches of
-    >= 64 clients over >= 4,096 chunks) on every element against the oracle: 64 clients
-    as separate tensors (the row layout, so the XCD chunk map is on too) over 4,096 chunks + a ragged
-    4,099-element key, every float dtype the path instantiates."""
-    from flame_amd import engine
+def test_low_residency_reduction_vs_oracle(dtype, case):
+    """flame_agg_reduce's 2-workgroups-per-CU instantiations (launches of >= 64 clients over >= 4,096
+    chunks; below 512 clients with kLoWGC chunks' outputs held in LDS and stored in bursts; DESIGN.md
+    §4) on every element against the oracle: clients as separate tensors (the row layout, so the
+    XCD chunk map is on too) over one 4,096-chunk key + small ragged keys, every float dtype the
+    path instantiates, and the branch each launch took."""
+    from flame_amd import _native, engine
     O = _oracle()
-    n = 64
+    n, extra, branch = case
     chunk = engine.chunk_elems(engine.dtype_code(dtype))
-    shapes = [("w", 4096 * chunk), ("t", 4_099)]
+    shapes = [("w", 4096 * chunk)] + [(f"t{j}", 4_099 + 13 * j) for j in range(extra)]
     g = torch.Generator().manual_seed(11)
     counts = torch.randint(1, 1000, (n,), generator=g).tolist()
     total = sum(counts)
@@ -224,8 +233,14 @@ def test_low_residency_reduction_vs_oracle(dtype):
     cache = S.SortedCache()
     for i in range(n):
         cache[f"{i:04d}"] = S.TR(cl[i], counts[i])
+    dt = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}[dtype]
+    before = _native.launch_branch_counts()
     out = make_amd("fedavg").do({k: v.clone() for k, v in base.items()}, cache, total=total)
-    S.assert_bitwise(f"low-residency {dtype}", out, exp)
+    torch.cuda.synchronize()
+    after = _native.launch_branch_counts()
+    hit = {k for k, v in after.items() if v > before.get(k, 0)}
+    assert f"{branch}/{dt}" in hit, hit
+    S.assert_bitwise(f"low-residency {dtype} n{n}", out, exp)
 
 
 @pytest.mark.oracle

@@ -49,6 +49,12 @@ VARIANTS = {
     "chain_cu12_occ3": {"FLAME_T_CHAIN_UNROLL": 12, "FLAME_T_CHAIN_LDS": 53248},
     "chain_cu32": {"FLAME_T_CHAIN_UNROLL": 32},
     "chain_cu24_occ3": {"FLAME_T_CHAIN_UNROLL": 24, "FLAME_T_CHAIN_LDS": 53248},
+    # the low-residency reduction's LDS-held output bursts (kLoWGC chunks per workgroup, below
+    # kLoBurstMaxClients clients): none, and 8 / 16 / 32 chunks at every client count
+    "lo_wgc1": {"FLAME_T_LO_WGC": 1},
+    "lo_wgc8_all": {"FLAME_T_LO_WGC": 8, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
+    "lo_wgc16_all": {"FLAME_T_LO_WGC": 16, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
+    "lo_wgc32_all": {"FLAME_T_LO_WGC": 32, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
 }
 
 
