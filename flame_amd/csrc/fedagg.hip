@@ -907,8 +907,9 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
     // faster: 1.294 vs 1.287 ms at 8 loads per batch, 1.457 at 12, 3.40 at 16 (two 64-register
     // batches); one process, bitwise, profiles/r05k_chain_pipe_ab.log.  Nor do two or four
     // chunks per lane -- twice / four times the independent step chains: 1.38-1.44 vs 1.378 ms,
-    // profiles/r05o_chain_ev_ab.log.  Three resident workgroups of the plain batch loop already
-    // overlap one another's loads and arithmetic.)
+    // profiles/r05o_chain_ev_ab.log -- nor 2 / 3 / 4 chunks per workgroup with their outputs burst
+    // from LDS: 1.386 / 1.417 / 1.372 vs 1.370 ms, profiles/r05w_chain_wgc_ab.log.  Three resident
+    // workgroups of the plain batch loop already overlap one another's loads and arithmetic.)
     for (; i + CU <= n_clients; i += CU) {
         T x[CU][EPT];
         float rr[CU];
