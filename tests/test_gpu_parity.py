@@ -4,6 +4,7 @@ Bitwise for FedAvg / FedBuff in every dtype; FedOPT within the SURVEY §8(c)
 tolerance (elementwise rel <= 1e-6 where |ref| >= 1e-6*max|ref|, rel-L2 <= 1e-6),
 and bitwise wherever only FedAvg arithmetic has happened.
 """
+import concurrent.futures
 import math
 
 import numpy as np
@@ -228,8 +229,15 @@ def test_low_residency_reduction_vs_oracle(dtype, case):
     base = {k: _synth_dev(12, 0 + j, s, 1.0, dtype) for j, (k, s) in enumerate(shapes)}
     cl = [{k: _synth_dev(12, 10 + 2 * i + j, s, 1e-2, dtype) for j, (k, s) in enumerate(shapes)} for i in range(n)]
     exp = {k: v.cpu() for k, v in base.items()}
+    rates = [c / total for c in counts]
     for k in exp:
-        O.reduce_tensor(exp[k], [c[k].cpu() for c in cl], [c / total for c in counts])
+        # the oracle is element-wise: disjoint element ranges reduce in parallel threads (the C
+        # call releases the GIL), each in client order
+        host = [c[k].cpu() for c in cl]
+        parts = [(a, min(a + (1 << 20), exp[k].numel())) for a in range(0, exp[k].numel(), 1 << 20)]
+        with concurrent.futures.ThreadPoolExecutor(8) as ex:
+            list(ex.map(lambda ab: O.reduce_tensor(exp[k][ab[0]:ab[1]], [h[ab[0]:ab[1]] for h in host], rates),
+                        parts))
     cache = S.SortedCache()
     for i in range(n):
         cache[f"{i:04d}"] = S.TR(cl[i], counts[i])
