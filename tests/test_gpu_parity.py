@@ -205,22 +205,24 @@ def test_reduce_vs_oracle_dtypes(dtype, numel):
 # (clients, extra small keys, the launch branch the round takes): the low-residency instantiation
 # with LDS-held output bursts below 512 clients and without at 512, through the kernel-argument
 # metadata (a few keys) and through the device table (more segments x clients than 3.5 KB holds)
-LO_CASES = [(64, 0, "flame_agg_reduce_argmeta/lo_burst"), (64, 7, "flame_agg_reduce/lo_burst"),
-            (512, 1, "flame_agg_reduce/lo")]
+LO_CASES = [(64, 0, "flame_agg_reduce_argmeta/lo_burst", "tensors"), (64, 7, "flame_agg_reduce/lo_burst", "tensors"),
+            (64, 7, "flame_agg_reduce/lo_burst", "slab"), (512, 1, "flame_agg_reduce/lo", "tensors")]
 
 
 @pytest.mark.oracle
-@pytest.mark.parametrize("case", LO_CASES, ids=[f"n{n}_k{k}" for n, k, _ in LO_CASES])
+@pytest.mark.parametrize("case", LO_CASES, ids=[f"n{n}_k{k}_{pl}" for n, k, _, pl in LO_CASES])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_low_residency_reduction_vs_oracle(dtype, case):
     """flame_agg_reduce's 2-workgroups-per-CU instantiations (launches of >= 64 clients over >= 4,096
     chunks; below 512 clients with kLoWGC chunks' outputs held in LDS and stored in bursts; DESIGN.md
     §4) on every element against the oracle: clients as separate tensors (the row layout, so the
-    XCD chunk map is on too) over one 4,096-chunk key + small ragged keys, every float dtype the
-    path instantiates, and the branch each launch took."""
+    XCD chunk map is on too) or slots of a tiled UpdateSlab (the client tile stride), over one
+    4,096-chunk key + small ragged keys (a burst's 8 chunks then straddle keys and tails), every
+    float dtype the path instantiates, and the branch each launch took."""
     from flame_amd import _native, engine
+    from flame_amd.slab import UpdateSlab
     O = _oracle()
-    n, extra, branch = case
+    n, extra, branch, placement = case
     chunk = engine.chunk_elems(engine.dtype_code(dtype))
     shapes = [("w", 4096 * chunk)] + [(f"t{j}", 4_099 + 13 * j) for j in range(extra)]
     g = torch.Generator().manual_seed(11)
@@ -238,6 +240,9 @@ def test_low_residency_reduction_vs_oracle(dtype, case):
         with concurrent.futures.ThreadPoolExecutor(8) as ex:
             list(ex.map(lambda ab: O.reduce_tensor(exp[k][ab[0]:ab[1]], [h[ab[0]:ab[1]] for h in host], rates),
                         parts))
+    if placement == "slab":
+        slab = UpdateSlab({k: torch.empty(sz, dtype=dtype) for k, sz in shapes}, capacity=n, device=DEV)
+        cl = [slab.put(c) for c in cl]
     cache = S.SortedCache()
     for i in range(n):
         cache[f"{i:04d}"] = S.TR(cl[i], counts[i])
