@@ -51,6 +51,12 @@ VARIANTS = {
     "chain_cu24_occ3": {"FLAME_T_CHAIN_UNROLL": 24, "FLAME_T_CHAIN_LDS": 53248},
     # the low-residency reduction's LDS-held output bursts (kLoWGC chunks per workgroup, below
     # kLoBurstMaxClients clients): none, and 8 / 16 / 32 chunks at every client count
+    # config 2 (256 clients x 1M fp32, 977 chunks): below the low-residency launch's 4,096 chunks
+    "c2_lo": {"FLAME_T_LO_MIN_CHUNKS": 512, "FLAME_T_LO_WGC": 1},
+    "c2_lo_occ3": {"FLAME_T_LO_MIN_CHUNKS": 512, "FLAME_T_LO_WGC": 1, "FLAME_T_LO_LDS": 53248},
+    "c2_lo_occ4": {"FLAME_T_LO_MIN_CHUNKS": 512, "FLAME_T_LO_WGC": 1, "FLAME_T_LO_LDS": 40960},
+    "c2_cu4": {"FLAME_T_CLIENT_UNROLL": 4},
+    "c2_cu16": {"FLAME_T_CLIENT_UNROLL": 16},
     "lo_wgc1": {"FLAME_T_LO_WGC": 1},
     "lo_wgc8_all": {"FLAME_T_LO_WGC": 8, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
     "lo_wgc16_all": {"FLAME_T_LO_WGC": 16, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
