@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--arrivals", type=int, default=64)
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     a = ap.parse_args()
     from flame_amd import _native, engine, synth
     from flame_amd.optimizers import optimizer_provider
@@ -43,8 +44,9 @@ def main():
         libs[nm] = _native.lib()
     dev = torch.device("cuda", 0)
     K, P = a.arrivals, a.params
-    slab = UpdateSlab({"model": torch.empty(P)}, capacity=K, device=dev)
-    tmp = torch.empty(P, device=dev)
+    tdt = torch.float32 if a.dtype == "f32" else torch.bfloat16
+    slab = UpdateSlab({"model": torch.empty(P, dtype=tdt)}, capacity=K, device=dev)
+    tmp = torch.empty(P, dtype=tdt, device=dev)
     arrivals = []
     for i in range(K):
         engine.synth_fill_(tmp, 21, 1 + i, 0, 1e-2)
@@ -85,9 +87,9 @@ def main():
                 times[nm].append(sum(e0.elapsed_time(e1) for n_, e0, e1, _ in ev if n_ == "flame_fedopt_chain"))
         for nm in names[1:]:
             for x, y in zip(outs[nm], outs[names[0]]):
-                assert torch.equal(x.view(torch.int32), y.view(torch.int32)), f"round {r}: {nm} differs"
+                assert torch.equal(x.view(torch.int16), y.view(torch.int16)), f"round {r}: {nm} differs"
         print(f"round {r} done", flush=True)
-    gb = (K + 8) * P * 4 / 1e9
+    gb = (K + 8) * P * tmp.element_size() / 1e9
     for nm in names:
         med = statistics.median(times[nm])
         print(f"{nm:40s} chain median {med:.4f} ms  {gb / med * 1e3:.0f} GB/s  ({', '.join(f'{t:.3f}' for t in times[nm])})",
