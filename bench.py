@@ -108,9 +108,10 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="host-resident updates (end-to-end)")
     ap.add_argument("--e2e-mode", default="zerocopy",
                     choices=["zerocopy", "copy", "pageable", "wire", "wire_pinned", "wire_reference", "eager",
-                             "shm", "shm_reference", "shard"],
+                             "shm", "shm_reference", "shard", "shm_shard"],
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
-                         "stream overlapped with the reduction; pageable: reference weights_to_model_device")
+                         "stream overlapped with the reduction; pageable: reference weights_to_model_device; "
+                         "shm at N > 1 (or shm_shard at any N): the sharded shm ingest + gathers + egress encode")
     ap.add_argument("--e2e-placement", default="slab", choices=["slab", "hbm"],
                     help="eager mode: DeviceUpdateCache placement of the arriving updates")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
@@ -349,6 +350,9 @@ def timed(world, steps, warmup, step):
     barrier(world)
     torch.cuda.synchronize()
     engine.kernel_events = []
+    from flame_amd import shard
+    if shard.GATHER_TIMING is not None:      # the N>1 lines time the timed steps' gathers only
+        shard.GATHER_TIMING.clear()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -593,7 +597,7 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
         traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P,
-                                                 workload=None if fedopt else args.workload)
+                                                 workload=args.workload)   # that variant's entry or None
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
@@ -689,6 +693,11 @@ def main():
     P = args.params or 25_000_000
     # ---- synthetic inputs (counter generator; rank-specific streams)
     if args.e2e:
+        if args.e2e_mode == "shm_shard" or (world > 1 and args.e2e_mode == "shm"):
+            return bench_e2e_shm_sharded(args, world, rank, dev, n, P)
+        if world > 1:
+            raise SystemExit(f"--e2e at {world} GPUs: --e2e-mode shm (the sharded shm ingest); "
+                             f"{args.e2e_mode} is a one-GPU mode")
         return bench_e2e(args, n, P, dev)
     if (world > 1 or args.force_shard) and args.workload in ("fedavg", "fedadam", "fedyogi", "fedadagrad"):
         return bench_sharded(args, world, rank, dev, n, P)
@@ -1040,9 +1049,13 @@ def bench_sharded(args, world, rank, dev, n, P):
 
     if not fedavg:
         step()            # FedOPT round 1 is a passthrough (fedopt.py:87-88); time adaptive rounds only
+    shard.GATHER_TIMING = []
     elapsed, events = timed(world, args.steps, args.warmup, step)
+    gt, shard.GATHER_TIMING = shard.GATHER_TIMING, None
     name = "flame_agg_reduce" if fedavg else "flame_fedopt_reduce_adapt"
     ks = kernel_stats(events, name)
+    attrib = time_attribution(world, ks["avg_s"] * ks["launches"] / args.steps * 1e3 if ks else None,
+                              elapsed / args.steps * 1e3, gt)
     # untimed self-check: every rank holds the same full model, sampled elements == the host
     idx = sample_indices(plan, "model", seed=args.seed)
     if fedavg:
@@ -1057,6 +1070,12 @@ def bench_sharded(args, world, rank, dev, n, P):
         lps = ks["launches"] / args.steps
         k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
         achieved = k_bytes / k_time / 1e9
+        # the per-rank shape's PMC bytes (n clients x P params, one launch): a lookup, labelled
+        traffic, traffic_source = traffic_lookup(args.traffic, kernel=name, clients=n, params=P, layout="slab",
+                                                 workload=args.workload)
+        if traffic_source is not None:
+            traffic_source["note"] = (f"measured on the unsharded per-rank shape (one launch); this line runs "
+                                      f"{lps:g} launches per step over {plan.owned_elements()} owned params")
         print(json.dumps({
             "metric": METRIC if fedavg else f"aggregated params/sec (device-resident), {n}-client {args.workload} "
                                             f"(adaptive round)",
@@ -1071,8 +1090,10 @@ def bench_sharded(args, world, rank, dev, n, P):
                        "clients": n, "params_per_gpu": P, "global_params": G,
                        "parallelism": f"param-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": name,
-                         "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes, "launches_per_step": lps},
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_source,
+                         "kernel": name, "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
+                         "launches_per_step": lps},
+            "time_attribution": attrib,
             "collective": _collective_note(plan, world, 4),
             "process_group": process_group_info(),
             "launcher": launcher(world),
@@ -1177,8 +1198,12 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
         rounds[0] += 1
         body()
 
+    shard.GATHER_TIMING = []
     elapsed, events = timed(world, args.steps, args.warmup, step)
+    gt, shard.GATHER_TIMING = shard.GATHER_TIMING, None
     ks = kernel_stats(events, "flame_hier_fedbuff")
+    attrib = time_attribution(world, ks["avg_s"] * ks["launches"] / args.steps * 1e3 if ks else None,
+                              elapsed / args.steps * 1e3, gt)
     idx = sample_indices(plan, "model", seed=args.seed)
     gc = verify_sharded(gw, idx, host_hier_rounds(args.seed + 4, M, C, idx, rounds[0], rnd, fetched,
                                                   args.hier_mode == "sync"))
@@ -1187,6 +1212,12 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
         lps = ks["launches"] / args.steps
         k_time, k_bytes = ks["avg_s"] * lps, ks["bytes_per_launch"] * lps
         sync = args.hier_mode == "sync"
+        traffic, traffic_source = (traffic_lookup(args.traffic, kernel="flame_hier_fedbuff", clients=M * C, params=P,
+                                                  layout="slab", workload="hier_fedbuff" if not fetched
+                                                  else "hier_fedbuff_fetched") if not sync else (None, None))
+        if traffic_source is not None:
+            traffic_source["note"] = (f"measured on the unsharded per-rank shape (one launch); this line runs "
+                                      f"{lps:g} launches per step over {plan.owned_elements()} owned params")
         print(json.dumps({
             "metric": "aggregated params/sec (device-resident), hierarchical "
                       + ("FedAvg (synchronous)" if sync else "FedBuff") + ", parameter-sharded",
@@ -1202,9 +1233,11 @@ def bench_hier_sharded(args, world, rank, dev, M, C, P):
                        "middle_layout": args.hier_mid_layout, "arrivals": args.hier_arrivals,
                        "params_per_gpu": P, "global_params": G, "parallelism": f"param-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                         "frac": k_bytes / k_time / 1e9 / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "kernel": "flame_hier_fedbuff", "kernel_ms": k_time * 1e3, "algorithmic_bytes": k_bytes,
                          "launches_per_step": lps},
+            "time_attribution": attrib,
             "collective": _collective_note(plan, world, 2),
             "process_group": process_group_info(),
             "launcher": launcher(world),
@@ -1447,6 +1480,294 @@ def bench_hier(args, world, rank, dev):
         }), flush=True)
 
 
+def pcie_probe(dev, world, nbytes=256 << 20, reps=5):
+    """Same-process pinned host <-> HBM copy rates, every rank at once (after a barrier): the
+    PCIe ceiling each rank's link gives this process (the e2e line's roofline peak).  Ranks that
+    share a GPU (the gloo rehearsal) share its link, so their aggregate is one link's."""
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    host.fill_(1)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+
+    def rate(fn):
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 1e3)
+        return nbytes / statistics.median(ts) / 1e9
+    barrier(world)
+    h2d = rate(lambda: d.copy_(host, non_blocking=True))
+    barrier(world)
+    d2h = rate(lambda: host.copy_(d, non_blocking=True))
+    mine = [h2d, d2h]
+    allr = gather_objects(world, mine)
+    del host, d
+    return {"h2d_GBps_by_rank": [round(a[0], 2) for a in allr], "d2h_GBps_by_rank": [round(a[1], 2) for a in allr],
+            "h2d_aggregate_GBps": round(sum(a[0] for a in allr), 2),
+            "probe": f"{nbytes >> 20} MiB pinned host <-> HBM copy per rank, all ranks at once, median of {reps}"}
+
+
+def gather_objects(world, obj):
+    """[obj of rank 0, ..., obj of rank world-1] (just [obj] without a process group)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def e2e_reference_sample(seg_names, sizes, counts, total, G, dev, budget_s=10.0, max_clients=8):
+    """The reference's receive path over the same shm segments, on a bounded sample of clients
+    (rank 0, untimed by the step clock): backend/shm.py:386-391 copies the message out of the
+    segment, channel.py:321-325 runs cloudpickle.loads on the copy; then
+    * cpu: FedAvg's op sequence on the host (fedavg.py:84-104, oracle/torch_cpu.py) -- the
+      line's cpu_baseline;
+    * gpu (shm_reference): weights_to_model_device (common/util.py:198-208) + the same torch
+      ops on the device."""
+    import cloudpickle
+    from multiprocessing import shared_memory
+    from oracle import torch_cpu
+    res = {}
+    cores, env = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        for where in ("cpu", "gpu"):
+            agg = {"model": torch.zeros(G, dtype=torch.float32, device="cpu" if where == "cpu" else dev)}
+            t_all, k = 0.0, 0
+            for i, (nm, sz) in enumerate(zip(seg_names, sizes)):
+                t0 = time.perf_counter()
+                seg = shared_memory.SharedMemory(nm)
+                try:
+                    data = bytes(seg.buf[:sz])
+                finally:
+                    seg.close()
+                msg = cloudpickle.loads(data)
+                del data
+                if where == "cpu":
+                    torch_cpu.fedavg_round(agg, [msg["weights"]], [int(msg["dataset_size"])], total)
+                else:
+                    w = {kk: v.to(dev) for kk, v in msg["weights"].items()}
+                    rate = float(np.float32(int(msg["dataset_size"]) / total))
+                    agg["model"] += (w["model"] * rate).to(w["model"].dtype)
+                    torch.cuda.synchronize()
+                t_all += time.perf_counter() - t0
+                k += 1
+                del msg
+                if k >= max_clients or t_all >= budget_s:
+                    break
+            res[where] = {"clients": k, "s": round(t_all, 3), "value": k * G / t_all,
+                          "host_read_GBps": k * G * 4 / t_all / 1e9}
+    finally:
+        torch.set_num_threads(prev)
+    res["host"] = env
+    return res
+
+
+def bench_e2e_shm_sharded(args, world, rank, dev, n, P):
+    """End to end at N GPUs: updates sit in per-sender POSIX shared-memory
+    segments, as the LIFL SHM backend delivers them (backend/shm.py:393-403); every rank opens
+    and hipHostRegisters the same segments once (flame_amd.ingest.ShmReceiver), decodes each
+    message in place and DMAs only ITS ranges of the update into its rank-local slab
+    (DeviceUpdateCache(shard=plan), its own PCIe link); ShardedOptimizer(FedAvg).do reduces the
+    owned ranges wave by wave with the in-place all-gathers behind each wave, so every rank ends
+    with the whole model (syncfl/top_aggregator.py:161-176); rank 0 then encodes the model
+    message into a pinned egress buffer (flame_amd.egress.MessageEncoder: one D2H straight into
+    the payload, syncfl/top_aggregator.py:184-215).  The step runs from "payloads in shared
+    memory" to "model message in host memory".  Weak scaling: the model has P x world params."""
+    import cloudpickle
+    from multiprocessing import shared_memory
+    from flame_amd import engine, ingest, shard, synth
+    from flame_amd.egress import MessageEncoder
+    from flame_amd.ingest import DeviceUpdateCache
+    from flame_amd.optimizers import optimizer_provider
+    n = min(n, 64)
+    G = P * world
+    counts = synth.counts(args.seed, n)
+    total = int(counts.sum())
+    sopt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=dev, fracs=_fracs(args, shard))
+    sopt.set_layout({"model": torch.empty(G, dtype=torch.float32, device="meta")})
+    plan = sopt.plan
+    tag = f"flamee2e{os.environ.get('MASTER_PORT', os.getpid())}"
+    names = [f"{tag}_t{i}-agg" for i in range(n)]
+    # the senders: rank r writes the messages of trainers r, r + world, ... (cloudpickle of
+    # {weights, dataset_size}, channel.py:203-218), each into its own segment
+    mine, my_sizes = [], {}
+    tmp = torch.empty(G, dtype=torch.float32, device=dev)
+    try:
+        for i in range(rank, n, world):
+            engine.synth_fill_(tmp, args.seed, 1 + i, 0, 1e-2)
+            b = cloudpickle.dumps({"weights": {"model": tmp.cpu()}, "dataset_size": int(counts[i])})
+            seg = shared_memory.SharedMemory(name=names[i], create=True, size=len(b))
+            seg.buf[:len(b)] = b
+            mine.append(seg)
+            my_sizes[i] = len(b)
+            del b
+        del tmp
+        sizes = {}
+        for d in gather_objects(world, my_sizes):
+            sizes.update(d)
+        sizes = [sizes[i] for i in range(n)]
+        barrier(world)
+        _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, plan, tag, names, sizes)
+    finally:
+        barrier(world)
+        for seg in mine:
+            seg.close()
+            seg.unlink()
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, plan, tag, names, sizes):
+    from flame_amd import engine, ingest, shard
+    from flame_amd.egress import MessageEncoder
+    from flame_amd.ingest import DeviceUpdateCache
+    rx = ingest.ShmReceiver("agg", register=True, untrack=True)
+    scache = DeviceUpdateCache(device=dev, placement="slab", capacity=n, shard=plan)
+    model = torch.empty(G, dtype=torch.float32, device=dev)
+    engine.synth_fill_(model, args.seed, 0, 0, 1.0)
+    weights = {"model": model}
+    enc = MessageEncoder(ring=1) if rank == 0 else None
+    keys = [f"{i:05d}" for i in range(n)]
+    phases, out = [], {}
+    rounds = [0]
+
+    def step():
+        rounds[0] += 1
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t0 = time.perf_counter()
+        e[0].record()
+        for i in range(n):          # the receive loop: decode in place, this rank's ranges -> its slab
+            msg = rx.loads(f"{tag}_t{i}", sizes[i])
+            scache[keys[i]] = TR(msg["weights"], msg["dataset_size"])
+            del msg
+        t1 = time.perf_counter()
+        e[1].record()
+        sopt.do(weights, scache, total=total, num_trainers=n)
+        e[2].record()
+        if enc is not None:         # the message every trainer gets (one encode, one D2H into it)
+            out["payload"] = enc.encode({"weights": weights, "round": rounds[0]})
+        e[3].record()
+        phases.append((t1 - t0, e))
+
+    global SETTLE
+    if SETTLE is None:       # PCIe-bound: no HBM settle (its 8 GB probe buffer per rank buys nothing here)
+        SETTLE = {"skipped": "end-to-end line: PCIe-bound, see roofline.probe"}
+    try:
+        shard.GATHER_TIMING = None
+        for _ in range(args.warmup):
+            step()
+        phases.clear()
+        shard.GATHER_TIMING = []
+        elapsed, events = timed(world, args.steps, 0, step)
+        gt, shard.GATHER_TIMING = shard.GATHER_TIMING, None
+        torch.cuda.synchronize()
+        ph = {"ingest_host_ms": statistics.mean(p[0] for p in phases) * 1e3,
+              "ingest_ms": statistics.mean(p[1][0].elapsed_time(p[1][1]) for p in phases),
+              "reduce_gather_ms": statistics.mean(p[1][1].elapsed_time(p[1][2]) for p in phases),
+              "egress_ms": statistics.mean(p[1][2].elapsed_time(p[1][3]) for p in phases)}
+        ks = kernel_stats(events, "flame_agg_reduce")
+        k_ms = ks["avg_s"] * ks["launches"] / args.steps * 1e3 if ks else None
+        attrib = time_attribution(world, k_ms, elapsed / args.steps * 1e3, gt)
+        per_rank = gather_objects(world, ph)
+        # untimed self-checks: every rank holds the same model == the host restatement on sampled
+        # elements, and rank 0's egress payload decodes (the trainers' cloudpickle.loads) to it
+        idx = sample_indices(plan, "model", seed=args.seed)
+        gc = verify_sharded(model, idx, host_fedavg_rounds(args.seed, counts, idx, rounds[0]))
+        gc["rounds_checked"] = rounds[0]
+        probe = pcie_probe(dev, world)
+        ref = None
+        if rank == 0:
+            import cloudpickle
+            msg = cloudpickle.loads(bytes(out["payload"]))
+            gc["egress_payload_bitwise"] = bool(torch.equal(msg["weights"]["model"].view(torch.int32),
+                                                           model.cpu().view(torch.int32)))
+            gc["egress_payload_bytes"] = len(out["payload"])
+            if args.cpu_clients > 0:
+                ref = e2e_reference_sample(names, sizes, counts, total, G, dev)
+        if rank == 0:
+            ms = elapsed / args.steps * 1e3
+            h2d = n * G * 4          # every update's bytes cross PCIe once (each rank its ranges)
+            d2h = G * 4              # the model, once, into the egress payload
+            achieved = (h2d + d2h) / (ms / 1e3) / 1e9
+            peak = probe["h2d_aggregate_GBps"]
+            line = {
+                "metric": "aggregated params/sec, END-TO-END (LIFL shm payloads -> model message in host memory)",
+                "mode": "shm (sharded ingest)", "value": n * G / (ms / 1e3), "unit": "client-params/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+                "higher_is_better": True, "scaling": "weak", "dtype": "f32", "settle": SETTLE,
+                "data": "synthetic (counter-based generator) cloudpickled into POSIX shm segments, one per trainer",
+                "config": {"workload": f"e2e shm: {n} trainers x {G} fp32 params ({P} per GPU), parameter-sharded "
+                                       f"ingest over {world} rank(s), in-place all-gathers, rank-0 egress encode",
+                           "clients": n, "params_per_gpu": P, "global_params": G,
+                           "parallelism": f"param-shard{world}"},
+                "host_read_GBps": h2d / (ms / 1e3) / 1e9,
+                "roofline": {"bound": "pcie", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                             "frac": achieved / peak if peak else None,
+                             "bytes_per_step": {"h2d": h2d, "d2h": d2h},
+                             "per_link_achieved_GBps": h2d / world / (ms / 1e3) / 1e9,
+                             "per_link_peak_GBps": probe["h2d_GBps_by_rank"], **{"probe": probe}},
+                "phases_ms_by_rank": per_rank,
+                "time_attribution": attrib,
+                "collective": _collective_note(plan, world, 4),
+                "process_group": process_group_info(), "launcher": launcher(world),
+                "gather_check": gc,
+                "shm_reference": None if ref is None else {
+                    **ref["gpu"], "unit": "client-params/s",
+                    "path": "bytes(segment[:size]) (backend/shm.py:386-391) + cloudpickle.loads (channel.py:321-325) "
+                            "+ .to(device) (common/util.py:198-208) + the reference's torch ops on the device, per "
+                            "trainer, rank 0 only, bounded sample"},
+                "cpu_baseline": None if ref is None else {
+                    "value": ref["cpu"]["value"], "unit": "client-params/s", "cores": ref["host"]["threads_used"],
+                    "kind": "port", "host": ref["host"],
+                    "sample": f"{ref['cpu']['clients']} trainers of the same segments: shm copy + cloudpickle.loads + "
+                              f"FedAvg's op sequence on the host (oracle/torch_cpu.py), {ref['cpu']['s']} s"},
+            }
+            print(json.dumps(line), flush=True)
+    finally:
+        shard.GATHER_TIMING = None
+        rx.close()
+    _checked(gc)
+    if rank == 0 and not gc.get("egress_payload_bitwise", True):
+        raise SystemExit("bench.py: the egress payload does not decode to the model")
+
+
+def time_attribution(world, k_ms, ms_per_step, gather_timing):
+    """Where an N>1 step's time went, from every rank: its kernel ms per step,
+    the step time not covered by the slowest rank's kernels (exposed collective + host time), and
+    per wave the in-place all-gather's span on the launch stream (shard.GATHER_TIMING: from the
+    wave's issue behind its kernels to its work.wait(); exact for the last wave, an upper bound
+    for the ones hidden behind later waves) with the bytes this rank received."""
+    waves = collections.defaultdict(list)
+    for w, recv, t0, t1 in gather_timing or []:
+        dt = t0.elapsed_time(t1) if hasattr(t0, "elapsed_time") else (t1 - t0) * 1e3
+        waves[w].append((dt, recv))
+    mine = {"kernel_ms": k_ms,
+            "waves": {int(w): {"span_ms": statistics.mean(d for d, _ in v), "bytes": v[0][1], "calls": len(v)}
+                      for w, v in sorted(waves.items())}}
+    allr = gather_objects(world, mine)
+    ks = [a["kernel_ms"] for a in allr if a["kernel_ms"] is not None]
+    out = {"kernel_ms_by_rank": [a["kernel_ms"] for a in allr],
+           "kernel_ms_max": max(ks) if ks else None, "kernel_ms_min": min(ks) if ks else None,
+           "exposed_collective_ms": (ms_per_step - max(ks)) if ks else None, "allgather": []}
+    for w in sorted({w for a in allr for w in a["waves"]}):
+        spans = [a["waves"][w]["span_ms"] if w in a["waves"] else None for a in allr]
+        nbytes = allr[0]["waves"].get(w, {}).get("bytes", 0)
+        sp = [s for s in spans if s is not None]
+        out["allgather"].append({"wave": w, "bytes_received_per_rank": nbytes, "span_ms_by_rank": spans,
+                                 "GBps": nbytes / (max(sp) / 1e3) / 1e9 if sp and max(sp) > 0 else None})
+    if out["allgather"]:
+        last = out["allgather"][-1]
+        out["last_wave_exposed_gather_ms"] = max(s for s in last["span_ms_by_rank"] if s is not None)
+    return out
+
+
 def bench_e2e(args, n, P, dev):
     """Host-resident updates -> FedAvg on the GPU -> global model back in host memory.
 
@@ -1616,12 +1937,22 @@ def bench_e2e(args, n, P, dev):
                 seg.close()
                 seg.unlink()
     ks = kernel_stats(events, "flame_agg_reduce")
+    probe = pcie_probe(dev, 1)
+    ms = elapsed / args.steps * 1e3
+    # bytes over PCIe per step: every update in (the wire modes: their payloads' tensors), the base
+    # model in and the aggregated model out (out_h)
+    h2d, d2h = (n + 1) * P * 4, P * 4
+    achieved = (h2d + d2h) / (ms / 1e3) / 1e9
     print(json.dumps({
         "metric": "aggregated params/sec, END-TO-END (host-resident updates -> global model in host memory)",
-        "mode": mode, "value": n * P / (elapsed / args.steps), "unit": "client-params/s",
-        "ms_per_step": elapsed / args.steps * 1e3, "clients": n, "params": P, "settle": SETTLE,
-        "host_read_GBps": n * P * 4 / (elapsed / args.steps) / 1e9,
+        "mode": mode, "value": n * P / (ms / 1e3), "unit": "client-params/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "clients": n, "params": P, "settle": SETTLE,
+        "host_read_GBps": n * P * 4 / (ms / 1e3) / 1e9,
         "kernel_ms_per_step": ks["avg_s"] * ks["launches"] / args.steps * 1e3,
+        "roofline": {"bound": "pcie", "achieved": achieved, "peak": probe["h2d_aggregate_GBps"], "unit": "GB/s",
+                     "frac": achieved / probe["h2d_aggregate_GBps"], "bytes_per_step": {"h2d": h2d, "d2h": d2h},
+                     "probe": probe},
+        "launcher": launcher(1),
     }), flush=True)
 
 

@@ -20,7 +20,7 @@ HDR = os.path.join(ROOT, "include", "flame_amd.h")
 DEPS = (SRC, HDR, os.path.join(PKG, "csrc", "fastmath.h"))
 LIB = os.path.join(PKG, "libflame_amd.so")
 # Sweep builds (tools/kernel_sweep.py, hier_sweep.py) compile SRC itself with -DFLAME_T_* overrides
-# of its tunables into build/diag; diagnostic stamps are inserted into a copy by
+# of its tunables into build/ab; diagnostic stamps are inserted into a copy by
 # tools/sweep/htime.py.  Neither ever writes LIB.
 ARCH = os.environ.get("FLAME_AMD_ARCH", "gfx950")
 # host side: the restricted pickle VM of flame_amd.ingest (a CPython extension, plain gcc)

@@ -36,6 +36,14 @@
 #include "../../include/flame_amd.h"
 #include "fastmath.h"
 
+// One IEEE rounding per reference op, denormals kept (fastmath.h's div_rn proof and every bitwise
+// test rest on it).  -ffast-math / -ffinite-math-only are refused here; the denormal mode of the
+// built kernels (-fgpu-flush-denormals-to-zero sets no macro) is checked on the code object by
+// tests/test_denorm_mode.py.
+#if defined(__FAST_MATH__) || (defined(__FINITE_MATH_ONLY__) && __FINITE_MATH_ONLY__)
+#error "fedagg.hip must not be built with -ffast-math / -ffinite-math-only"
+#endif
+
 namespace {
 
 // Tunables, each chosen by an interleaved A/B sweep on MI355X.  The product build
@@ -169,6 +177,19 @@ constexpr int kChainUnroll16 = FLAME_T_CHAIN_UNROLL16;
 #define FLAME_T_CHAIN_LDS 53248
 #endif
 constexpr int kChainLds = FLAME_T_CHAIN_LDS;           // dynamic LDS per fp32 workgroup (a residency cap)
+// bf16 FedOPT step (adapt_vec) and eager-chain arrivals: two elements per packed fp32 instruction,
+// one instruction per bf16 rounding, v_sqrt_f32 / v_rcp_f32 where the bf16 rounding absorbs their
+// ulp; 0 = the generic per-element path (same bits, for A/B builds)
+#ifndef FLAME_T_BF16_PACKED
+#define FLAME_T_BF16_PACKED 1
+#endif
+constexpr bool kBf16Packed = FLAME_T_BF16_PACKED != 0;
+// FedYogi's (1 - beta_2) d^2 * sign(v - d^2): sign as one ordered compare + bit-select (1) or as
+// torch writes it, two compares and an integer difference (0); same bits
+#ifndef FLAME_T_YOGI_SIGN
+#define FLAME_T_YOGI_SIGN 1
+#endif
+constexpr bool kYogiSelect = FLAME_T_YOGI_SIGN != 0;
 constexpr int kEwBlock = 256;  // elementwise kernels (scale-add, synth)
 
 thread_local char g_err[512] = "";
@@ -199,6 +220,20 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
 __device__ __forceinline__ uint16_t f32_to_bf16_exact(float x) {  // x already bf16-representable
     return static_cast<uint16_t>(__float_as_uint(x) >> 16);
 }
+// The same rounding with the result left where fp32 wants it (bits = bf16 << 16): ONE
+// v_cvt_pk_bf16_f32 whose low half converts +0, instead of the convert into the low half and the
+// shift up that bf16_round compiles to -- the same instruction, so the same bits (NaNs included).
+// Never applied to a transcendental's result: gfx950 needs a wait state before a VALU reads a
+// v_sqrt / v_rcp / v_rsq result, and the compiler does not insert it ahead of inline asm (those
+// roundings use bf16_round).
+__device__ __forceinline__ float bf16_rnd1(float x) {
+    float r;
+    asm("v_cvt_pk_bf16_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+using f2 = __attribute__((ext_vector_type(2))) float;    // v_pk_{mul,add,fma}_f32 operands
+__device__ __forceinline__ f2 bf16_rnd2(f2 x) { return f2{bf16_rnd1(x.x), bf16_rnd1(x.y)}; }
+__device__ __forceinline__ f2 splat2(float x) { return f2{x, x}; }
 // The empty asm pins x as an fp32 VGPR value: without it the backend folds
 // fptrunc(fmul(a, r)) into v_fma_mixlo_f16, which rounds the exact product to
 // fp16 ONCE, while torch rounds the fp32 product to fp16 (two roundings; they
@@ -560,7 +595,13 @@ __global__ __launch_bounds__(kBlock) void agg_reduce_kernel_argmeta(const ArgMet
 
 // ---------------------------------------------------------------- fused FedOPT (fp32)
 __device__ __forceinline__ float sign_f(float x) {  // torch.sign: NaN -> 0, -0 -> 0
-    return static_cast<float>((0.0f < x) - (x < 0.0f));
+    if constexpr (kYogiSelect) {
+        // +-1 with x's sign where x is ordered and nonzero (one v_cmp_lg_f32 + one v_bfi_b32),
+        // else +0: the same value as the integer difference below, in 3 instructions instead of 6
+        return __builtin_islessgreater(x, 0.0f) ? __builtin_copysignf(1.0f, x) : 0.0f;
+    } else {
+        return static_cast<float>((0.0f < x) - (x < 0.0f));
+    }
 }
 
 // Per-dtype rounding after each reference op (identity for fp32; RNE to bf16 / fp16).
@@ -612,10 +653,77 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
 // square root and the divide take flame_fm::sqrt_rn / div_rn (rsq / rcp seeds, packed fma), else
 // the general sequences.  Both give the same m, v and current (tools/fp_probe.py), so which one a
 // lane takes never shows in the results.
+// bf16 (a lane's 8 elements as 4 pairs): adapt_vec's op sequence with every fp32 op on a pair
+// (v_pk_mul_f32 / v_pk_add_f32) and every bf16 rounding one instruction (bf16_rnd1).  Admitted
+// lanes take v_sqrt_f32 and num * v_rcp_f32(den) for the correctly rounded root and quotient: both
+// are within 2 fp32 ulps of the exact value, and the exact root of a bf16 v, and the exact quotient
+// of two bf16 values, are never within 2^-18 (relative) of a bf16 rounding midpoint (8-bit
+// significands), so the bf16 rounding of either equals the bf16 rounding of the correctly rounded
+// fp32 value (v_sqrt_f32 flushes a subnormal v to a zero root, but den = RN(RN(root) + tau) = tau
+// for both roots there).  tools/fp_probe.py checks the root on every normal bf16 v, den on every
+// admitted v and the quotient on every admitted (num, den) pair.
+template <int VARIANT>
+__device__ __forceinline__ void adapt_vec_bf16(const float (&avg)[8], const float (&cur)[8], bool cur_is_avg,
+                                               float (&m)[8], float (&v)[8], float (&cur_out)[8], float b1,
+                                               float omb1, float b2, float omb2, float eta, float tau) {
+    float c[8], num[8];
+#pragma unroll
+    for (int p = 0; p < 8; p += 2) {
+        const f2 a = {avg[p], avg[p + 1]};
+        const f2 cc = cur_is_avg ? a : f2{cur[p], cur[p + 1]};
+        const f2 d = bf16_rnd2(a - cc);
+        const f2 mn = bf16_rnd2(bf16_rnd2(splat2(b1) * f2{m[p], m[p + 1]}) + bf16_rnd2(splat2(omb1) * d));
+        const f2 d2 = bf16_rnd2(d * d);
+        const f2 vo = {v[p], v[p + 1]};
+        f2 vn;
+        if constexpr (VARIANT == FLAME_FEDADAM) {
+            vn = bf16_rnd2(bf16_rnd2(splat2(b2) * vo) + bf16_rnd2(splat2(omb2) * d2));
+        } else if constexpr (VARIANT == FLAME_FEDYOGI) {
+            const f2 t = bf16_rnd2(splat2(omb2) * d2);
+            const f2 x = bf16_rnd2(vo - d2);
+            vn = bf16_rnd2(vo - bf16_rnd2(t * f2{sign_f(x.x), sign_f(x.y)}));
+        } else {
+            vn = bf16_rnd2(vo + d2);
+        }
+        const f2 nm = bf16_rnd2(splat2(eta) * mn);
+        c[p] = cc.x;
+        c[p + 1] = cc.y;
+        m[p] = mn.x;
+        m[p + 1] = mn.y;
+        v[p] = vn.x;
+        v[p + 1] = vn.y;
+        num[p] = nm.x;
+        num[p + 1] = nm.y;
+    }
+    const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & flame_fm::admits<8>(v, num);
+    if (ok) {
+#pragma unroll
+        for (int p = 0; p < 8; p += 2) {
+            // the roots' rounding through bf16_round: a v_sqrt_f32 result never feeds inline asm
+            const f2 s = {bf16_round(__builtin_amdgcn_sqrtf(v[p])), bf16_round(__builtin_amdgcn_sqrtf(v[p + 1]))};
+            const f2 den = bf16_rnd2(s + splat2(tau));
+            const f2 q = bf16_rnd2(f2{num[p], num[p + 1]} * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)});
+            const f2 co = bf16_rnd2(f2{c[p], c[p + 1]} + q);
+            cur_out[p] = co.x;
+            cur_out[p + 1] = co.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float den = bf16_round(__fadd_rn(bf16_round(__builtin_sqrtf(v[j])), tau));
+            cur_out[j] = bf16_round(__fadd_rn(c[j], bf16_round(__fdiv_rn(num[j], den))));
+        }
+    }
+}
+
 template <int DT, int VARIANT, int EPT>
 __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (&cur)[EPT], bool cur_is_avg,
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
                                           float omb1, float b2, float omb2, float eta, float tau) {
+    if constexpr (DT == FLAME_BF16 && EPT == 8 && kBf16Packed) {
+        adapt_vec_bf16<VARIANT>(avg, cur, cur_is_avg, m, v, cur_out, b1, omb1, b2, omb2, eta, tau);
+        return;
+    }
     float c[EPT], num[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -878,8 +986,18 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
         load_t(reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[i]) + coff), x, true);
     };
     auto arrive = [&](const T (&x)[EPT], float r, bool ends) {
+        if constexpr (DT == FLAME_BF16 && kBf16Packed) {   // X::add(b, X::tmp(x, r)) on pairs
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
+            for (int j = 0; j < EPT; j += 2) {
+                const f2 t = bf16_rnd2(f2{bf16_to_f32(x[j]), bf16_to_f32(x[j + 1])} * splat2(r));
+                const f2 s = bf16_rnd2(f2{b[j], b[j + 1]} + t);
+                b[j] = s.x;
+                b[j + 1] = s.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) b[j] = X::add(b[j], X::tmp(x[j], r, 0.0));
+        }
         if (ends) {     // uniform: one do() call ends here
             if (__builtin_expect(aliased, 0)) {   // the first step after the passthrough: current IS base
 #pragma unroll

@@ -541,6 +541,12 @@ def fedopt_chain_(variant: str, base: List[torch.Tensor], cur: List[Optional[tor
     for code, idx in groups.items():
         if code not in (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16):
             raise NotImplementedError(f"fedopt_chain_: dtype {base[idx[0]].dtype}")
+    # every dtype group is planned and its tables uploaded BEFORE the first launch: a failure
+    # there (a bad tensor, an allocation) leaves base / m / v untouched.  Only a
+    # launch itself failing after another group's launch ran can leave the groups out of step;
+    # that exception carries flame_partial = True (FedOPT then refuses further calls).
+    launches = []
+    for code, idx in groups.items():
         segs, keep = [], []
         p_alias = 0
         for s_ in idx:
@@ -564,13 +570,20 @@ def fedopt_chain_(variant: str, base: List[torch.Tensor], cur: List[Optional[tor
         pad = np.zeros(-(-ends_host.size // 8) * 8, dtype=np.uint8)
         pad[:ends_host.size] = ends_host
         dm = _staging.upload(np.concatenate([p.meta, pad.view(np.int64)]), device)
-        segp, clp, r32p, _ = _device_ptrs(dm, p)
-        with _timed("flame_fedopt_chain", device, nbytes):
-            N.check(L.flame_fedopt_chain(code, FEDOPT_VARIANT[variant], N.FLAME_OPT_STATE_ZERO if state_zero else 0,
-                                         segp, p.n_segs, p.n_chunks, clp, p.n_clients, r32p,
-                                         dm.data_ptr() + p.meta.nbytes, *[float(x) for x in h],
-                                         _stream_ptr(device)))
         keep.append(dm)
+        launches.append((code, p, dm, h, nbytes, keep))
+    for i, (code, p, dm, h, nbytes, keep) in enumerate(launches):
+        segp, clp, r32p, _ = _device_ptrs(dm, p)
+        try:
+            with _timed("flame_fedopt_chain", device, nbytes):
+                N.check(L.flame_fedopt_chain(code, FEDOPT_VARIANT[variant],
+                                             N.FLAME_OPT_STATE_ZERO if state_zero else 0, segp, p.n_segs, p.n_chunks,
+                                             clp, p.n_clients, r32p, dm.data_ptr() + p.meta.nbytes,
+                                             *[float(x) for x in h], _stream_ptr(device)))
+        except Exception as e:
+            if i:
+                e.flame_partial = True
+            raise
         _keepalive(keep, device)
 
 

@@ -77,6 +77,7 @@ class FedOPT(FedAvg):
     max_chain_bytes = 16 << 30
 
     def __init__(self, beta_1, beta_2, eta, tau, defer: bool = False):
+        self._poisoned = None
         self._chain = None
         self._current = None
         self._m = None
@@ -148,12 +149,15 @@ class FedOPT(FedAvg):
 
     def do(self, base_weights, cache, *, total: int = 0, version: int = 0, **kwargs):
         logger.debug("calling fedopt (flame_amd)")
+        self._check_poisoned()
         if self.chain_defer and not kwargs.keys() & _SHARD_KWARGS:
             ch = self._chain
             if ch is not None and ch.base is base_weights and (len(cache) == 0 or total == 0):
                 # an arrival with nothing to aggregate: the reference's FedAvg.do returns None
                 # and do() hands back current_weights unchanged (fedopt.py:80-85) -- here the
-                # queued chain's last result, without cutting the chain
+                # queued chain's last result, without cutting the chain; agg_weights reads None
+                # once the queue has run, as the reference's self.agg_weights = None (:80-83)
+                ch.last_empty = True
                 return ch.result(self, len(ch.steps) - 1, list(base_weights.keys()))
             popped = self._try_queue(base_weights, cache, total)
             if isinstance(popped, DeferredCurrent):
@@ -314,6 +318,7 @@ class FedOPT(FedAvg):
                 return popped
             ch = self._chain = _Chain(base_weights, cur, aliased, self._m is None)
         step = [(tres.weights, tres.count / total) for _, tres in popped]
+        ch.last_empty = False
         ch.steps.append(step)
         ch.n_entries += len(step)
         ch.nbytes += len(step) * sum(base_weights[k].numel() * 4 for k in keys)
@@ -326,6 +331,7 @@ class FedOPT(FedAvg):
         ch = self.__dict__.get("_chain")
         if ch is None:
             return
+        self._check_poisoned()
         self._chain = None
         last = len(ch.steps) - 1
         cuts = sorted({i for i, refs in enumerate(ch.results) if any(r() is not None for r in refs)} | {last})
@@ -362,7 +368,13 @@ class FedOPT(FedAvg):
                     if r is not None:
                         r._value = new
                 cur, aliased, zero, start = new, {k: False for k in keys}, False, cut + 1
+            if ch.last_empty:        # the last queued call had nothing to aggregate (fedopt.py:80-85)
+                self._agg = None
         except BaseException as e:
+            if getattr(e, "flame_partial", False):
+                # one dtype group's launch ran, a later one's failed: base / m / v of the first
+                # group moved on, the others did not -- no later call may reuse that state
+                self._poisoned = e
             for refs in ch.results[start:]:
                 for ref in refs:
                     r = ref()
@@ -373,6 +385,13 @@ class FedOPT(FedAvg):
             # the queued updates (slab slots among them) are released now, not when the last
             # DeferredCurrent dies (the role keeps that one as its weights)
             ch.steps, ch.current, ch.base = [], None, None
+
+    def _check_poisoned(self):
+        e = self.__dict__.get("_poisoned")
+        if e is not None:
+            raise RuntimeError("flame_amd FedOPT: a queued round's launch failed after part of the model's dtype "
+                               "groups had been updated, so m_t / v_t / current_weights no longer agree; "
+                               f"re-create the optimizer ({type(e).__name__}: {e})") from e
 
     def _adapt_generic(self, keys, average, current, state_zero):
         """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""
@@ -427,6 +446,7 @@ class _Chain:
         self.results = []               # per do(): weakrefs to the DeferredCurrents handed out for it
         self.n_entries = 0
         self.nbytes = 0
+        self.last_empty = False         # the last do() call queued had nothing to aggregate
 
     def result(self, owner, step, keys):
         res = DeferredCurrent(owner, self, step, keys)

@@ -230,6 +230,32 @@ def _slice(t: torch.Tensor, lo: int, hi: int, numel: int) -> torch.Tensor:
 COALESCE = os.environ.get("FLAME_AMD_COALESCE", "1") != "0"
 # collectives issued per path ("coalesced" groups, "async" single gathers, "host_staged"), for tests
 GATHER_STATS = collections.Counter()
+# None, or a list that every call's in-place gathers are timed into (bench.py's N > 1 lines):
+# (wave, bytes this rank received, start, end) with start marked on the launch stream right before
+# the wave's collective is issued (behind the wave's kernels) and end right after its work.wait()
+# -- CUDA events for device tensors, host perf_counter seconds for CPU tensors.  A wave's span is
+# its gather's time plus whatever later kernels the launch stream ran before the wait: exact for
+# the last wave, an upper bound for the hidden ones.
+GATHER_TIMING = None
+
+
+def _mark_like(start):
+    """A mark of the same kind as ``start`` (a CUDA event on the current stream, or a host time)."""
+    if isinstance(start, float):
+        import time
+        return time.perf_counter()
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def _mark(t: torch.Tensor):
+    if t.is_cuda:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(t.device))
+        return ev
+    import time
+    return time.perf_counter()
 
 
 def _coalescing_manager():
@@ -253,6 +279,7 @@ class _Comm:
         self.backend = dist.get_backend(group) if self.dist else None
         self.coalesce = COALESCE
         self._works = []
+        self._timing = []       # (wave, bytes received, start mark) of gathers issued since the last wait
 
     def _fail(self, wave, what, e):
         raise RuntimeError(f"flame_amd.shard: rank {self.rank} of {self.world} ({self.backend}): {what} of "
@@ -270,6 +297,9 @@ class _Comm:
         share one GPU; gloo has no device all-gather) stages through the host synchronously."""
         if not pairs or self.dist is None:
             return
+        if GATHER_TIMING is not None:
+            recv = sum((p.numel() - o.numel()) * p.element_size() for p, o in pairs)
+            self._timing.append((wave, recv, _mark(pairs[0][0])))
         try:
             self._all_gather_inplace(pairs, wave)
         except Exception as e:  # noqa: BLE001 - re-raised with the rank and wave
@@ -307,11 +337,24 @@ class _Comm:
     def wait(self) -> None:
         """Order the launch stream after every gather issued so far (host does not block)."""
         works, self._works = self._works, []
-        for wave, w in works:
+        timing, self._timing = self._timing, []
+        starts = {wave: (recv, start) for wave, recv, start in timing}
+        for i, (wave, w) in enumerate(works):
             try:
                 w.wait()
             except Exception as e:  # noqa: BLE001 - re-raised with the rank and wave
                 self._fail(wave, "wait on the all-gather", e)
+            if wave in starts and (i + 1 == len(works) or works[i + 1][0] != wave):
+                # right after the wave's last wait: the launch stream reaches this mark once the
+                # kernels queued so far and gathers 0..wave are done
+                self._timed(wave, *starts.pop(wave))
+        for wave, (recv, start) in starts.items():      # host-staged gathers: done at issue
+            self._timed(wave, recv, start)
+
+    @staticmethod
+    def _timed(wave, recv, start) -> None:
+        if GATHER_TIMING is not None:
+            GATHER_TIMING.append((wave, recv, start, _mark_like(start)))
 
 
 class _Work:

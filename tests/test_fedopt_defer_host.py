@@ -123,3 +123,79 @@ def test_nothing_to_aggregate_does_not_cut_the_chain(host_chain, empty, hold):
     else:          # one launch for the round: the empty arrival did not cut it
         assert calls == [2], calls
     assert opt.current_weights["w"] is final["w"]
+
+
+@pytest.mark.parametrize("trailing", [False, True])
+def test_agg_weights_after_an_empty_arrival(host_chain, trailing):
+    """the reference's do() sets agg_weights = FedAvg.do(...) = None for an arrival with
+    nothing to aggregate (fedopt.py:80-85); the deferred path matches once the queue has run -- and
+    a later real arrival makes agg_weights the base again."""
+    fake, calls = host_chain
+    opt, base = _after_passthrough("fedadam")
+    _arrive(opt, base, 1, 3)
+    last = opt.do(base, Cache(), total=10)            # empty arrival, queued chain not cut
+    if trailing:
+        last = _arrive(opt, base, 2, 4)
+    dict(last)
+    assert calls == [2 if trailing else 1]
+    if trailing:
+        assert opt.agg_weights is base
+    else:
+        assert opt.agg_weights is None
+        assert opt.current_weights is not None       # do() returned current_weights, as the reference
+
+
+def test_partial_launch_failure_poisons_the_optimizer(host_chain):
+    """when a later dtype group's launch fails after an earlier one ran (engine marks the
+    exception flame_partial), m / v / base disagree across keys: every later call refuses."""
+    fake, calls = host_chain
+    opt, base = _after_passthrough("fedyogi")
+    r = _arrive(opt, base, 1, 3)
+    orig = engine.fedopt_chain_
+
+    def partial(*a, **k):
+        e = RuntimeError("bf16 group refused")
+        e.flame_partial = True
+        raise e
+    engine.fedopt_chain_ = partial
+    try:
+        with pytest.raises(RuntimeError, match="bf16 group refused"):
+            r["w"]
+    finally:
+        engine.fedopt_chain_ = orig
+    with pytest.raises(RuntimeError, match="re-create the optimizer"):
+        _arrive(opt, base, 2, 4)
+
+
+def test_chain_plans_every_group_before_launching(monkeypatch):
+    """engine.fedopt_chain_ uploads every dtype group's tables before the first launch: a failure
+    while planning the second group launches nothing (the kernel is never called)."""
+    from flame_amd import _native as N
+    launched = []
+
+    real = N.lib()        # (the library loads without a GPU: chunk sizes etc. come from it)
+
+    class FakeLib:
+        def flame_fedopt_chain(self, *a):
+            launched.append(a[0])
+            return 0
+
+        def __getattr__(self, name):
+            return getattr(real, name)
+    uploads = []
+
+    def upload(meta, device):
+        uploads.append(len(meta))
+        if len(uploads) == 2:
+            raise RuntimeError("out of staging memory")
+        return torch.zeros(len(meta), dtype=torch.int64)
+    monkeypatch.setattr(N, "lib", lambda: FakeLib())
+    monkeypatch.setattr(engine._staging, "upload", upload)
+    monkeypatch.setattr(engine, "_client_row", lambda cl, b, dev, keep: ([b.data_ptr()] * len(cl), 0))
+    base = [torch.zeros(4096), torch.zeros(4096, dtype=torch.bfloat16)]
+    outs = [torch.empty_like(b) for b in base]
+    with pytest.raises(RuntimeError, match="out of staging memory"):
+        engine.fedopt_chain_("fedadam", base, [None, None], outs, [torch.empty_like(b) for b in base],
+                             [torch.empty_like(b) for b in base], [[b] for b in base], [1.0], [True],
+                             engine.fedopt_scalars(0.9, 0.99, 1e-2, 1e-3), True, [True, True])
+    assert uploads == [uploads[0], uploads[1]] and launched == []

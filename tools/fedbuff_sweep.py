@@ -2,7 +2,7 @@
 """Interleaved A/B of compile-time variants for the async FedBuff aggregator's round
 (asyncfl/top_aggregator.py:85-110: aggGoal arrivals, one per do(), then the fused
 scale_add -- or a middle's scale_add + upload delta, --delta), in ONE process: each variant
-is a build in build/diag/variants (tools/kernel_sweep.py --build), swapped in as the engine's
+is a build in build/ab/variants (tools/kernel_sweep.py --build), swapped in as the engine's
 native library round by round; kernel time from HIP events; the model (and deltas) checked
 bitwise across variants every round.
 
@@ -18,7 +18,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag", "variants")   # built by tools/kernel_sweep.py --build
+VDIR = os.path.join(ROOT, "build", "ab", "variants")   # built by tools/kernel_sweep.py --build
 
 
 class Cache(dict):
@@ -51,7 +51,7 @@ def main():
     names = a.variants.split(",")
     libs = {}
     for nm in names:
-        # a name with a "/" is a library path (e.g. flame_amd/libflame_amd.so, build/diag/lib_base.so)
+        # a name with a "/" is a library path (e.g. flame_amd/libflame_amd.so, build/ab/lib_base.so)
         path = os.path.join(ROOT, nm) if "/" in nm else os.path.join(VDIR, f"lib_{nm}.so")
         _native._lib, _native.LIB_PATH = None, path
         libs[nm] = _native.lib()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of compile-time variants of flame_feddyn_round through the FedDyn drop-in,
 in ONE process: each variant is a build of the product source with -DFLAME_T_* overrides in
-build/diag/variants (tools/kernel_sweep.py --build), swapped in as the engine's native library
+build/ab/variants (tools/kernel_sweep.py --build), swapped in as the engine's native library
 round by round;
 the same slab-resident arrivals drive one FedDyn instance per variant; kernel time from HIP
 events; cld_model checked bitwise across variants every round.
@@ -18,7 +18,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag", "variants")   # built by tools/kernel_sweep.py --build
+VDIR = os.path.join(ROOT, "build", "ab", "variants")   # built by tools/kernel_sweep.py --build
 
 
 class Cache(dict):

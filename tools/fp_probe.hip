@@ -7,6 +7,8 @@
 //   probe_rcp(lo, hi, v, out):  every b in [lo, hi): v=0 v_rcp_f32, v=1 rcp_rn -- vs __fdiv_rn(1, b)
 //   probe_div(seed, n, w, out): n counter-drawn (a, b) pairs: div_rn vs __fdiv_rn(a, b)
 //   probe_den(lo, hi, tau, out): every v in [lo, hi): RN(sqrt_rn(v) + tau) vs RN(sqrtf(v) + tau)
+//   probe_bf16_sqrt / _den / _div: the bf16 step's v_sqrt_f32 and num * v_rcp_f32(den) under the
+//                               bf16 rounding, on every bf16 operand (adapt_vec_bf16)
 // out[0] = mismatches, out[1..2] = the first mismatching operands (bits), out[3..4] = results.
 // Built by tools/fp_probe.py (hipcc, same flags as the product library).
 #include <hip/hip_runtime.h>
@@ -89,6 +91,29 @@ __global__ void div_kernel(uint64_t seed, uint64_t n, int wide, unsigned long lo
         const uint32_t am = static_cast<uint32_t>(r) & 0x807fffffu;          // sign + mantissa
         const uint32_t bm = static_cast<uint32_t>(r >> 32) & 0x7fffffu;
         uint32_t ea, eb;
+        uint32_t bmm = bm;
+        if (wide == 2) {
+            // the admitted range's corners: |a| in [2^-85, 2^-83) over b in [2^39, 2^40],
+            // and |a| in [2^99, 2^100] over b in [2^-20, 2^-19) -- quotients down to 2^-125, where
+            // Markstein's residual r * y is subnormal, and up to 2^120
+            const uint32_t k = static_cast<uint32_t>(r >> 62);
+            if (k < 2) {
+                ea = 42u + k;
+                eb = (r >> 61) & 1 ? 166u : 167u;
+                if (eb == 167u) bmm = 0u;                      // b = 2^40 exactly
+            } else {
+                ea = k == 2 ? 226u : 227u;
+                eb = 107u;
+            }
+            const uint32_t aa = (ea == 227u) ? (am & 0x80000000u) : am;   // |a| = 2^100 exactly
+            const float a = __uint_as_float(aa | (ea << 23));
+            const float b = __uint_as_float((eb << 23) | bmm);
+            const float want = __fdiv_rn(a, b);
+            const float got = flame_fm::div_rn(a, b);
+            if (__float_as_uint(got) != __float_as_uint(want))
+                report(out, __float_as_uint(a), __float_as_uint(b), __float_as_uint(got), __float_as_uint(want));
+            continue;
+        }
         if (wide) {
             ea = static_cast<uint32_t>((r >> 23) & 0xff) % 255u;
             eb = 67u + static_cast<uint32_t>((r >> 55) % 194u);
@@ -118,9 +143,67 @@ __global__ void den_kernel(uint64_t lo, uint64_t hi, float tau, unsigned long lo
     }
 }
 
+// bf16 (adapt_vec_bf16 in fedagg.hip): the bf16 rounding of v_sqrt_f32(v) vs of the correctly
+// rounded root, for every bf16 v with hi16 in [lo, hi).
+__device__ __forceinline__ float rbf(float x) { return static_cast<float>(static_cast<__bf16>(x)); }
+__global__ void bf16_sqrt_kernel(uint32_t lo, uint32_t hi, unsigned long long* out) {
+    const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const float v = __uint_as_float(i << 16);
+    const float want = rbf(__builtin_sqrtf(v));
+    const float got = rbf(__builtin_amdgcn_sqrtf(v));
+    if (__float_as_uint(got) != __float_as_uint(want)) report(out, i << 16, 0, __float_as_uint(got), __float_as_uint(want));
+}
+
+// ... and of num * v_rcp_f32(den) vs of the correctly rounded quotient, for every bf16 num (hi16 =
+// blockIdx.y * 256 + x) that adapt_vec admits (+-0, 2^-85 <= |num| <= 2^100) and every bf16 den
+// with hi16 in [dlo, dhi) (den = RN(RN(sqrt v) + tau) lies in [2^-20, 2^40] on admitted lanes).
+__global__ void bf16_div_kernel(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+    const uint32_t nb = (blockIdx.y * 256u + threadIdx.x) << 16;
+    const float num = __uint_as_float(nb);
+    const float an = __builtin_fabsf(num);
+    if (!(an == 0.f || (an >= 0x1p-85f && an <= 0x1p100f))) return;
+    for (uint32_t d = dlo + blockIdx.x; d < dhi; d += gridDim.x) {
+        const float den = __uint_as_float(d << 16);
+        const float want = rbf(__fdiv_rn(num, den));
+        const float got = rbf(__fmul_rn(num, __builtin_amdgcn_rcpf(den)));
+        if (__float_as_uint(got) != __float_as_uint(want)) report(out, nb, d << 16, __float_as_uint(got), __float_as_uint(want));
+    }
+}
+
+// ... and the denominator the step forms from it, RN_bf16(RN_bf16(sqrt v) + tau), for every bf16 v with
+// hi16 in [lo, hi) (v_sqrt_f32 flushes subnormal inputs to a zero root: under tau >= 2^-20 the
+// denominator is tau either way)
+__global__ void bf16_den_kernel(uint32_t lo, uint32_t hi, float tau, unsigned long long* out) {
+    const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const float v = __uint_as_float(i << 16);
+    const float want = rbf(__fadd_rn(rbf(__builtin_sqrtf(v)), tau));
+    const float got = rbf(__fadd_rn(rbf(__builtin_amdgcn_sqrtf(v)), tau));
+    if (__float_as_uint(got) != __float_as_uint(want)) report(out, i << 16, __float_as_uint(tau), __float_as_uint(got), __float_as_uint(want));
+}
+
 }  // namespace
 
 extern "C" {
+
+int probe_bf16_den(uint32_t lo, uint32_t hi, float tau, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    if (hi > lo) bf16_den_kernel<<<(hi - lo + 255) / 256, 256>>>(lo, hi, tau, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_bf16_sqrt(uint32_t lo, uint32_t hi, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    if (hi > lo) bf16_sqrt_kernel<<<(hi - lo + 255) / 256, 256>>>(lo, hi, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_bf16_div(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    bf16_div_kernel<<<dim3(512, 256), 256>>>(dlo, dhi, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
 
 int probe_sqrt(uint64_t lo, uint64_t hi, int variant, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));

@@ -15,7 +15,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "build", "diag", "libfp_probe.so")
+LIB = os.path.join(ROOT, "build", "probe", "libfp_probe.so")
 
 NORMAL_LO, INF = 0x00800000, 0x7F800000
 
@@ -74,6 +74,26 @@ def main():
         show(f"div_rn {n} admitted pairs (seed {seed})", L.probe_div(u64(seed), u64(n), 0, p), True)
     show(f"div_rn {n // 4} pairs over every finite a, b in [2^-60, 2^66] (outside the admitted range)",
          L.probe_div(u64(3), u64(n // 4), 1, p), False)
+    show(f"div_rn {n // 4} pairs at the admitted corners (|a| near 2^-85 over b near 2^40, |a| near 2^100 "
+         f"over b near 2^-20)", L.probe_div(u64(4), u64(n // 4), 2, p), True)
+    # bf16 (adapt_vec_bf16): v_sqrt_f32 / num * v_rcp_f32 under the bf16 rounding, exhaustively
+    u32 = ctypes.c_uint32
+    L.probe_bf16_sqrt.argtypes = [u32, u32, ctypes.c_void_p]
+    L.probe_bf16_div.argtypes = [u32, u32, ctypes.c_void_p]
+    L.probe_bf16_den.argtypes = [u32, u32, ctypes.c_float, ctypes.c_void_p]
+    show("bf16: RN_bf16(v_sqrt_f32(v)) == RN_bf16(sqrt(v)) on bf16 v = +0", L.probe_bf16_sqrt(0, 1, p), True)
+    show("bf16: RN_bf16(v_sqrt_f32(v)) == RN_bf16(sqrt(v)) on every normal bf16 v in [2^-126, 2^78]",
+         L.probe_bf16_sqrt(0x0080, 0x6681, p), True)
+    show("bf16: the same on the bf16 subnormals (v_sqrt_f32 flushes them: informational)",
+         L.probe_bf16_sqrt(1, 0x0080, p), False)
+    for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):
+        tb = float(torch.tensor(tau, dtype=torch.bfloat16))       # the step's tau is pre-rounded to bf16
+        show(f"bf16: RN(RN(v_sqrt_f32(v)) + {tb:g}) == RN(RN(sqrt(v)) + {tb:g}) on every admitted bf16 v "
+             f"(+0 .. 2^78, subnormals included)", L.probe_bf16_den(0, 0x6681, tb, p), True)
+    show("bf16: v_sqrt_f32 on every other bf16 pattern (negative, > 2^78, inf, NaN; informational)",
+         L.probe_bf16_sqrt(0x6681, 0x10000, p), False)
+    show("bf16: RN_bf16(num * v_rcp_f32(den)) == RN_bf16(num / den) on every admitted bf16 num x every bf16 den "
+         "in [2^-20, 2^40]", L.probe_bf16_div(0x3580, 0x5381, p), True)
     # adapt_vec admits v below 2^-96 too: it only reaches sqrt(v) + tau (tau >= 2^-20)
     L.probe_den.argtypes = [u64, u64, ctypes.c_float, ctypes.c_void_p]
     for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""One GPU session on the MI355X box: named steps run one after another, each under its own time
+limit, output in gpurun_out/<tag>_<step>.log; the session stops at the first step that fails,
+times out or crashes (no retries, nothing else touches the GPU after a fault).  Replaces round 5's
+thirty one-off tools/gpu_r05_*.sh scripts.
+
+    gpurun --timeout 1100 -- python3 tools/gpu_session.py r06a probe chain_bf16 e2e_shm
+    python3 tools/gpu_session.py --list
+
+The parent never initialises the GPU (every step is a child process, never an exec).  A step is
+a command line (run from the repository root) and a time limit; ``{key}`` fields are filled from
+``--set key=value`` (defaults in PARAMS).  Summaries worth keeping are copied into profiles/
+afterwards (tools/README.md).
+"""
+import argparse
+import os
+import shlex
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PY = sys.executable or "python3"
+AB = "build/ab/variants/lib_r05_step.so"     # the round-5 step (tools/kernel_sweep.py --build --variants r05_step)
+PARAMS = {"clients": "64", "params": "2000000", "steps": "10", "warmup": "3"}
+
+# name -> (seconds, command).  Commands are lists; "rocprof:" prefixes run under rocprofv3 stats.
+STEPS = {
+    "pytest_gpu": (1000, [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-q", "--timeout", "300",
+                          "--timeout-method", "thread", "--durations", "5"]),
+    "pytest_chain": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_eager_fedopt_chain.py",
+                           "tests/test_gpu_fastmath.py", "tests/test_gpu_dtype_matrix.py", "-m", "gpu", "-x", "-q",
+                           "--timeout", "200", "--timeout-method", "thread"]),
+    "smoke": (300, [PY, "-c", "import __graft_entry__ as g; g.smoke(); print('smoke ok')"]),
+    "bench_default": (300, [PY, "bench.py"]),
+    "probe": (300, [PY, "tools/fp_probe.py"]),
+    # eager FedOPT chain, 64 x 25M: the shipped library against the round-5 step, one process, bitwise
+    **{f"chain_{v}_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", dt, "--rounds", "6",
+                                  "--libs", f"flame_amd/libflame_amd.so,{AB}"])
+       for v in ("adam", "yogi", "adagrad") for dt in ("f32", "bf16")},
+    **{f"eager_{v}": (300, [PY, "bench.py", "--workload", f"fed{v}_eager"]) for v in ("adam", "yogi", "adagrad")},
+    # the three variants interleaved in ONE process (Yogi within 3 % of Adam)
+    **{f"chain_variants_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", "fedadam,fedyogi,fedadagrad",
+                                      "--dtype", dt, "--rounds", "6", "--libs", "flame_amd/libflame_amd.so"])
+       for dt in ("f32", "bf16")},
+    # end-to-end rows, 64 clients x 25M fp32 from host memory back to host memory
+    **{f"e2e_{m}": (400, [PY, "bench.py", "--e2e", "--e2e-mode", m])
+       for m in ("zerocopy", "copy", "pageable", "shm", "shm_reference", "eager", "shard", "shm_shard", "wire",
+                 "wire_reference")},
+    # the N-GPU end-to-end line rehearsed with gloo ranks sharing the box's one GPU
+    **{f"e2e_shm_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--e2e",
+                                  "--e2e-mode", "shm", "--clients", "{clients}", "--params", "{params}"])
+       for n in (2, 8)},
+    **{f"sharded_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--clients",
+                                  "{clients}", "--params", "{params}"]) for n in (2, 8)},
+    **{f"hier_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--workload",
+                               "hier_fedbuff", "--clients", "256", "--params", "{params}"]) for n in (2,)},
+    "force_shard": (300, [PY, "bench.py", "--force-shard"]),
+    # kernel trace of a bench line (the same process's HIP-event numbers are in the log)
+    "rocprof_chain": (300, ["rocprof:", PY, "tools/chain_sweep.py", "--variant", "fedadam", "--dtype", "bf16",
+                            "--rounds", "3", "--libs", "flame_amd/libflame_amd.so"]),
+}
+
+
+def expand(cmd, params, tag, name):
+    out = [c.format(**params) for c in cmd]
+    if out and out[0] == "rocprof:":
+        d = os.path.join("gpurun_out", f"{tag}_{name}_prof")
+        out = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", name, "--"] + out[1:]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag", nargs="?")
+    ap.add_argument("steps", nargs="*")
+    ap.add_argument("--set", action="append", default=[], help="key=value for {key} fields")
+    ap.add_argument("--list", action="store_true")
+    a = ap.parse_args()
+    if a.list or not a.tag:
+        for nm, (lim, cmd) in STEPS.items():
+            print(f"{nm:22s} {lim:5d} s  {' '.join(cmd)}")
+        return 0
+    params = dict(PARAMS)
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        params[k] = v
+    unknown = [s for s in a.steps if s not in STEPS]
+    if unknown:
+        print(f"gpu_session: unknown step(s) {unknown}; --list shows them", file=sys.stderr)
+        return 2
+    os.chdir(os.environ.get("GRAFT_REPO_ROOT", ROOT))
+    os.makedirs("gpurun_out", exist_ok=True)
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MASTER_ADDR="127.0.0.1")
+    for name in a.steps:
+        lim, cmd = STEPS[name]
+        argv = expand(cmd, params, a.tag, name)
+        log = os.path.join("gpurun_out", f"{a.tag}_{name}.log")
+        t0 = time.time()
+        with open(log, "w") as f:
+            f.write("$ " + " ".join(shlex.quote(x) for x in argv) + "\n")
+            f.flush()
+            rc = subprocess.call(["timeout", "-k", "10", str(lim)] + argv, stdout=f, stderr=subprocess.STDOUT, env=env)
+        tail = open(log).read().splitlines()[-4:]
+        print(f"[{a.tag}] {name}: rc={rc} {time.time() - t0:.0f} s", flush=True)
+        for ln in tail:
+            print("    " + ln[:400], flush=True)
+        if rc != 0:       # a failure, a time limit (124 / 137), an abort or a fault: nothing more on the GPU
+            print(f"[{a.tag}] stopping after {name} (rc={rc})", flush=True)
+            return rc
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -29,7 +29,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag", "attrib")   # uploaded to the box (not in .gpurunignore)
+VDIR = os.path.join(ROOT, "build", "ab", "attrib")   # uploaded to the box (not in .gpurunignore)
 SLOTS = 288
 
 

@@ -20,7 +20,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag", "hier")   # travels to the GPU box with the tree
+VDIR = os.path.join(ROOT, "build", "ab", "hier")   # travels to the GPU box with the tree
 
 # Round-2/3 sweeps of the store grouping, unroll, residency (LDS groups of 12 = 3 workgroups per
 # CU), prefetch and pipelining variants are in profiles/r02_hier_*.log, r03z*_hier_sweep.log.
@@ -41,7 +41,7 @@ def build_variants(names):
 
 
 def load(name):
-    # a name with a "/" is a library path (e.g. build/diag/lib_hnx.so, flame_amd/libflame_amd.so)
+    # a name with a "/" is a library path (e.g. build/ab/lib_hnx.so, flame_amd/libflame_amd.so)
     L = ctypes.CDLL(os.path.join(ROOT, name) if "/" in name else os.path.join(VDIR, f"lib_{name}.so"))
     vp, i32, i64, u32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint, ctypes.c_float
     L.flame_hier_fedbuff.restype = ctypes.c_int

@@ -20,7 +20,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "diag", "variants")   # travels to the GPU box with the tree
+VDIR = os.path.join(ROOT, "build", "ab", "variants")   # travels to the GPU box with the tree
 
 # Knobs of the PRODUCT source (flame_amd/csrc/fedagg.hip's FLAME_T_* defaults are the shipped
 # kernel).  Variants of rounds 1-4 that were measured no faster and are no longer in the source
@@ -61,6 +61,10 @@ VARIANTS = {
     "lo_wgc8_all": {"FLAME_T_LO_WGC": 8, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
     "lo_wgc16_all": {"FLAME_T_LO_WGC": 16, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
     "lo_wgc32_all": {"FLAME_T_LO_WGC": 32, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
+    # round 6: the round-5 bf16 FedOPT step / Yogi sign (generic per-element code), for the chain A/B
+    "r05_step": {"FLAME_T_BF16_PACKED": 0, "FLAME_T_YOGI_SIGN": 0},
+    "r05_bf16": {"FLAME_T_BF16_PACKED": 0},
+    "r05_yogi": {"FLAME_T_YOGI_SIGN": 0},
 }
 
 
@@ -76,7 +80,7 @@ def build_variants(names):
 
 
 def load(name):
-    # a name with a "/" is a library path (e.g. build/diag/lib_prev.so)
+    # a name with a "/" is a library path (e.g. build/ab/lib_prev.so)
     L = ctypes.CDLL(os.path.join(ROOT, name) if "/" in name else os.path.join(VDIR, f"lib_{name}.so"))
     vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint
     L.flame_chunk_elems.restype = i64
