@@ -1608,6 +1608,8 @@ def bench_e2e_shm_sharded(args, world, rank, dev, n, P):
             my_sizes[i] = len(b)
             del b
         del tmp
+        print(f"bench.py e2e: rank {rank}: {len(mine)} trainer messages written to shared memory", file=sys.stderr,
+              flush=True)
         sizes = {}
         for d in gather_objects(world, my_sizes):
             sizes.update(d)
@@ -1664,6 +1666,7 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
         for _ in range(args.warmup):
             step()
         phases.clear()
+        print(f"bench.py e2e: rank {rank}: warm-up done", file=sys.stderr, flush=True)
         shard.GATHER_TIMING = []
         elapsed, events = timed(world, args.steps, 0, step)
         gt, shard.GATHER_TIMING = shard.GATHER_TIMING, None

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import collections
 import collections.abc
+import os
 from typing import Dict, List
 
 import numpy as np
@@ -42,6 +43,10 @@ PINNED_RING = 4
 # a payload span is staged as one transfer only if it is at most this much larger than the
 # tensor bytes it carries (pickle framing and storage headers are a few hundred bytes per key)
 STAGE_SPAN_SLACK = 1.25
+# a page-locked host source that is not 4-byte aligned (hipMemcpy2DAsync runs ~5 GB/s there):
+# "stage" = a contiguous DMA into HBM + the tile kernel, "mapped" = the tile kernel reading it over
+# PCIe through its device-mapped address (tools/ingest_diag.py measures both)
+MISALIGNED_HOST = os.environ.get("FLAME_AMD_MISALIGNED_HOST", "stage")
 
 
 class SlotWeights(dict):
@@ -243,6 +248,29 @@ class UpdateSlab:
         staged = []
         if len(host_rows) > 1:
             dev_rows += self._stage_payloads(host_rows, keep, st, staged)
+        # hipMemcpy2DAsync drops to ~5 GB/s for a host source that is not 4-byte aligned -- and a
+        # storage inside a pickled payload starts anywhere (a decoded view into a LIFL shm segment,
+        # or this rank's slice of one) -- against ~50 GB/s for the tile-copy kernel reading the same
+        # page-locked bytes over PCIe through their device-mapped address
+        # (profiles/r06e2_h2d_paths.log, r06e_ingest_diag.log)
+        mapped = []
+        if host_rows:
+            by_ptr = {t.data_ptr(): t for t in keep if not t.is_cuda}
+            for r in [r for r in host_rows if r[0] % 4]:
+                t = by_ptr.get(r[0])
+                if t is None or not t.is_pinned():
+                    continue
+                host_rows.remove(r)
+                if MISALIGNED_HOST == "mapped":
+                    dev_rows.append((engine.host_device_pointer(r[0]), r[1], r[2], r[3]))
+                    mapped.append(t)
+                else:        # "stage": one contiguous DMA (full rate at any alignment), then the kernel tiles it in HBM
+                    with torch.cuda.stream(st):
+                        d = t.reshape(-1).to(self.device, non_blocking=True)
+                    d.record_stream(st)
+                    keep.append(d)
+                    staged.append(t)
+                    dev_rows.append((d.data_ptr(), r[1], r[2], r[3]))
         L = N.lib()
         if dev_rows:
             tab = np.asarray(dev_rows, dtype=np.uint64).view(np.int64)
@@ -253,6 +281,8 @@ class UpdateSlab:
                         t.record_stream(st)       # read on `st`: keep the caching allocator off it
             if staged:
                 engine._staging.hold_on(st, staged)
+            if mapped:       # read by the kernel over PCIe: held until it has run
+                engine._staging.hold_on(st, mapped)
         if host_rows:
             tab = np.asarray(host_rows, dtype=np.uint64).view(np.int64)
             N.check(L.flame_slab_write_2d(tab.ctypes.data, len(host_rows), st.cuda_stream))

@@ -184,3 +184,37 @@ def test_decoded_payloads_one_transfer_each_and_pinned_ring():
         co[f"t{i}"] = S.TR({k: v.clone() for k, v in u.items()}, counts[i])
     O.OracleFedAvg().do(exp, co, total=sum(counts))
     S.assert_bitwise("payload-staged fedavg", S.to_cpu(got), exp)
+
+
+@pytest.mark.parametrize("offset", [1, 3, 4, 8])
+def test_misaligned_pinned_host_source(monkeypatch, offset):
+    """A pinned host source that is not 4-byte aligned (a storage inside a pickled payload in a
+    LIFL shm segment, or a rank's slice of one) goes through the tile-copy kernel over its
+    device-mapped address, not hipMemcpy2DAsync (~5 GB/s there, profiles/r06e2_h2d_paths.log);
+    aligned ones keep the pitched DMA.  Bitwise either way, ragged tail included."""
+    from flame_amd import _native as N
+    from flame_amd.slab import UpdateSlab
+    real = N.lib()
+    calls = []
+
+    class Spy:
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name in ("flame_slab_write", "flame_slab_write_2d"):
+                def wrapped(*a):
+                    calls.append(name)
+                    return fn(*a)
+                return wrapped
+            return fn
+    monkeypatch.setattr(N, "lib", lambda: Spy())
+    n = 3 * 1024 + 17
+    buf = torch.empty(4 * n + 64, dtype=torch.uint8, pin_memory=True)
+    src = torch.frombuffer(buf.numpy(), dtype=torch.float32, offset=offset, count=n)
+    src.copy_(torch.randn(n, generator=torch.Generator().manual_seed(offset)))
+    assert src.is_pinned() and src.data_ptr() % 4 == offset % 4
+    slab = UpdateSlab({"w": torch.empty(n)}, capacity=3, device=DEV)
+    slab.put({"w": torch.zeros(n, device=DEV)})
+    sw = slab.put({"w": src})
+    torch.cuda.synchronize()
+    assert torch.equal(slab.read(sw.slot, "w").cpu(), src)
+    assert calls[-1] == ("flame_slab_write" if offset % 4 else "flame_slab_write_2d"), calls

@@ -22,18 +22,22 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = sys.executable or "python3"
 AB = "build/ab/variants/lib_r05_step.so"     # the round-5 step (tools/kernel_sweep.py --build --variants r05_step)
-PARAMS = {"clients": "64", "params": "2000000", "steps": "10", "warmup": "3"}
+PARAMS = {"clients": "64", "params": "2000000", "steps": "10", "warmup": "3", "offsets": "0,4,356"}
 
 # name -> (seconds, command).  Commands are lists; "rocprof:" prefixes run under rocprofv3 stats.
 STEPS = {
     "pytest_gpu": (1000, [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-q", "--timeout", "300",
                           "--timeout-method", "thread", "--durations", "5"]),
+    "pytest_slab": (300, [PY, "-u", "-m", "pytest", "tests/test_gpu_slab_write.py", "tests/test_gpu_shm.py", "-m", "gpu",
+                          "-x", "-q", "--timeout", "200", "--timeout-method", "thread"]),
     "pytest_chain": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_eager_fedopt_chain.py",
                            "tests/test_gpu_fastmath.py", "tests/test_gpu_dtype_matrix.py", "-m", "gpu", "-x", "-q",
                            "--timeout", "200", "--timeout-method", "thread"]),
     "smoke": (300, [PY, "-c", "import __graft_entry__ as g; g.smoke(); print('smoke ok')"]),
     "bench_default": (300, [PY, "bench.py"]),
     "probe": (300, [PY, "tools/fp_probe.py"]),
+    "h2d_paths": (200, [PY, "tools/h2d_paths.py", "--offsets", "{offsets}"]),
+    "ingest_diag": (300, [PY, "tools/ingest_diag.py"]),
     # eager FedOPT chain, 64 x 25M: the shipped library against the round-5 step, one process, bitwise
     **{f"chain_{v}_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", dt, "--rounds", "6",
                                   "--libs", f"flame_amd/libflame_amd.so,{AB}"])
@@ -56,18 +60,56 @@ STEPS = {
     **{f"hier_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--workload",
                                "hier_fedbuff", "--clients", "256", "--params", "{params}"]) for n in (2,)},
     "force_shard": (300, [PY, "bench.py", "--force-shard"]),
-    # kernel trace of a bench line (the same process's HIP-event numbers are in the log)
-    "rocprof_chain": (300, ["rocprof:", PY, "tools/chain_sweep.py", "--variant", "fedadam", "--dtype", "bf16",
-                            "--rounds", "3", "--libs", "flame_amd/libflame_amd.so"]),
+    # the evidence collection (round 5's gpu_r05_prof.sh): each default path's bench line under
+    # rocprofv3 --kernel-trace --stats (the SAME process's kernel summary) ...
+    **{f"prof_{w}": (400, ["rocprof:", PY, "bench.py", *a]) for w, a in {
+        "fedavg": ["--steps", "20", "--warmup", "5"],
+        "fedadam": ["--workload", "fedadam", "--steps", "10", "--warmup", "3", "--cpu-clients", "16"],
+        "fedyogi": ["--workload", "fedyogi", "--steps", "10", "--warmup", "3", "--cpu-clients", "0"],
+        "fedadagrad": ["--workload", "fedadagrad", "--steps", "10", "--warmup", "3", "--cpu-clients", "0"],
+        "hier_fedbuff": ["--workload", "hier_fedbuff", "--steps", "10", "--warmup", "3", "--cpu-clients", "0"],
+        "fedbuff": ["--workload", "fedbuff", "--steps", "10", "--warmup", "3", "--cpu-clients", "0"],
+        "fedadam_eager": ["--workload", "fedadam_eager", "--steps", "10", "--warmup", "3"],
+        "fedyogi_eager": ["--workload", "fedyogi_eager", "--steps", "10", "--warmup", "3"],
+        "fedadagrad_eager": ["--workload", "fedadagrad_eager", "--steps", "10", "--warmup", "3"],
+        "feddyn": ["--workload", "feddyn", "--steps", "6", "--warmup", "2", "--cpu-clients", "0"]}.items()},
+    "prof_chain_bf16": (300, ["rocprof:", PY, "tools/chain_sweep.py", "--variant", "fedadam,fedyogi,fedadagrad",
+                              "--dtype", "bf16", "--rounds", "3", "--libs", "flame_amd/libflame_amd.so"]),
+    # ... and PMC passes, one counter per run (no trace domains), for the HBM traffic of a kernel
+    **{f"pmc_{w}_{c}": (120, ["pmc:", c, rx, PY, "bench.py", *a, "--steps", "3", "--warmup", "1", "--cpu-clients", "0"])
+       for w, rx, a in (("fedavg", "agg_reduce", []),
+                        ("fedadam_eager", "fedopt_chain", ["--workload", "fedadam_eager"]),
+                        ("fedyogi_eager", "fedopt_chain", ["--workload", "fedyogi_eager"]),
+                        ("fedadagrad_eager", "fedopt_chain", ["--workload", "fedadagrad_eager"]),
+                        ("hier_fedbuff", "hier_fedbuff", ["--workload", "hier_fedbuff"]))
+       for c in ("FETCH_SIZE", "WRITE_SIZE")},
+    **{f"pmc_chain_{dt}_{lb}_{c.split()[0]}": (120, ["pmc:", c, "fedopt_chain", PY, "tools/chain_sweep.py",
+                                                     "--variant", "fedadam", "--dtype", dt, "--rounds", "1", "--libs",
+                                                     lib])
+       for dt in ("f32", "bf16") for lb, lib in (("r06", "flame_amd/libflame_amd.so"), ("r05", AB))
+       for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU SQ_WAVES")},
 }
 
 
 def expand(cmd, params, tag, name):
     out = [c.format(**params) for c in cmd]
+    d = os.path.join("gpurun_out", tag, name)
     if out and out[0] == "rocprof:":
-        d = os.path.join("gpurun_out", f"{tag}_{name}_prof")
-        out = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", name, "--"] + out[1:]
+        out = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--"] + out[1:]
+    elif out and out[0] == "pmc:":
+        counters, rx = out[1].split(), out[2]
+        out = ["rocprofv3", "--pmc", *counters, "--kernel-include-regex", rx, "--output-format", "csv", "-d", d,
+               "-o", "run", "--"] + out[3:]
     return out
+
+
+def tidy(tag, name):
+    """Drop a kernel-trace run's per-dispatch CSV (MBs); its stats summary stays."""
+    d = os.path.join("gpurun_out", tag, name)
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("kernel_trace.csv"):
+                os.remove(os.path.join(root, f))
 
 
 def main():
@@ -91,7 +133,7 @@ def main():
         return 2
     os.chdir(os.environ.get("GRAFT_REPO_ROOT", ROOT))
     os.makedirs("gpurun_out", exist_ok=True)
-    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MASTER_ADDR="127.0.0.1", TMPDIR="/tmp")
     for name in a.steps:
         lim, cmd = STEPS[name]
         argv = expand(cmd, params, a.tag, name)
@@ -101,6 +143,7 @@ def main():
             f.write("$ " + " ".join(shlex.quote(x) for x in argv) + "\n")
             f.flush()
             rc = subprocess.call(["timeout", "-k", "10", str(lim)] + argv, stdout=f, stderr=subprocess.STDOUT, env=env)
+        tidy(a.tag, name)
         tail = open(log).read().splitlines()[-4:]
         print(f"[{a.tag}] {name}: rc={rc} {time.time() - t0:.0f} s", flush=True)
         for ln in tail:
