@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 
 ISSUE_S = None  # host issue time of the timed steps (set by timed())
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
+PCIE_SPEC_GBS = 64.0   # the host link: PCIe 5.0 x16, per direction, before protocol overhead
 METRIC = "aggregated params/sec (device-resident), 1024-client FedAvg @1/2/4/8 GPU"
 
 
@@ -112,6 +113,10 @@ def parse():
                     help="zerocopy: kernel streams pinned host memory; copy: pinned -> HBM on a copy "
                          "stream overlapped with the reduction; pageable: reference weights_to_model_device; "
                          "shm at N > 1 (or shm_shard at any N): the sharded shm ingest + gathers + egress encode")
+    ap.add_argument("--e2e-egress", default="sharded", choices=["sharded", "gathered"],
+                    help="N-GPU shm line: sharded = no all-gather, every rank D2Hs its ranges into one shared "
+                         "payload (flame_amd.egress.ShardedEgress); gathered = in-place all-gathers, then rank 0 "
+                         "encodes the whole model (MessageEncoder)")
     ap.add_argument("--e2e-placement", default="slab", choices=["slab", "hbm"],
                     help="eager mode: DeviceUpdateCache placement of the arriving updates")
     ap.add_argument("--cpu-clients", type=int, default=128, help="cpu_baseline sample size (0: skip)")
@@ -1589,7 +1594,9 @@ def bench_e2e_shm_sharded(args, world, rank, dev, n, P):
     G = P * world
     counts = synth.counts(args.seed, n)
     total = int(counts.sum())
-    sopt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=dev, fracs=_fracs(args, shard))
+    gathered = args.e2e_egress == "gathered"
+    sopt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=dev, fracs=_fracs(args, shard),
+                                  gather=gathered)
     sopt.set_layout({"model": torch.empty(G, dtype=torch.float32, device="meta")})
     plan = sopt.plan
     tag = f"flamee2e{os.environ.get('MASTER_PORT', os.getpid())}"
@@ -1635,7 +1642,12 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
     model = torch.empty(G, dtype=torch.float32, device=dev)
     engine.synth_fill_(model, args.seed, 0, 0, 1.0)
     weights = {"model": model}
-    enc = MessageEncoder(ring=1) if rank == 0 else None
+    gathered = args.e2e_egress == "gathered"
+    if gathered:
+        enc = MessageEncoder(ring=1) if rank == 0 else None
+    else:
+        from flame_amd.egress import ShardedEgress
+        enc = ShardedEgress(plan, f"{tag}_egress")
     keys = [f"{i:05d}" for i in range(n)]
     phases, out = [], {}
     rounds = [0]
@@ -1653,8 +1665,12 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
         e[1].record()
         sopt.do(weights, scache, total=total, num_trainers=n)
         e[2].record()
-        if enc is not None:         # the message every trainer gets (one encode, one D2H into it)
-            out["payload"] = enc.encode({"weights": weights, "round": rounds[0]})
+        # the message every trainer gets: one encode; gathered: rank 0 D2Hs the whole model into it,
+        # sharded: every rank D2Hs its ranges into the one shared payload (rank 0 receives it)
+        if enc is not None:
+            p = enc.encode({"weights": weights, "round": rounds[0]})
+            if rank == 0:
+                out["payload"] = p
         e[3].record()
         phases.append((t1 - t0, e))
 
@@ -1679,21 +1695,26 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
         k_ms = ks["avg_s"] * ks["launches"] / args.steps * 1e3 if ks else None
         attrib = time_attribution(world, k_ms, elapsed / args.steps * 1e3, gt)
         per_rank = gather_objects(world, ph)
-        # untimed self-checks: every rank holds the same model == the host restatement on sampled
-        # elements, and rank 0's egress payload decodes (the trainers' cloudpickle.loads) to it
+        # untimed self-checks: gathered -- every rank holds the same model == the host restatement on
+        # sampled elements; both -- rank 0's egress payload decodes (the trainers' cloudpickle.loads)
+        # to a model whose every rank's ranges equal that rank's device copy (digests) and whose
+        # sampled elements equal the host restatement, bitwise
         idx = sample_indices(plan, "model", seed=args.seed)
-        gc = verify_sharded(model, idx, host_fedavg_rounds(args.seed, counts, idx, rounds[0]))
+        expected = host_fedavg_rounds(args.seed, counts, idx, rounds[0])
+        gc = verify_sharded(model, idx, expected) if gathered else {}
         gc["rounds_checked"] = rounds[0]
+        ec = egress_check(plan, world, rank, model, out.get("payload"), idx, expected)
+        gc.update(ec)
+        if not gathered:      # (for _checked) no rank holds the whole model: the payload is the check
+            gc["ranks_agree"] = ec["egress_range_mismatches"] == 0
+            gc["sample_mismatches_per_rank"] = [ec["egress_sample_mismatches"]] + [0] * (world - 1)
+            gc["sample_parity"] = "bitwise" if ec["egress_payload_bitwise"] else "MISMATCH"
+        elif not ec["egress_payload_bitwise"]:
+            gc["ranks_agree"] = False
         probe = pcie_probe(dev, world)
         ref = None
-        if rank == 0:
-            import cloudpickle
-            msg = cloudpickle.loads(bytes(out["payload"]))
-            gc["egress_payload_bitwise"] = bool(torch.equal(msg["weights"]["model"].view(torch.int32),
-                                                           model.cpu().view(torch.int32)))
-            gc["egress_payload_bytes"] = len(out["payload"])
-            if args.cpu_clients > 0:
-                ref = e2e_reference_sample(names, sizes, counts, total, G, dev)
+        if rank == 0 and args.cpu_clients > 0:
+            ref = e2e_reference_sample(names, sizes, counts, total, G, dev)
         if rank == 0:
             ms = elapsed / args.steps * 1e3
             h2d = n * G * 4          # every update's bytes cross PCIe once (each rank its ranges)
@@ -1707,12 +1728,16 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
                 "higher_is_better": True, "scaling": "weak", "dtype": "f32", "settle": SETTLE,
                 "data": "synthetic (counter-based generator) cloudpickled into POSIX shm segments, one per trainer",
                 "config": {"workload": f"e2e shm: {n} trainers x {G} fp32 params ({P} per GPU), parameter-sharded "
-                                       f"ingest over {world} rank(s), in-place all-gathers, rank-0 egress encode",
+                                       f"ingest over {world} rank(s), "
+                                       + ("in-place all-gathers, rank-0 egress encode" if gathered else
+                                          "no all-gather, every rank's ranges D2H into one shared egress payload"),
+                           "egress": args.e2e_egress,
                            "clients": n, "params_per_gpu": P, "global_params": G,
                            "parallelism": f"param-shard{world}"},
                 "host_read_GBps": h2d / (ms / 1e3) / 1e9,
                 "roofline": {"bound": "pcie", "achieved": achieved, "peak": peak, "unit": "GB/s",
                              "frac": achieved / peak if peak else None,
+                             "spec_GBps": PCIE_SPEC_GBS * world, "frac_of_spec": achieved / (PCIE_SPEC_GBS * world),
                              "bytes_per_step": {"h2d": h2d, "d2h": d2h},
                              "per_link_achieved_GBps": h2d / world / (ms / 1e3) / 1e9,
                              "per_link_peak_GBps": probe["h2d_GBps_by_rank"], **{"probe": probe}},
@@ -1736,9 +1761,34 @@ def _e2e_shm_sharded_run(args, world, rank, dev, n, P, G, counts, total, sopt, p
     finally:
         shard.GATHER_TIMING = None
         rx.close()
+        if enc is not None and hasattr(enc, "close"):
+            enc.close()
     _checked(gc)
-    if rank == 0 and not gc.get("egress_payload_bitwise", True):
-        raise SystemExit("bench.py: the egress payload does not decode to the model")
+
+
+def egress_check(plan, world, rank, model, payload, idx, expected):
+    """The egress payload against the device model and the host restatement (every rank gets the
+    verdict): rank 0 decodes it with cloudpickle.loads; each rank's digests of its owned ranges
+    (and rank 0's of the tails) must match the same ranges of the payload, and the sampled
+    elements must equal the host restatement bitwise."""
+    import hashlib
+    flat = model.detach().reshape(-1)
+
+    def dig(t):
+        return hashlib.blake2b(t.contiguous().view(torch.uint8).cpu().numpy(), digest_size=16).hexdigest()
+    mine = [(s.lo, s.hi, dig(flat[s.lo:s.hi])) for s in plan.subs if s.hi > s.lo and (not s.tail or rank == 0)]
+    allr = gather_objects(world, mine)
+    res = None
+    if rank == 0:
+        import cloudpickle
+        got = cloudpickle.loads(bytes(payload))["weights"]["model"].reshape(-1)
+        bad_ranges = sum(1 for r in allr for lo, hi, d in r if dig(got[lo:hi]) != d)
+        gb = got[torch.as_tensor(idx)].numpy().view(np.uint32)
+        eb = np.asarray(expected, dtype=np.float32).view(np.uint32)
+        res = {"egress_payload_bytes": len(payload), "egress_ranges_checked": sum(len(r) for r in allr),
+               "egress_range_mismatches": bad_ranges, "egress_sample_mismatches": int(np.count_nonzero(gb != eb))}
+        res["egress_payload_bitwise"] = bad_ranges == 0 and res["egress_sample_mismatches"] == 0
+    return gather_objects(world, res)[0]
 
 
 def time_attribution(world, k_ms, ms_per_step, gather_timing):
@@ -1954,6 +2004,9 @@ def bench_e2e(args, n, P, dev):
         "kernel_ms_per_step": ks["avg_s"] * ks["launches"] / args.steps * 1e3,
         "roofline": {"bound": "pcie", "achieved": achieved, "peak": probe["h2d_aggregate_GBps"], "unit": "GB/s",
                      "frac": achieved / probe["h2d_aggregate_GBps"], "bytes_per_step": {"h2d": h2d, "d2h": d2h},
+                     "spec_GBps": PCIE_SPEC_GBS, "frac_of_spec": achieved / PCIE_SPEC_GBS,
+                     "note": "peak = this process's pinned-copy probe (one SDMA copy); a kernel streaming "
+                             "pinned memory, or copies from a registered segment, can read a few % above it",
                      "probe": probe},
         "launcher": launcher(1),
     }), flush=True)

@@ -681,7 +681,9 @@ __device__ __forceinline__ void adapt_vec_bf16(const float (&avg)[8], const floa
         } else if constexpr (VARIANT == FLAME_FEDYOGI) {
             const f2 t = bf16_rnd2(splat2(omb2) * d2);
             const f2 x = bf16_rnd2(vo - d2);
-            vn = bf16_rnd2(vo - bf16_rnd2(t * f2{sign_f(x.x), sign_f(x.y)}));
+            // t * sign(x) needs no rounding of its own: t is bf16 and the sign +-1 or +0, so the
+            // product is +-t or +-0 exactly (a NaN stays a NaN; its payload bits are not pinned)
+            vn = bf16_rnd2(vo - t * f2{sign_f(x.x), sign_f(x.y)});
         } else {
             vn = bf16_rnd2(vo + d2);
         }

@@ -149,6 +149,35 @@ class _SkeletonPickler(_pickler_base()):
         return sup(obj) if sup is not None else NotImplemented
 
 
+def _layout(message: Any, mark: bytes):
+    """The payload of ``message`` as ``([(offset, bytes | tensor)], total bytes)``: the pickle's
+    own bytes, and each tensor's raw bytes at a 64-byte aligned offset (its storage stream head
+    right before it).  A pure function of the message's structure and ``mark``."""
+    tensors: List[torch.Tensor] = []
+    f = io.BytesIO()
+    _SkeletonPickler(f, tensors, mark).dump(message)
+    skel = f.getvalue()
+    # the placeholders, in order: SHORT_BINBYTES 16 <mark i> -> the storage's whole stream,
+    # its raw bytes 64-byte aligned in the payload (so a device tensor lands by one aligned DMA)
+    pieces, pos, off = [], 0, 0
+    for i, t in enumerate(tensors):
+        ph = b"C\x10" + mark + i.to_bytes(6, "little")
+        j = skel.find(ph, pos)
+        if j < 0:
+            raise RuntimeError("flame_amd.egress: placeholder not found in the skeleton")
+        pieces.append((off, skel[pos:j]))
+        off += j - pos
+        nb = t.numel() * t.element_size()
+        head = _aligned_head(t.dtype, t.numel(), nb, off)
+        pieces.append((off, head))
+        off += len(head)
+        pieces.append((off, t))
+        off += nb
+        pos = j + len(ph)
+    pieces.append((off, skel[pos:]))
+    return pieces, off + len(skel) - pos
+
+
 class MessageEncoder:
     """Encodes flame messages whose tensors (device or host) go straight into one pinned payload
     buffer.  ``encode`` returns a read-only ``memoryview`` of that buffer, valid until the next
@@ -171,39 +200,14 @@ class MessageEncoder:
         return buf
 
     def encode(self, message: Any) -> memoryview:
-        tensors: List[torch.Tensor] = []
-        f = io.BytesIO()
         # a fresh random mark per message: no bytes of the message itself can pass for a placeholder
-        mark = os.urandom(_MARK_LEN)
-        _SkeletonPickler(f, tensors, mark).dump(message)
-        skel = f.getvalue()
-        # the placeholders, in order: SHORT_BINBYTES 16 <mark i> -> the storage's whole stream,
-        # its raw bytes 64-byte aligned in the payload (so a device tensor lands by one aligned DMA)
-        pieces, pos, off = [], 0, 0
-        for i, t in enumerate(tensors):
-            ph = b"C\x10" + mark + i.to_bytes(6, "little")
-            j = skel.find(ph, pos)
-            if j < 0:
-                raise RuntimeError("flame_amd.egress: placeholder not found in the skeleton")
-            pieces.append(skel[pos:j])
-            off += j - pos
-            nb = t.numel() * t.element_size()
-            head = _aligned_head(t.dtype, t.numel(), nb, off)
-            pieces.append(head)
-            off += len(head)
-            pieces.append(t)
-            off += nb
-            pos = j + len(ph)
-        pieces.append(skel[pos:])
-        total = off + len(skel) - pos
+        pieces, total = _layout(message, os.urandom(_MARK_LEN))
         buf = self._buffer(total)
         out = buf.numpy()
-        off = 0
         copies = set()          # devices whose streams carry D2H copies into the buffer
-        for pc in pieces:
+        for off, pc in pieces:
             if isinstance(pc, bytes):
                 out[off:off + len(pc)] = np.frombuffer(pc, dtype=np.uint8)
-                off += len(pc)
                 continue
             nb = pc.numel() * pc.element_size()
             if nb:
@@ -214,10 +218,8 @@ class MessageEncoder:
                     copies.add(src.device)
                 else:
                     dst.copy_(src)
-            off += nb
         for d in copies:        # the payload is complete when encode returns
             torch.cuda.current_stream(d).synchronize()
-        assert off == total
         return memoryview(out[:total]).toreadonly()
 
     def encode_bytes(self, message: Any) -> bytes:
@@ -234,3 +236,127 @@ def dumps(message: Any) -> bytes:
     if _default is None:
         _default = MessageEncoder(ring=1, pin=os.environ.get("FLAME_AMD_EGRESS_PIN", "1") != "0")
     return _default.encode_bytes(message)
+
+
+class ShardedEgress:
+    """The model message of a parameter-sharded aggregator, written into ONE host payload by every
+    rank at once (the other side of ``DeviceUpdateCache(shard=plan)``'s ingest).
+
+    Each rank D2Hs only ITS ranges of the model -- the plan's owned pieces of every key; rank 0 also
+    the replicated key tails and the pickle's own bytes -- over its own PCIe link, straight into a
+    POSIX shared-memory segment that every rank has mapped and page-locked; after a barrier rank 0
+    holds the complete payload (``encode`` returns it there, ``None`` elsewhere), byte-for-byte what
+    :class:`MessageEncoder` builds.  With ``ShardedOptimizer(gather=False)`` the model never crosses
+    xGMI: at N GPUs the egress is N links' D2H of 1/N of the model each instead of one link's D2H of
+    all of it behind an all-gather (``syncfl/top_aggregator.py:184-215`` sends the model from host
+    memory anyway).
+
+    ``message`` must be the same structure on every rank; tensors that are values of
+    ``message["weights"]`` under the plan's keys are written by range, any other tensor whole by
+    rank 0.  The placeholder mark is drawn from a seed rank 0 broadcasts once (every rank builds the
+    same layout without exchanging it per message)."""
+
+    def __init__(self, plan, name: str, group=None):
+        import torch.distributed as dist
+        self.plan, self.name, self.group = plan, name, group
+        self.dist = dist if (dist.is_available() and dist.is_initialized()) else None
+        self.rank = self.dist.get_rank(group) if self.dist else 0
+        self.world = self.dist.get_world_size(group) if self.dist else 1
+        seed = [os.urandom(16) if self.rank == 0 else None]
+        if self.dist and self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            self.dist.broadcast_object_list(seed, src=src, group=group)
+        self._seed, self._seq = seed[0], 0
+        self._seg = self._reg = None
+        self._size = 0
+
+    def _barrier(self):
+        if self.dist and self.world > 1:
+            self.dist.barrier(group=self.group)
+
+    def _segment(self, total: int) -> None:
+        if self._seg is not None and self._size >= total:
+            return
+        self.close()
+        from multiprocessing import shared_memory
+        from .ingest import RegisteredBuffer
+        size = -(-max(total, 1) // (1 << 20)) * (1 << 20)
+        nm = f"{self.name}-{size}"
+        seg = None
+        if self.rank == 0:
+            try:                                  # a stale segment of a crashed run
+                old = shared_memory.SharedMemory(nm)
+                old.close()
+                old.unlink()
+            except FileNotFoundError:
+                pass
+            seg = shared_memory.SharedMemory(nm, create=True, size=size)
+        self._barrier()
+        if seg is None:
+            seg = shared_memory.SharedMemory(nm)
+            try:                                  # rank 0 owns (and unlinks) the segment
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(seg._name, "shared_memory")  # noqa: SLF001
+            except Exception:  # noqa: BLE001
+                pass
+        self._reg = RegisteredBuffer(seg.buf) if torch.cuda.is_available() else None
+        self._seg, self._size = seg, size
+
+    def encode(self, message: Any):
+        import hashlib
+        self._seq += 1
+        mark = hashlib.blake2b(self._seed + self._seq.to_bytes(8, "little"), digest_size=_MARK_LEN).digest()
+        pieces, total = _layout(message, mark)
+        self._segment(total)
+        buf = torch.frombuffer(self._seg.buf, dtype=torch.uint8)
+        out = buf.numpy()
+        weights = message.get("weights") if isinstance(message, dict) else None
+        by_id = {id(v): k for k, v in weights.items() if k in self.plan.numel} if isinstance(weights, dict) else {}
+        devices = set()
+
+        def put(off, src):
+            nb = src.numel() * src.element_size()
+            if nb:
+                dst = buf[off:off + nb].view(src.dtype)
+                dst.copy_(src.reshape(-1), non_blocking=src.is_cuda)
+                if src.is_cuda:
+                    devices.add(src.device)
+        for off, pc in pieces:
+            if isinstance(pc, bytes):
+                if self.rank == 0:
+                    out[off:off + len(pc)] = np.frombuffer(pc, dtype=np.uint8)
+                continue
+            key = by_id.get(id(pc))
+            flat = pc.detach().reshape(-1)
+            if key is None:
+                if self.rank == 0:
+                    put(off, flat)
+                continue
+            s = flat.element_size()
+            for sub in self.plan.subs:
+                if sub.key == key and sub.hi > sub.lo and (not sub.tail or self.rank == 0):
+                    put(off + sub.lo * s, flat[sub.lo:sub.hi])
+        for d in devices:
+            torch.cuda.current_stream(d).synchronize()
+        self._barrier()                           # every rank's ranges are in the payload
+        if self.rank != 0:
+            return None
+        return memoryview(out[:total]).toreadonly()
+
+    def close(self) -> None:
+        if self._seg is None:
+            return
+        if self._reg is not None:
+            self._reg.close()
+        self._reg = None
+        seg, self._seg, self._size = self._seg, None, 0
+        self._barrier()                           # nobody maps it any more
+        try:
+            seg.close()
+        except BufferError:
+            pass
+        if self.rank == 0:
+            try:
+                seg.unlink()
+            except FileNotFoundError:
+                pass

@@ -598,8 +598,13 @@ class ShardedOptimizer:
 
     def __init__(self, inner, group=None, device: Optional[torch.device] = None, accumulate_only: bool = False,
                  *, waves: Optional[bool] = None, fracs=DEFAULT_FRACS, align: int = ALIGN_ELEMS,
-                 plan: Optional[ShardPlan] = None):
+                 plan: Optional[ShardPlan] = None, gather: bool = True):
         self.inner = inner
+        # gather=False (FedAvg / FedProx): no all-gathers -- each rank's base_weights is current on its
+        # owned ranges (and the replicated tails) only, one launch over them; for a caller whose next
+        # use of the model is host-side, e.g. flame_amd.egress.ShardedEgress writing every rank's
+        # ranges straight into one host payload over each rank's own PCIe link
+        self.gather = gather
         self.comm = _Comm(group)
         self.device = device
         self.accumulate_only = accumulate_only
@@ -648,6 +653,19 @@ class ShardedOptimizer:
                 return self._last_full
             return self._remember(res, self._gather_all(res, local, gat))
         records = _drain(cache, plan)
+        if not self.gather:
+            # one do() over all local names (no waves: they exist to overlap the gathers); the
+            # wrapped optimizer must write in place, as FedAvg / FedProx do (fedavg.py:74,87)
+            res = self.inner.do(local, _Replay(records), total=total, version=version, **kwargs)
+            if res is None:
+                return None
+            try:
+                gat.check_inplace(res, local)
+            except RuntimeError as e:
+                raise NotImplementedError(f"ShardedOptimizer(gather=False) needs an in-place optimizer "
+                                          f"(FedAvg / FedProx): {e}") from e
+            work.writeback()
+            return base_weights
         if _stateless(self.inner) and self.waves is not False:
             # flame_amd FedAvg / FedProx: one do(), one launch per wave (pointer rows built once),
             # each wave's in-place all-gather queued right behind its launch

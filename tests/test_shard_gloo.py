@@ -372,3 +372,61 @@ def test_sharded_paths_gloo_world8():
     _run(_fedavg_worker, world=8)
     _run(_opt_worker, world=8)
     _run(_hier_worker, world=8)
+
+
+def _egress_worker(rank, world, port, q):
+    """ShardedOptimizer(gather=False) + ShardedEgress: no all-gather; every rank writes only its
+    ranges (rank 0 also the tails and the pickle's bytes) into one shared payload, which decodes --
+    through the trainers' cloudpickle.loads -- to exactly the single-process FedAvg result."""
+    dist = _init(rank, world, port)
+    try:
+        import cloudpickle
+        from oracle import oracle as O
+        import scenarios as S
+        from flame_amd.egress import ShardedEgress
+        g = torch.Generator().manual_seed(11)
+        shapes = {k: v for k, v in FEDAVG_SHAPES.items() if k != "mask"}
+        base = _model(g, shapes, 1.0)
+        opt = shard.ShardedOptimizer(O.OracleFedAvg(), device=torch.device("cpu"), align=8, gather=False)
+        eg = None
+        ok = True
+        before = sum(shard.GATHER_STATS.values())
+        mine = {k: v.clone() for k, v in base.items()}
+        ref = {k: v.clone() for k, v in base.items()}
+        for r in range(3):
+            n = 7
+            clients = [_model(g, shapes, 1e-2) for _ in range(n)]
+            counts = torch.randint(1, 1000, (n,), generator=g).tolist()
+            ca, cb = S.SortedCache(), S.SortedCache()
+            for i in range(n):
+                ca[f"{i:02d}"] = S.TR({k: v.clone() for k, v in clients[i].items()}, counts[i])
+                cb[f"{i:02d}"] = S.TR({k: v.clone() for k, v in clients[i].items()}, counts[i])
+            out = opt.do(mine, ca, total=sum(counts))
+            ok = ok and out is mine
+            O.OracleFedAvg().do(ref, cb, total=sum(counts))
+            if eg is None:
+                eg = ShardedEgress(opt.plan, f"flametestegress{port}")
+            payload = eg.encode({"weights": mine, "round": r})
+            if rank == 0:
+                msg = cloudpickle.loads(bytes(payload))
+                ok = ok and msg["round"] == r and all(_eq(msg["weights"][k], ref[k]) for k in ref)
+            else:
+                ok = ok and payload is None
+            # the model's non-owned ranges were never exchanged (rank-local state differs)
+            if world > 1 and rank == 1:
+                big = max(shapes, key=lambda k: torch.Size(shapes[k][0]).numel())
+                ok = ok and not _eq(mine[big], ref[big])
+        ok = ok and sum(shard.GATHER_STATS.values()) == before
+        eg.close()
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_egress_without_gathers(world):
+    _run(_egress_worker, world=world)

@@ -52,9 +52,12 @@ STEPS = {
        for m in ("zerocopy", "copy", "pageable", "shm", "shm_reference", "eager", "shard", "shm_shard", "wire",
                  "wire_reference")},
     # the N-GPU end-to-end line rehearsed with gloo ranks sharing the box's one GPU
-    **{f"e2e_shm_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--e2e",
-                                  "--e2e-mode", "shm", "--clients", "{clients}", "--params", "{params}"])
-       for n in (2, 8)},
+    **{f"e2e_shm_gloo{n}{suf}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--e2e",
+                                       "--e2e-mode", "shm", "--e2e-egress", eg, "--clients", "{clients}", "--params",
+                                       "{params}"])
+       for n in (2, 8) for suf, eg in (("", "sharded"), ("_gathered", "gathered"))},
+    **{f"e2e_shm_shard{suf}": (400, [PY, "bench.py", "--e2e", "--e2e-mode", "shm_shard", "--e2e-egress", eg])
+       for suf, eg in (("_sharded_egress", "sharded"), ("_gathered", "gathered"))},
     **{f"sharded_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--clients",
                                   "{clients}", "--params", "{params}"]) for n in (2, 8)},
     **{f"hier_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--workload",
