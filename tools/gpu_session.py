@@ -63,6 +63,13 @@ STEPS = {
     **{f"hier_gloo{n}": (600, ["env", "FLAME_BENCH_BACKEND=gloo", PY, "bench.py", "--gpus", str(n), "--workload",
                                "hier_fedbuff", "--clients", "256", "--params", "{params}"]) for n in (2,)},
     "force_shard": (300, [PY, "bench.py", "--force-shard"]),
+    # plain bench lines of the secondary paths (DESIGN §0's second table)
+    **{f"line_{w}": (300, [PY, "bench.py", "--cpu-clients", "0", *a]) for w, a in {
+        "c2": ["--clients", "256", "--params", "1000000", "--steps", "50", "--warmup", "5"],
+        "fedavg_eager": ["--workload", "fedavg_eager", "--steps", "10", "--warmup", "3"],
+        "scaffold": ["--workload", "scaffold", "--steps", "10", "--warmup", "3"],
+        "hier_fetched": ["--workload", "hier_fedbuff", "--hier-middles", "fetched", "--steps", "10", "--warmup", "3"],
+        "hier_sync": ["--workload", "hier_fedbuff", "--hier-mode", "sync", "--steps", "10", "--warmup", "3"]}.items()},
     # the evidence collection (round 5's gpu_r05_prof.sh): each default path's bench line under
     # rocprofv3 --kernel-trace --stats (the SAME process's kernel summary) ...
     **{f"prof_{w}": (400, ["rocprof:", PY, "bench.py", *a]) for w, a in {
