@@ -599,3 +599,62 @@ def test_sharded_fedbuff_scale_add_waves_world1():
             outs.append(model)
         for k in tmpl:
             assert _eq(outs[0][k], outs[1][k]), (fuse, k)
+
+
+# ---------------------------------------------------------------- sharded egress, two ranks
+def _egress_worker(rank, world, port, q):
+    """ShardedOptimizer(gather=False) on the HIP FedAvg + ShardedEgress: updates arrive as decoded
+    channel payloads (views at arbitrary alignment) into DeviceUpdateCache(shard=plan); no gather
+    runs; every rank D2Hs its ranges into the one shared, registered egress segment; rank 0's
+    payload decodes (cloudpickle.loads) to one process's FedAvg result, bitwise, over two rounds."""
+    dist = _init(rank, world, port)
+    try:
+        import cloudpickle
+        from flame_amd import ingest, shard
+        from flame_amd.egress import ShardedEgress
+        from flame_amd.ingest import DeviceUpdateCache
+        from flame_amd.optimizers import optimizer_provider
+        g = torch.Generator().manual_seed(61)
+        tmpl = _model(g, 300_007)
+        del tmpl["z"]
+        opt = shard.ShardedOptimizer(optimizer_provider.get("fedavg"), device=torch.device(DEV), gather=False)
+        opt.set_layout(tmpl)
+        cache = DeviceUpdateCache(device=DEV, placement="slab", capacity=8, shard=opt.plan)
+        mine = {k: v.clone().to(DEV) for k, v in tmpl.items()}
+        ref = {k: v.clone().to(DEV) for k, v in tmpl.items()}
+        single = optimizer_provider.get("fedavg")
+        eg = ShardedEgress(opt.plan, f"flamegpuegress{port}")
+        before = sum(shard.GATHER_STATS.values())
+        ok = True
+        for r in range(2):
+            n = 5
+            ups = [_update(g, tmpl, i) for i in range(n)]
+            counts = [10 + 7 * i for i in range(n)]
+            payloads = [cloudpickle.dumps({"weights": u, "dataset_size": c}) for u, c in zip(ups, counts)]
+            rc = S.SortedCache()
+            for i, b in enumerate(payloads):
+                msg = ingest.decode(b)
+                cache[f"{i:02d}"] = S.TR(msg["weights"], msg["dataset_size"])
+                rc[f"{i:02d}"] = S.TR({k: v.to(DEV) for k, v in ups[i].items()}, counts[i])
+            out = opt.do(mine, cache, total=sum(counts))
+            ok = ok and out is mine
+            single.do(ref, rc, total=sum(counts))
+            payload = eg.encode({"weights": mine, "round": r})
+            if rank == 0:
+                got = cloudpickle.loads(bytes(payload))
+                ok = ok and got["round"] == r and all(_eq(got["weights"][k], ref[k]) for k in ref)
+            else:
+                ok = ok and payload is None
+        ok = ok and sum(shard.GATHER_STATS.values()) == before
+        eg.close()
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_egress_two_ranks_one_gpu():
+    _two_ranks(_egress_worker)

@@ -30,6 +30,8 @@ STEPS = {
                           "--timeout-method", "thread", "--durations", "5"]),
     "pytest_slab": (300, [PY, "-u", "-m", "pytest", "tests/test_gpu_slab_write.py", "tests/test_gpu_shm.py", "-m", "gpu",
                           "-x", "-q", "--timeout", "200", "--timeout-method", "thread"]),
+    "pytest_shard": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_shard.py", "-m", "gpu", "-x", "-q", "--timeout",
+                           "200", "--timeout-method", "thread"]),
     "pytest_chain": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_eager_fedopt_chain.py",
                            "tests/test_gpu_fastmath.py", "tests/test_gpu_dtype_matrix.py", "-m", "gpu", "-x", "-q",
                            "--timeout", "200", "--timeout-method", "thread"]),
