@@ -184,6 +184,21 @@ constexpr int kChainLds = FLAME_T_CHAIN_LDS;           // dynamic LDS per fp32 w
 #define FLAME_T_BF16_PACKED 1
 #endif
 constexpr bool kBf16Packed = FLAME_T_BF16_PACKED != 0;
+// the same for fp16 (two elements per fp32 instruction, a pair rounded by one v_cvt_pk_f16_f32 and
+// widened back by two converts); 0 = the generic per-element path
+#ifndef FLAME_T_F16_PACKED
+#define FLAME_T_F16_PACKED 1
+#endif
+constexpr bool kF16Packed = FLAME_T_F16_PACKED != 0;
+// fp16 root: v_sqrt_f32 under the fp16 rounding (1; tools/fp_probe.py finds it equal to the
+// correctly rounded root's on every finite fp16 v, and the step's denominator on every v for every
+// tau it draws, profiles/r06k_fp_probe.log) or flame_fm::sqrt_rn, then the rounding (0).  The
+// quotient stays flame_fm::div_rn: num * v_rcp_f32 differs on 10,528 fp16 pairs (ties of subnormal
+// results, where an fp16 quotient has too few bits for the midpoint argument)
+#ifndef FLAME_T_F16_HWROOT
+#define FLAME_T_F16_HWROOT 1
+#endif
+constexpr bool kF16HwRoot = FLAME_T_F16_HWROOT != 0;
 // FedYogi's (1 - beta_2) d^2 * sign(v - d^2): sign as one ordered compare + bit-select (1) or as
 // torch writes it, two compares and an integer difference (0); same bits
 #ifndef FLAME_T_YOGI_SIGN
@@ -253,6 +268,15 @@ __device__ __forceinline__ uint16_t f32_to_f16_bits(float x) {
     uint16_t h;
     __builtin_memcpy(&h, &v, 2);
     return h;
+}
+// A pair RNE-rounded to fp16 and widened back: ONE v_cvt_pk_f16_f32 (the same conversion as
+// f16_round's v_cvt_f16_f32, per half; inline asm, so the backend cannot fold a product into a
+// single-rounding v_fma_mix) and two exact widening converts (the high half by SDWA).  Never
+// applied to a transcendental's result (see bf16_rnd1).
+__device__ __forceinline__ f2 f16_rnd2(f2 x) {
+    uint32_t p;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(x.x), "v"(x.y));
+    return f2{f16_to_f32(static_cast<uint16_t>(p)), f16_to_f32(static_cast<uint16_t>(p >> 16))};
 }
 
 // ---------------------------------------------------------------- dtype traits
@@ -662,8 +686,23 @@ __device__ __forceinline__ void adapt_elem(float avg, float cur, float& m, float
 // fp32 value (v_sqrt_f32 flushes a subnormal v to a zero root, but den = RN(RN(root) + tau) = tau
 // for both roots there).  tools/fp_probe.py checks the root on every normal bf16 v, den on every
 // admitted v and the quotient on every admitted (num, den) pair.
-template <int VARIANT>
-__device__ __forceinline__ void adapt_vec_bf16(const float (&avg)[8], const float (&cur)[8], bool cur_is_avg,
+// fp16: the same sequence with f16_rnd2 (one v_cvt_pk_f16_f32 + two widening converts per pair).
+// An fp16 significand has 11 bits, too many for the midpoint argument; the exhaustive fp16 probe
+// of tools/fp_probe.py finds v_sqrt_f32 exact under the fp16 rounding on every finite v (so the
+// root takes it, FLAME_T_F16_HWROOT) but num * v_rcp_f32 not (the quotient stays div_rn).
+// The pair rounding (inline asm: never on a transcendental's result) and the single rounding the
+// compiler builds (safe on one) of the 16-bit dtypes.
+template <int DT> __device__ __forceinline__ f2 hrnd2(f2 x) {
+    if constexpr (DT == FLAME_BF16) return bf16_rnd2(x);
+    else return f16_rnd2(x);
+}
+template <int DT> __device__ __forceinline__ float hrnd1(float x) {
+    if constexpr (DT == FLAME_BF16) return bf16_round(x);
+    else return f16_round(x);
+}
+
+template <int DT, int VARIANT>
+__device__ __forceinline__ void adapt_vec_half(const float (&avg)[8], const float (&cur)[8], bool cur_is_avg,
                                                float (&m)[8], float (&v)[8], float (&cur_out)[8], float b1,
                                                float omb1, float b2, float omb2, float eta, float tau) {
     float c[8], num[8];
@@ -671,23 +710,23 @@ __device__ __forceinline__ void adapt_vec_bf16(const float (&avg)[8], const floa
     for (int p = 0; p < 8; p += 2) {
         const f2 a = {avg[p], avg[p + 1]};
         const f2 cc = cur_is_avg ? a : f2{cur[p], cur[p + 1]};
-        const f2 d = bf16_rnd2(a - cc);
-        const f2 mn = bf16_rnd2(bf16_rnd2(splat2(b1) * f2{m[p], m[p + 1]}) + bf16_rnd2(splat2(omb1) * d));
-        const f2 d2 = bf16_rnd2(d * d);
+        const f2 d = hrnd2<DT>(a - cc);
+        const f2 mn = hrnd2<DT>(hrnd2<DT>(splat2(b1) * f2{m[p], m[p + 1]}) + hrnd2<DT>(splat2(omb1) * d));
+        const f2 d2 = hrnd2<DT>(d * d);
         const f2 vo = {v[p], v[p + 1]};
         f2 vn;
         if constexpr (VARIANT == FLAME_FEDADAM) {
-            vn = bf16_rnd2(bf16_rnd2(splat2(b2) * vo) + bf16_rnd2(splat2(omb2) * d2));
+            vn = hrnd2<DT>(hrnd2<DT>(splat2(b2) * vo) + hrnd2<DT>(splat2(omb2) * d2));
         } else if constexpr (VARIANT == FLAME_FEDYOGI) {
-            const f2 t = bf16_rnd2(splat2(omb2) * d2);
-            const f2 x = bf16_rnd2(vo - d2);
-            // t * sign(x) needs no rounding of its own: t is bf16 and the sign +-1 or +0, so the
-            // product is +-t or +-0 exactly (a NaN stays a NaN; its payload bits are not pinned)
-            vn = bf16_rnd2(vo - t * f2{sign_f(x.x), sign_f(x.y)});
+            const f2 t = hrnd2<DT>(splat2(omb2) * d2);
+            const f2 x = hrnd2<DT>(vo - d2);
+            // t * sign(x) needs no rounding of its own: t is in the dtype and the sign +-1 or +0, so
+            // the product is +-t or +-0 exactly (a NaN stays a NaN; its payload bits are not pinned)
+            vn = hrnd2<DT>(vo - t * f2{sign_f(x.x), sign_f(x.y)});
         } else {
-            vn = bf16_rnd2(vo + d2);
+            vn = hrnd2<DT>(vo + d2);
         }
-        const f2 nm = bf16_rnd2(splat2(eta) * mn);
+        const f2 nm = hrnd2<DT>(splat2(eta) * mn);
         c[p] = cc.x;
         c[p + 1] = cc.y;
         m[p] = mn.x;
@@ -699,21 +738,32 @@ __device__ __forceinline__ void adapt_vec_bf16(const float (&avg)[8], const floa
     }
     const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & flame_fm::admits<8>(v, num);
     if (ok) {
+        constexpr bool hw_root = DT == FLAME_BF16 || kF16HwRoot;
+        constexpr bool hw_div = DT == FLAME_BF16;
 #pragma unroll
         for (int p = 0; p < 8; p += 2) {
-            // the roots' rounding through bf16_round: a v_sqrt_f32 result never feeds inline asm
-            const f2 s = {bf16_round(__builtin_amdgcn_sqrtf(v[p])), bf16_round(__builtin_amdgcn_sqrtf(v[p + 1]))};
-            const f2 den = bf16_rnd2(s + splat2(tau));
-            const f2 q = bf16_rnd2(f2{num[p], num[p + 1]} * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)});
-            const f2 co = bf16_rnd2(f2{c[p], c[p + 1]} + q);
+            // the roots' rounding through hrnd1: a v_sqrt_f32 / v_rsq_f32 result never feeds inline asm
+            f2 s, q;
+            if constexpr (hw_root) {
+                s = f2{hrnd1<DT>(__builtin_amdgcn_sqrtf(v[p])), hrnd1<DT>(__builtin_amdgcn_sqrtf(v[p + 1]))};
+            } else {
+                s = f2{hrnd1<DT>(flame_fm::sqrt_rn(v[p])), hrnd1<DT>(flame_fm::sqrt_rn(v[p + 1]))};
+            }
+            const f2 den = hrnd2<DT>(s + splat2(tau));
+            if constexpr (hw_div) {
+                q = hrnd2<DT>(f2{num[p], num[p + 1]} * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)});
+            } else {
+                q = hrnd2<DT>(f2{flame_fm::div_rn(num[p], den.x), flame_fm::div_rn(num[p + 1], den.y)});
+            }
+            const f2 co = hrnd2<DT>(f2{c[p], c[p + 1]} + q);
             cur_out[p] = co.x;
             cur_out[p + 1] = co.y;
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float den = bf16_round(__fadd_rn(bf16_round(__builtin_sqrtf(v[j])), tau));
-            cur_out[j] = bf16_round(__fadd_rn(c[j], bf16_round(__fdiv_rn(num[j], den))));
+            const float den = hrnd1<DT>(__fadd_rn(hrnd1<DT>(__builtin_sqrtf(v[j])), tau));
+            cur_out[j] = hrnd1<DT>(__fadd_rn(c[j], hrnd1<DT>(__fdiv_rn(num[j], den))));
         }
     }
 }
@@ -722,8 +772,8 @@ template <int DT, int VARIANT, int EPT>
 __device__ __forceinline__ void adapt_vec(const float (&avg)[EPT], const float (&cur)[EPT], bool cur_is_avg,
                                           float (&m)[EPT], float (&v)[EPT], float (&cur_out)[EPT], float b1,
                                           float omb1, float b2, float omb2, float eta, float tau) {
-    if constexpr (DT == FLAME_BF16 && EPT == 8 && kBf16Packed) {
-        adapt_vec_bf16<VARIANT>(avg, cur, cur_is_avg, m, v, cur_out, b1, omb1, b2, omb2, eta, tau);
+    if constexpr (EPT == 8 && ((DT == FLAME_BF16 && kBf16Packed) || (DT == FLAME_F16 && kF16Packed))) {
+        adapt_vec_half<DT, VARIANT>(avg, cur, cur_is_avg, m, v, cur_out, b1, omb1, b2, omb2, eta, tau);
         return;
     }
     float c[EPT], num[EPT];
@@ -988,11 +1038,11 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
         load_t(reinterpret_cast<const T*>(reinterpret_cast<const char*>(cp[i]) + coff), x, true);
     };
     auto arrive = [&](const T (&x)[EPT], float r, bool ends) {
-        if constexpr (DT == FLAME_BF16 && kBf16Packed) {   // X::add(b, X::tmp(x, r)) on pairs
+        if constexpr ((DT == FLAME_BF16 && kBf16Packed) || (DT == FLAME_F16 && kF16Packed)) {
 #pragma unroll
-            for (int j = 0; j < EPT; j += 2) {
-                const f2 t = bf16_rnd2(f2{bf16_to_f32(x[j]), bf16_to_f32(x[j + 1])} * splat2(r));
-                const f2 s = bf16_rnd2(f2{b[j], b[j + 1]} + t);
+            for (int j = 0; j < EPT; j += 2) {     // X::add(b, X::tmp(x, r)) on pairs
+                const f2 t = hrnd2<DT>(f2{X::ld(x[j]), X::ld(x[j + 1])} * splat2(r));
+                const f2 s = hrnd2<DT>(f2{b[j], b[j + 1]} + t);
                 b[j] = s.x;
                 b[j + 1] = s.y;
             }

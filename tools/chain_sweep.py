@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--arrivals", type=int, default=64)
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"])
     ap.add_argument("--variant", default="fedadam",
                     help="fedadam | fedyogi | fedadagrad, or a comma list: every variant runs with every library, "
                          "interleaved in this one process (bitwise checked across libraries per variant)")
@@ -50,7 +50,7 @@ def main():
     names = [(lb, v) for v in variants for lb in lib_names]
     dev = torch.device("cuda", 0)
     K, P = a.arrivals, a.params
-    tdt = torch.float32 if a.dtype == "f32" else torch.bfloat16
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
     slab = UpdateSlab({"model": torch.empty(P, dtype=tdt)}, capacity=K, device=dev)
     tmp = torch.empty(P, dtype=tdt, device=dev)
     arrivals = []

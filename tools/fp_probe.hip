@@ -183,9 +183,84 @@ __global__ void bf16_den_kernel(uint32_t lo, uint32_t hi, float tau, unsigned lo
     if (__float_as_uint(got) != __float_as_uint(want)) report(out, i << 16, __float_as_uint(tau), __float_as_uint(got), __float_as_uint(want));
 }
 
+// fp16 (adapt_vec_half, FLAME_T_F16_PACKED / FLAME_T_F16_HWROOT): the pair rounding
+// v_cvt_pk_f16_f32 against v_cvt_f16_f32 per element on every fp32 pattern, and the hardware root
+// / quotient under the fp16 rounding against the correctly rounded ones, on every fp16 operand.
+__device__ __forceinline__ uint16_t h16(float x) {
+    asm volatile("" : "+v"(x));
+    _Float16 v = static_cast<_Float16>(x);
+    uint16_t b;
+    __builtin_memcpy(&b, &v, 2);
+    return b;
+}
+__device__ __forceinline__ float f16v(uint32_t bits) {
+    const uint16_t b = static_cast<uint16_t>(bits);
+    _Float16 v;
+    __builtin_memcpy(&v, &b, 2);
+    return static_cast<float>(v);
+}
+__device__ __forceinline__ float rh(float x) { return f16v(h16(x)); }
+
+__global__ void f16_pack_kernel(uint64_t lo, uint64_t hi, unsigned long long* out) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = lo + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < hi; i += stride) {
+        const float x = __uint_as_float(static_cast<uint32_t>(i));
+        const float y = __uint_as_float(static_cast<uint32_t>(i) ^ 0x5a5a5a5au);
+        uint32_t p;
+        asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(x), "v"(y));
+        const uint32_t want = static_cast<uint32_t>(h16(x)) | (static_cast<uint32_t>(h16(y)) << 16);
+        if (p != want) report(out, static_cast<uint32_t>(i), __float_as_uint(y), p, want);
+    }
+}
+
+__global__ void f16_sqrt_kernel(uint32_t lo, uint32_t hi, float tau, unsigned long long* out) {
+    const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const float v = f16v(i);
+    float want, got;
+    if (tau == 0.f) {
+        want = rh(flame_fm::sqrt_rn(v));
+        got = rh(__builtin_amdgcn_sqrtf(v));
+    } else {
+        want = rh(__fadd_rn(rh(flame_fm::sqrt_rn(v)), tau));
+        got = rh(__fadd_rn(rh(__builtin_amdgcn_sqrtf(v)), tau));
+    }
+    if (__float_as_uint(got) != __float_as_uint(want)) report(out, i, __float_as_uint(tau), __float_as_uint(got), __float_as_uint(want));
+}
+
+__global__ void f16_div_kernel(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+    const uint32_t nb = blockIdx.y * 256u + threadIdx.x;
+    const float num = f16v(nb);
+    if (!(__builtin_fabsf(num) <= 65504.f)) return;              // every finite fp16 num is admitted
+    for (uint32_t d = dlo + blockIdx.x; d < dhi; d += gridDim.x) {
+        const float den = f16v(d);
+        const float want = rh(flame_fm::div_rn(num, den));
+        const float got = rh(__fmul_rn(num, __builtin_amdgcn_rcpf(den)));
+        if (__float_as_uint(got) != __float_as_uint(want)) report(out, nb, d, __float_as_uint(got), __float_as_uint(want));
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int probe_f16_pack(uint64_t lo, uint64_t hi, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    f16_pack_kernel<<<16384, 256>>>(lo, hi, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_f16_sqrt(uint32_t lo, uint32_t hi, float tau, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    if (hi > lo) f16_sqrt_kernel<<<(hi - lo + 255) / 256, 256>>>(lo, hi, tau, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_f16_div(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    f16_div_kernel<<<dim3(512, 256), 256>>>(dlo, dhi, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
 
 int probe_bf16_den(uint32_t lo, uint32_t hi, float tau, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));

@@ -94,6 +94,19 @@ def main():
          L.probe_bf16_sqrt(0x6681, 0x10000, p), False)
     show("bf16: RN_bf16(num * v_rcp_f32(den)) == RN_bf16(num / den) on every admitted bf16 num x every bf16 den "
          "in [2^-20, 2^40]", L.probe_bf16_div(0x3580, 0x5381, p), True)
+    # fp16 (adapt_vec_half): the pair rounding on every fp32 pattern; the hardware root / quotient
+    L.probe_f16_sqrt.argtypes = [u32, u32, ctypes.c_float, ctypes.c_void_p]
+    L.probe_f16_div.argtypes = [u32, u32, ctypes.c_void_p]
+    show("fp16: v_cvt_pk_f16_f32 == v_cvt_f16_f32 per half on every fp32 pattern (paired with x ^ 0x5a5a5a5a)",
+         L.probe_f16_pack(u64(0), u64(1 << 32), p), True)
+    show("fp16 (FLAME_T_F16_HWROOT, shipped): RN_f16(v_sqrt_f32(v)) == RN_f16(sqrt_rn(v)) on every non-negative "
+         "finite fp16 v", L.probe_f16_sqrt(0, 0x7C00, 0.0, p), True)
+    for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0):
+        th = float(torch.tensor(tau, dtype=torch.float16))
+        show(f"fp16 (shipped): RN(RN(v_sqrt_f32(v)) + {th:g}) == RN(RN(sqrt_rn(v)) + {th:g}) on every non-negative "
+             f"finite fp16 v", L.probe_f16_sqrt(0, 0x7C00, th, p), True)
+    show("fp16 (not shipped: the quotient stays div_rn): RN_f16(num * v_rcp_f32(den)) == RN_f16(div_rn(num, den)) on "
+         "every finite fp16 num x every fp16 den in [2^-20, 65504]", L.probe_f16_div(0x0010, 0x7C00, p), False)
     # adapt_vec admits v below 2^-96 too: it only reaches sqrt(v) + tau (tau >= 2^-20)
     L.probe_den.argtypes = [u64, u64, ctypes.c_float, ctypes.c_void_p]
     for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):

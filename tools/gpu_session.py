@@ -43,12 +43,12 @@ STEPS = {
     # eager FedOPT chain, 64 x 25M: the shipped library against the round-5 step, one process, bitwise
     **{f"chain_{v}_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", dt, "--rounds", "6",
                                   "--libs", f"flame_amd/libflame_amd.so,{AB}"])
-       for v in ("adam", "yogi", "adagrad") for dt in ("f32", "bf16")},
+       for v in ("adam", "yogi", "adagrad") for dt in ("f32", "bf16", "f16")},
     **{f"eager_{v}": (300, [PY, "bench.py", "--workload", f"fed{v}_eager"]) for v in ("adam", "yogi", "adagrad")},
     # the three variants interleaved in ONE process (Yogi within 3 % of Adam)
     **{f"chain_variants_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", "fedadam,fedyogi,fedadagrad",
                                       "--dtype", dt, "--rounds", "6", "--libs", "flame_amd/libflame_amd.so"])
-       for dt in ("f32", "bf16")},
+       for dt in ("f32", "bf16", "f16")},
     # end-to-end rows, 64 clients x 25M fp32 from host memory back to host memory
     **{f"e2e_{m}": (400, [PY, "bench.py", "--e2e", "--e2e-mode", m])
        for m in ("zerocopy", "copy", "pageable", "shm", "shm_reference", "eager", "shard", "shm_shard", "wire",
