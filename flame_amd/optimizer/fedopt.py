@@ -341,10 +341,14 @@ class FedOPT(FedAvg):
             self._run_chain(ch, cuts, keys, hyper)
 
     def _run_chain(self, ch, cuts, keys, hyper):
-        """One flame_fedopt_chain launch per stretch of queued calls.  The optimizer's state
-        (m_t / v_t, current_weights, agg_weights) moves to a stretch's results only once its
-        launch has returned; if one fails, the state stays at the last stretch that ran and every
-        result of the stretches that did not run re-raises the failure when read."""
+        """One flame_fedopt_chain launch per stretch of queued calls (one per dtype group; every
+        group is planned and uploaded before the first launches, engine.fedopt_chain_).  The
+        optimizer's state (m_t / v_t, current_weights, agg_weights) moves to a stretch's results
+        only once its launches have returned; if a stretch fails before any of its launches ran,
+        the state stays at the last stretch that ran and every result of the stretches that did
+        not run re-raises the failure when read.  If a later dtype group's launch fails after an
+        earlier group's ran (the exception carries ``flame_partial``), base / m / v no longer
+        agree across keys: the optimizer is poisoned and every later call raises."""
         cur, aliased, zero, start = ch.current, ch.aliased, ch.state_zero, 0
         try:
             for cut in cuts:
