@@ -430,3 +430,38 @@ def _egress_worker(rank, world, port, q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_egress_without_gathers(world):
     _run(_egress_worker, world=world)
+
+
+def _one(w):
+    import scenarios as S
+    c = S.SortedCache()
+    c["a"] = S.TR({"w": w}, 3)
+    return c
+
+
+def test_gather_false_refuses_an_optimizer_that_does_not_write_in_place():
+    """ShardedOptimizer(gather=False) leaves the model sharded in the caller's tensors, so the
+    wrapped do() must write in place (FedAvg / FedProx); FedOPT's new current_weights refuse."""
+    from oracle import oracle as O
+    import scenarios as S
+    g = torch.Generator().manual_seed(3)
+    model = {"w": torch.randn(4096, generator=g)}
+    opt = shard.ShardedOptimizer(O.OracleFedAvg(), device=torch.device("cpu"), align=8, gather=False)
+    c = S.SortedCache()
+    upd = torch.randn(4096, generator=g)
+    c["a"] = S.TR({"w": upd.clone()}, 3)
+    expect = O.OracleFedAvg().do({"w": model["w"].clone()}, _one(upd), total=3)
+    out = opt.do(model, c, total=3)
+    assert out is model
+    assert torch.equal(out["w"], expect["w"])
+
+    class NotInPlace:
+        def do(self, base, cache, *, total=0, version=0, **kw):
+            for k in list(cache.iterkeys()):
+                cache.pop(k)
+            return {k: v.clone() for k, v in base.items()}
+    bad = shard.ShardedOptimizer(NotInPlace(), device=torch.device("cpu"), align=8, gather=False)
+    c2 = S.SortedCache()
+    c2["a"] = S.TR({"w": torch.randn(4096, generator=g)}, 3)
+    with pytest.raises(NotImplementedError, match="in-place optimizer"):
+        bad.do({"w": torch.randn(4096, generator=g)}, c2, total=3)
