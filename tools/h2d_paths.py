@@ -65,26 +65,31 @@ def main():
             got = dst.view(tiles, stride)[:, :T].reshape(-1).cpu()
             return bool(torch.equal(got, ref))
 
+        def paths_at(off):
+            pinned, shm = pinned_all[off:off + nbytes], shm_all[off:off + nbytes]
+            paths = {
+                f"+{off} B pinned: contiguous copy_ (hipMemcpyAsync)":
+                    (lambda: flat.copy_(pinned, non_blocking=True), None),
+                f"+{off} B shm registered: contiguous copy_": (lambda: flat.copy_(shm, non_blocking=True), None),
+            }
+            for nm, src in ((f"+{off} B pinned", pinned), (f"+{off} B shm registered", shm)):
+                tb = table(src.data_ptr())
+                paths[f"{nm}: flame_slab_write_2d (hipMemcpy2DAsync, 4 KiB rows)"] = (
+                    lambda tb=tb: N.check(L.flame_slab_write_2d(tb.ctypes.data, 1, st.cuda_stream)), check_tiled)
+                tbd = table(engine.host_device_pointer(src.data_ptr()))
+                paths[f"{nm}: flame_slab_write kernel over the device-mapped pointer"] = (
+                    lambda tbd=tbd: N.check(L.flame_slab_write(tbd.ctypes.data, 1, st.cuda_stream)), check_tiled)
+            return pinned, paths
+
         for off in [int(x) for x in a.offsets.split(",")]:
-          pinned, shm = pinned_all[off:off + nbytes], shm_all[off:off + nbytes]
-          paths = {}
-          paths[f"+{off} B pinned: contiguous copy_ (hipMemcpyAsync)"] = (
-              lambda pinned=pinned: flat.copy_(pinned, non_blocking=True), None)
-          paths[f"+{off} B shm registered: contiguous copy_"] = (lambda shm=shm: flat.copy_(shm, non_blocking=True), None)
-          for nm, src in ((f"+{off} B pinned", pinned), (f"+{off} B shm registered", shm)):
-            tb = table(src.data_ptr())
-            paths[f"{nm}: flame_slab_write_2d (hipMemcpy2DAsync, 4 KiB rows)"] = (
-                lambda tb=tb: N.check(L.flame_slab_write_2d(tb.ctypes.data, 1, st.cuda_stream)), check_tiled)
-            tbd = table(engine.host_device_pointer(src.data_ptr()))
-            paths[f"{nm}: flame_slab_write kernel over the device-mapped pointer"] = (
-                lambda tbd=tbd: N.check(L.flame_slab_write(tbd.ctypes.data, 1, st.cuda_stream)), check_tiled)
-          for nm, (fn, chk) in paths.items():
-            dst.zero_()
-            r = run(fn)
-            ok = chk(pinned) if chk else bool(torch.equal(flat.cpu(), pinned))
-            print(f"{nm:72s} {r:7.2f} GB/s  {'ok' if ok else 'MISMATCH'}", flush=True)
+            pinned, paths = paths_at(off)
+            for nm, (fn, chk) in paths.items():
+                dst.zero_()
+                r = run(fn)
+                ok = chk(pinned) if chk else bool(torch.equal(flat.cpu(), pinned))
+                print(f"{nm:72s} {r:7.2f} GB/s  {'ok' if ok else 'MISMATCH'}", flush=True)
         reg.close()
-        del shm_all, shm
+        del shm_all, paths
     finally:
         seg.close()
         seg.unlink()
