@@ -255,9 +255,9 @@ class UpdateSlab:
         # (profiles/r06e2_h2d_paths.log, r06e_ingest_diag.log)
         mapped = []
         if host_rows:
-            by_ptr = {t.data_ptr(): t for t in keep if not t.is_cuda}
+            by_src = {(t.data_ptr(), t.numel() * t.element_size()): t for t in keep if not t.is_cuda}
             for r in [r for r in host_rows if r[0] % 4]:
-                t = by_ptr.get(r[0])
+                t = by_src.get((r[0], r[2]))       # the row's source: same address, same bytes
                 if t is None or not t.is_pinned():
                     continue
                 host_rows.remove(r)
