@@ -2,7 +2,6 @@
 (FedAvg / FedOPT rounds, config 5's async and sync hierarchy in bf16) equal the oracle's
 do() restatements on the same counter-generated inputs, bitwise; the sampled indices
 cover every wave, every rank boundary and the replicated tails."""
-import math
 
 import numpy as np
 import torch

@@ -14,9 +14,7 @@ Also here: FedOPT at >= 8,192 chunks in bf16 / f16 (one chunk per workgroup: the
 multi-chunk grid is fp32-only), and the eager caller's aliased FedOPT step
 (FLAME_SEG_CUR_IS_AVG) through the fused kernel.
 """
-import math
 
-import numpy as np
 import pytest
 import torch
 

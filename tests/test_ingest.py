@@ -1,6 +1,5 @@
 """Zero-copy restricted decoding of flame channel payloads (flame_amd.ingest)."""
 import enum
-import io
 import os
 import pickle
 import time

@@ -13,7 +13,6 @@ import sys
 
 import cloudpickle
 import numpy as np
-import pytest
 import torch
 
 from flame_amd import ingest

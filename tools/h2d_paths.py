@@ -7,7 +7,6 @@ contiguous one for the plain copy), median of --reps, GB/s; the destination is c
     python tools/h2d_paths.py [--mb 100] [--reps 5]
 """
 import argparse
-import ctypes
 import os
 import statistics
 import sys
