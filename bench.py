@@ -23,6 +23,8 @@ Other workloads (DESIGN.md numbers; the driver's bench line is the default):
   --workload fedavg_eager [--eager-defer on|off]
                                           the eager top aggregator's round: one do() per
                                           arrival, batched into one launch (on) or not
+  --workload fedadam_eager --dtype bf16   the eager FedOPT round on a 16-bit model (bf16 / f16:
+                                          every op rounded to the dtype as torch-CPU does)
   --e2e                                   host-resident updates: H2D + kernel + D2H
 """
 import argparse
@@ -78,6 +80,10 @@ def parse():
     ap.add_argument("--workload", default="fedavg",
                     choices=["fedavg", "fedadam", "fedyogi", "fedadagrad", "fedbuff", "hier_fedbuff", "feddyn",
                              "scaffold", "fedavg_eager", "fedadam_eager", "fedyogi_eager", "fedadagrad_eager"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"],
+                    help="fed*_eager: the model's and the updates' dtype (the eager FedOPT chain ships for all "
+                         "three, each op rounded to the dtype as torch-CPU does); every other workload runs its "
+                         "BASELINE config's dtype")
     ap.add_argument("--eager-defer", default="on", choices=["on", "off"],
                     help="fed*_eager / --e2e-mode eager: FedAvg / FedOPT(defer=True) queues the one-arrival do() "
                          "calls and reduces them in one launch (on) or launches per arrival (off)")
@@ -280,6 +286,53 @@ def cpu_baseline_fedopt(sort, host_row, n, P, base0, counts, n_cpu, rounds):
     }
 
 
+def cpu_baseline_eager(sort, host_row, n, P, base0, counts, n_cpu, rounds):
+    """The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) as the reference
+    runs it, on host cores: per arrival, FedAvg.do of that one arrival into the round's base with
+    the running total (fedavg.py:84-104) and, for FedOPT, the adaptive step (fedopt.py:102-129)
+    with m / v / current carried from arrival to arrival -- every op in the model's dtype, as
+    torch-CPU rounds it.  A bounded sample: the round's first ``n_cpu`` arrivals, one untimed
+    round first (it allocates m / v), the median of ``rounds``; value = arrivals x P / time."""
+    from oracle import torch_cpu
+    cores, env = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    fedopt = sort != "fedavg"
+    n_cpu = max(1, min(n_cpu, n))
+    ups = [{"model": host_row(i)} for i in range(n_cpu)]
+    cts = [int(c) for c in counts[:n_cpu]]
+    state = {"cur": {"model": base0.clone()}, "m": {}, "v": {}}
+
+    def one_round():
+        agg, running = {"model": base0.clone()}, 0
+        for w, c in zip(ups, cts):
+            running += c
+            torch_cpu.fedavg_round(agg, [w], [c], running)
+            if fedopt:
+                state["cur"] = torch_cpu.fedopt_adapt(sort, agg, state["cur"], state["m"], state["v"],
+                                                      0.9, 0.99, 1e-2, 1e-3)
+    try:
+        one_round()
+        ts = []
+        for _ in range(rounds):
+            t0 = time.perf_counter()
+            one_round()
+            ts.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    t = statistics.median(ts)
+    ops = "FedAvg.do per arrival (fedavg.py:84-104)" + (
+        f" + the {sort} step (fedopt.py:102-129)" if fedopt else "")
+    return {
+        "value": n_cpu * P / t, "unit": "client-params/s", "cores": cores, "kind": "port",
+        "sample": f"reference eager round op sequence: {ops}, torch CPU (oracle/torch_cpu.py), the first "
+                  f"{n_cpu} of the {n} arrivals x {P} {str(base0.dtype).replace('torch.', '')} params, median "
+                  f"of {rounds} rounds ({t:.3f} s per {n_cpu} arrivals), {cores} threads on {_cpu_model()}; "
+                  f"value = sampled arrival-params / time (the op sequence costs the same per arrival)",
+        "host": env,
+    }
+
+
 def cpu_baseline_hier(rows, P, stale, rnd, rounds):
     """One middle aggregator of config 5 on host cores: FedBuff per arrival
     (fedbuff.py:94-96,136-157) + scale_add (:122-127) + the middle's delta
@@ -448,22 +501,25 @@ def read_ceiling(buf: torch.Tensor, reps: int = 5, regions=()):
     return max(res.values()), res
 
 
-def make_clients(args, n, P, rank, dev):
-    """n synthetic fp32 client updates of P params in HBM (tiled slab or one row each)."""
+def make_clients(args, n, P, rank, dev, dtype=torch.float32):
+    """n synthetic client updates of P params in HBM (tiled slab or one row each): the fp32
+    synthetic values, rounded to ``dtype`` for a 16-bit model."""
     from flame_amd import engine
+    tmp = torch.empty(P, dtype=torch.float32, device=dev)
     if args.layout == "slab":
         from flame_amd.slab import UpdateSlab
-        store = UpdateSlab({"model": torch.empty(P, dtype=torch.float32)}, capacity=n, device=dev)
-        tmp = torch.empty(P, dtype=torch.float32, device=dev)
+        store = UpdateSlab({"model": torch.empty(P, dtype=dtype)}, capacity=n, device=dev)
         client_w = []
         for i in range(n):
             engine.synth_fill_(tmp, args.seed, 1 + i + rank * 100_000, 0, 1e-2)
-            client_w.append(store.put({"model": tmp}))        # tiled slot views, held for the run
+            client_w.append(store.put({"model": tmp.to(dtype)}))   # tiled slot views, held for the run
         del tmp
-        return client_w, store.storage[torch.float32], (lambda i: store.read(i, "model").cpu())
-    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
+        return client_w, store.storage[dtype], (lambda i: store.read(i, "model").cpu())
+    slab = torch.empty((n, P), dtype=dtype, device=dev)
     for i in range(n):
-        engine.synth_fill_(slab[i], args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+        engine.synth_fill_(tmp, args.seed, 1 + i + rank * 100_000, 0, 1e-2)
+        slab[i].copy_(tmp)
+    del tmp
     return [{"model": slab[i]} for i in range(n)], slab, (lambda i: slab[i].cpu())
 
 
@@ -550,9 +606,10 @@ def traffic_lookup(path, **match):
 
 
 _TRAFFIC_DEFAULTS = {"layout": "row"}
+DTYPES = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
 
 
-def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
+def bench_eager(args, world, rank, dev, n, P, client_w, base, counts, host_row=None):
     """The eager top aggregator's round (eager_syncfl/top_aggregator.py:36-90) on
     device-resident updates: base = deepcopy(weights), then one do() per arrival with the
     running total; the role keeps the returned object (read once, at the round's end).
@@ -574,6 +631,9 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     kname = ("flame_fedopt_chain" if defer else "flame_fedopt_reduce_adapt") if fedopt else "flame_agg_reduce"
     keys = [f"{i:05d}" for i in range(n)]
     state = {"weights": {"model": base}}
+    base0 = base.cpu() if (rank == 0 and args.cpu_clients > 0 and host_row is not None) else None
+    dt = args.dtype
+    isz = base.element_size()
 
     def step():
         bw = {"model": state["weights"]["model"].clone()}      # deepcopy(self.weights)
@@ -601,13 +661,16 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
     if rank == 0:
         k_time = ks["avg_s"] * ks["launches"] / args.steps
         k_bytes = ks["bytes_per_launch"] * ks["launches"] / args.steps
+        # that variant's (and dtype's) entry or None
         traffic, traffic_source = traffic_lookup(args.traffic, kernel=kname, clients=n, params=P,
-                                                 workload=args.workload)   # that variant's entry or None
+                                                 workload=args.workload + ("" if dt == "f32" else f"_{dt}"))
+        cpu = (cpu_baseline_eager(sort, host_row, n, P, base0, counts, min(args.cpu_clients, 8), args.cpu_rounds)
+               if base0 is not None else None)
         print(json.dumps({
             "metric": f"aggregated params/sec (device-resident), eager {sort} round",
             "value": n * P / (elapsed / args.steps), "unit": "client-params/s", "n_gpus": world,
-            "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f32", "settle": SETTLE,
-            "config": {"workload": f"{args.workload}: {n} arrivals (one do() each, running total) x {P} fp32 "
+            "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": dt, "settle": SETTLE,
+            "config": {"workload": f"{args.workload}: {n} arrivals (one do() each, running total) x {P} {dt} "
                                    f"params, {args.layout} layout, defer {args.eager_defer}"},
             "first_round": first,
             "roofline": {"bound": "hbm", "achieved": k_bytes / k_time / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -615,12 +678,17 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts):
                          "kernel_ms_per_step": k_time * 1e3, "launches_per_step": ks["launches"] / args.steps,
                          "algorithmic_bytes_per_step": k_bytes, "traffic_per_launch": traffic,
                          "traffic_source": traffic_source,
-                         "bytes_per_client_param": k_bytes / (n * P * 4),
+                         "bytes_per_client_param": k_bytes / (n * P * isz),
                          **({"note": "flame_fedopt_chain runs every arrival's adaptive step in sequence per "
-                                     "element (~20 VALU instructions each with the fast correctly rounded "
+                                     "element (~18 VALU instructions each with the fast correctly rounded "
                                      "sqrt and divide, 2 of them quarter-rate transcendentals): VALU and "
                                      "HBM both ~70-75 % busy (DESIGN.md §4)"}
+                            if fedopt and defer and dt == "f32" else
+                            {"note": f"flame_fedopt_chain, {dt}: every op rounded to {dt} as torch-CPU does, on "
+                                     f"packed fp32 (~29 VALU instructions per bf16 element-step, DESIGN.md §4): "
+                                     f"VALU-bound, 2 bytes per element"}
                             if fedopt and defer else {})},
+            "cpu_baseline": cpu,
         }), flush=True)
 
 
@@ -682,6 +750,9 @@ def main():
         raise SystemExit(arg)
     if what == "spawn":
         raise SystemExit(spawn_ranks(arg, sys.argv[1:]))
+    if args.dtype != "f32" and (args.e2e or not args.workload.endswith("_eager")):
+        raise SystemExit(f"--dtype {args.dtype}: the fed*_eager workloads only (--workload {args.workload} runs its "
+                         f"BASELINE config's dtype)")
     world, rank, local = setup_dist(args.force_shard)
     dev = torch.device("cuda", local)
     from flame_amd import _native, engine, synth
@@ -706,14 +777,17 @@ def main():
         return bench_e2e(args, n, P, dev)
     if (world > 1 or args.force_shard) and args.workload in ("fedavg", "fedadam", "fedyogi", "fedadagrad"):
         return bench_sharded(args, world, rank, dev, n, P)
-    client_w, slab_buf, host_row = make_clients(args, n, P, rank, dev)
+    dtype = DTYPES[args.dtype]
+    client_w, slab_buf, host_row = make_clients(args, n, P, rank, dev, dtype)
     base = torch.empty(P, dtype=torch.float32, device=dev)
     engine.synth_fill_(base, args.seed, rank * 100_000, 0, 1.0)
+    base = base.to(dtype)
     counts = synth.counts(args.seed, n)
     if args.workload in ("feddyn", "scaffold"):
         return bench_feddyn_scaffold(args, world, rank, dev, n, P, client_w, base, counts)
     if args.workload.endswith("_eager"):
-        return bench_eager(args, world, rank, dev, n, P, client_w, base, counts)
+        return bench_eager(args, world, rank, dev, n, P, client_w, base, counts,
+                           host_row if world == 1 else None)
     base0 = base.clone() if (rank == 0 and world == 1 and args.cpu_clients > 0) else None
     total = int(counts.sum())
     keys = [f"{i:05d}" for i in range(n)]

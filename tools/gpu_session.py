@@ -85,6 +85,13 @@ STEPS = {
         "fedyogi_eager": ["--workload", "fedyogi_eager", "--steps", "10", "--warmup", "3"],
         "fedadagrad_eager": ["--workload", "fedadagrad_eager", "--steps", "10", "--warmup", "3"],
         "feddyn": ["--workload", "feddyn", "--steps", "6", "--warmup", "2", "--cpu-clients", "0"]}.items()},
+    # the eager lines at 16-bit dtypes (bench.py --dtype): line + CPU baseline under rocprofv3 stats
+    **{f"prof_{v}_eager_{dt}": (400, ["rocprof:", PY, "bench.py", "--workload", f"fed{v}_eager", "--dtype", dt,
+                                      "--steps", "10", "--warmup", "3"])
+       for v in ("adam", "yogi", "adagrad") for dt in ("bf16", "f16")},
+    **{f"pmc_{v}_eager_{dt}_{c}": (120, ["pmc:", c, "fedopt_chain", PY, "bench.py", "--workload", f"fed{v}_eager",
+                                         "--dtype", dt, "--steps", "3", "--warmup", "1", "--cpu-clients", "0"])
+       for v in ("adam", "yogi", "adagrad") for dt in ("bf16", "f16") for c in ("FETCH_SIZE", "WRITE_SIZE")},
     "prof_chain_bf16": (300, ["rocprof:", PY, "tools/chain_sweep.py", "--variant", "fedadam,fedyogi,fedadagrad",
                               "--dtype", "bf16", "--rounds", "3", "--libs", "flame_amd/libflame_amd.so"]),
     # ... and PMC passes, one counter per run (no trace domains), for the HBM traffic of a kernel
