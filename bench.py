@@ -685,8 +685,8 @@ def bench_eager(args, world, rank, dev, n, P, client_w, base, counts, host_row=N
                                      "HBM both ~70-75 % busy (DESIGN.md §4)"}
                             if fedopt and defer and dt == "f32" else
                             {"note": f"flame_fedopt_chain, {dt}: every op rounded to {dt} as torch-CPU does, on "
-                                     f"packed fp32 (~29 VALU instructions per bf16 element-step, DESIGN.md §4): "
-                                     f"VALU-bound, 2 bytes per element"}
+                                     f"packed fp32 with one-instruction roundings (DESIGN.md §4): VALU-bound at "
+                                     f"2 bytes per element"}
                             if fedopt and defer else {})},
             "cpu_baseline": cpu,
         }), flush=True)

@@ -80,4 +80,22 @@ __device__ __forceinline__ bool admits(const float (&v)[N], const float (&num)[N
     return (vhi <= 0x66800000u) & (nhi <= 0x1p100f) & (nlo >= (0x15000000u << 1) - 2u);
 }
 
+// The parts of admits the 16-bit steps need (adapt_vec_half in fedagg.hip): v in [+0, 2^78]
+// (the root's and den's range), and a finite |num| <= 2^100 (a NaN passes: its quotient is NaN on
+// either path) for fp16's div_rn, whose other bound, |num| >= 2^-85 or +-0, every fp16 value meets.
+template <int N>
+__device__ __forceinline__ bool admits_v(const float (&v)[N]) {
+    uint32_t vhi = 0u;
+#pragma unroll
+    for (int j = 0; j < N; ++j) vhi = max(vhi, __float_as_uint(v[j]));
+    return vhi <= 0x66800000u;
+}
+template <int N>
+__device__ __forceinline__ bool admits_finite(const float (&num)[N]) {
+    float nhi = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) nhi = fmaxf(nhi, __builtin_fabsf(num[j]));
+    return nhi <= 0x1p100f;
+}
+
 }  // namespace flame_fm

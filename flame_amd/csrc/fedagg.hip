@@ -192,13 +192,23 @@ constexpr bool kBf16Packed = FLAME_T_BF16_PACKED != 0;
 constexpr bool kF16Packed = FLAME_T_F16_PACKED != 0;
 // fp16 root: v_sqrt_f32 under the fp16 rounding (1; tools/fp_probe.py finds it equal to the
 // correctly rounded root's on every finite fp16 v, and the step's denominator on every v for every
-// tau it draws, profiles/r06k_fp_probe.log) or flame_fm::sqrt_rn, then the rounding (0).  The
+// tau it draws, profiles/r06l_fp_probe.log) or flame_fm::sqrt_rn, then the rounding (0).  The
 // quotient stays flame_fm::div_rn: num * v_rcp_f32 differs on 10,528 fp16 pairs (ties of subnormal
 // results, where an fp16 quotient has too few bits for the midpoint argument)
 #ifndef FLAME_T_F16_HWROOT
 #define FLAME_T_F16_HWROOT 1
 #endif
 constexpr bool kF16HwRoot = FLAME_T_F16_HWROOT != 0;
+// the 16-bit steps' fast-path admission (adapt_vec_half): 1 = only what their root / quotient need --
+// v in [+0, 2^78] for both, and for fp16 (flame_fm::div_rn) a finite |num|: every nonzero finite
+// fp16 value is >= 2^-24, inside div_rn's range, and the bf16 quotient num * v_rcp_f32 matches on
+// every non-NaN bf16 num (tools/fp_probe.py) -- so a bf16 m decaying through [2^-133, 2^-85]
+// (a weight whose average stops moving) no longer sends its lane down the general path;
+// 0 = the fp32 step's admission (flame_fm::admits), for A/B builds
+#ifndef FLAME_T_HALF_ADMIT
+#define FLAME_T_HALF_ADMIT 1
+#endif
+constexpr bool kHalfAdmit = FLAME_T_HALF_ADMIT != 0;
 // FedYogi's (1 - beta_2) d^2 * sign(v - d^2): sign as one ordered compare + bit-select (1) or as
 // torch writes it, two compares and an integer difference (0); same bits
 #ifndef FLAME_T_YOGI_SIGN
@@ -736,7 +746,11 @@ __device__ __forceinline__ void adapt_vec_half(const float (&avg)[8], const floa
         num[p] = nm.x;
         num[p + 1] = nm.y;
     }
-    const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & flame_fm::admits<8>(v, num);
+    bool adm;
+    if constexpr (!kHalfAdmit) adm = flame_fm::admits<8>(v, num);
+    else if constexpr (DT == FLAME_BF16) adm = flame_fm::admits_v<8>(v);
+    else adm = flame_fm::admits_v<8>(v) & flame_fm::admits_finite<8>(num) & (tau <= 0x1p15f);  // den finite in fp16
+    const bool ok = (tau >= 0x1p-20f) & (tau <= 0x1p38f) & adm;
     if (ok) {
         constexpr bool hw_root = DT == FLAME_BF16 || kF16HwRoot;
         constexpr bool hw_div = DT == FLAME_BF16;

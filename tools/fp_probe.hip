@@ -156,13 +156,15 @@ __global__ void bf16_sqrt_kernel(uint32_t lo, uint32_t hi, unsigned long long* o
 }
 
 // ... and of num * v_rcp_f32(den) vs of the correctly rounded quotient, for every bf16 num (hi16 =
-// blockIdx.y * 256 + x) that adapt_vec admits (+-0, 2^-85 <= |num| <= 2^100) and every bf16 den
-// with hi16 in [dlo, dhi) (den = RN(RN(sqrt v) + tau) lies in [2^-20, 2^40] on admitted lanes).
-__global__ void bf16_div_kernel(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+// blockIdx.y * 256 + x) that the fp32 step's admission takes (+-0, 2^-85 <= |num| <= 2^100; all = 0)
+// or every bf16 num but NaN (all = 1: what adapt_vec_half admits, FLAME_T_HALF_ADMIT), and every
+// bf16 den with hi16 in [dlo, dhi) (den = RN(RN(sqrt v) + tau) lies in [2^-20, 2^40] on admitted
+// lanes).
+__global__ void bf16_div_kernel(uint32_t dlo, uint32_t dhi, int all, unsigned long long* out) {
     const uint32_t nb = (blockIdx.y * 256u + threadIdx.x) << 16;
     const float num = __uint_as_float(nb);
     const float an = __builtin_fabsf(num);
-    if (!(an == 0.f || (an >= 0x1p-85f && an <= 0x1p100f))) return;
+    if (all ? __builtin_isnan(num) : !(an == 0.f || (an >= 0x1p-85f && an <= 0x1p100f))) return;
     for (uint32_t d = dlo + blockIdx.x; d < dhi; d += gridDim.x) {
         const float den = __uint_as_float(d << 16);
         const float want = rbf(__fdiv_rn(num, den));
@@ -274,9 +276,9 @@ int probe_bf16_sqrt(uint32_t lo, uint32_t hi, unsigned long long* out) {
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
 
-int probe_bf16_div(uint32_t dlo, uint32_t dhi, unsigned long long* out) {
+int probe_bf16_div(uint32_t dlo, uint32_t dhi, int all, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
-    bf16_div_kernel<<<dim3(512, 256), 256>>>(dlo, dhi, out);
+    bf16_div_kernel<<<dim3(512, 256), 256>>>(dlo, dhi, all, out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
 

@@ -79,7 +79,7 @@ def main():
     # bf16 (adapt_vec_bf16): v_sqrt_f32 / num * v_rcp_f32 under the bf16 rounding, exhaustively
     u32 = ctypes.c_uint32
     L.probe_bf16_sqrt.argtypes = [u32, u32, ctypes.c_void_p]
-    L.probe_bf16_div.argtypes = [u32, u32, ctypes.c_void_p]
+    L.probe_bf16_div.argtypes = [u32, u32, ctypes.c_int, ctypes.c_void_p]
     L.probe_bf16_den.argtypes = [u32, u32, ctypes.c_float, ctypes.c_void_p]
     show("bf16: RN_bf16(v_sqrt_f32(v)) == RN_bf16(sqrt(v)) on bf16 v = +0", L.probe_bf16_sqrt(0, 1, p), True)
     show("bf16: RN_bf16(v_sqrt_f32(v)) == RN_bf16(sqrt(v)) on every normal bf16 v in [2^-126, 2^78]",
@@ -93,7 +93,10 @@ def main():
     show("bf16: v_sqrt_f32 on every other bf16 pattern (negative, > 2^78, inf, NaN; informational)",
          L.probe_bf16_sqrt(0x6681, 0x10000, p), False)
     show("bf16: RN_bf16(num * v_rcp_f32(den)) == RN_bf16(num / den) on every admitted bf16 num x every bf16 den "
-         "in [2^-20, 2^40]", L.probe_bf16_div(0x3580, 0x5381, p), True)
+         "in [2^-20, 2^40]", L.probe_bf16_div(0x3580, 0x5381, 0, p), True)
+    show("bf16 (FLAME_T_HALF_ADMIT, shipped): the same on every bf16 num but NaN (zeros, the tiny and subnormal "
+         "nums a decaying m reaches, huge, inf) x every bf16 den in [2^-20, 2^40]",
+         L.probe_bf16_div(0x3580, 0x5381, 1, p), True)
     # fp16 (adapt_vec_half): the pair rounding on every fp32 pattern; the hardware root / quotient
     L.probe_f16_sqrt.argtypes = [u32, u32, ctypes.c_float, ctypes.c_void_p]
     L.probe_f16_div.argtypes = [u32, u32, ctypes.c_void_p]

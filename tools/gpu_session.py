@@ -45,6 +45,13 @@ STEPS = {
                                   "--libs", f"flame_amd/libflame_amd.so,{AB}"])
        for v in ("adam", "yogi", "adagrad") for dt in ("f32", "bf16", "f16")},
     **{f"eager_{v}": (300, [PY, "bench.py", "--workload", f"fed{v}_eager"]) for v in ("adam", "yogi", "adagrad")},
+    # the 16-bit steps' admission (FLAME_T_HALF_ADMIT) against the fp32 step's, one process, bitwise, over
+    # enough rounds for stalled weights' m to decay through [2^-133, 2^-85] (bf16)
+    **{f"chain_admit_{v}_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", dt, "--rounds",
+                                       "18", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_admit.so"])
+       for v in ("adam", "yogi", "adagrad") for dt in ("bf16", "f16")},
+    "pytest_half": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_half_admission.py", "-m", "gpu", "-x", "-v",
+                          "--timeout", "200", "--timeout-method", "thread"]),
     # the three variants interleaved in ONE process (Yogi within 3 % of Adam)
     **{f"chain_variants_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", "fedadam,fedyogi,fedadagrad",
                                       "--dtype", dt, "--rounds", "6", "--libs", "flame_amd/libflame_amd.so"])

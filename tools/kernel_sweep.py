@@ -62,9 +62,13 @@ VARIANTS = {
     "lo_wgc16_all": {"FLAME_T_LO_WGC": 16, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
     "lo_wgc32_all": {"FLAME_T_LO_WGC": 32, "FLAME_T_LO_BURST_MAX_CLIENTS": 1 << 30},
     # round 6: the round-5 bf16 FedOPT step / Yogi sign (generic per-element code), for the chain A/B
-    "r05_step": {"FLAME_T_BF16_PACKED": 0, "FLAME_T_YOGI_SIGN": 0},
+    # (the 16-bit steps' per-element code: bf16 and fp16; lib_r05_step.so was built before the fp16
+    # packed step existed, and these defines rebuild the same code)
+    "r05_step": {"FLAME_T_BF16_PACKED": 0, "FLAME_T_YOGI_SIGN": 0, "FLAME_T_F16_PACKED": 0},
     "r05_bf16": {"FLAME_T_BF16_PACKED": 0},
     "r05_yogi": {"FLAME_T_YOGI_SIGN": 0},
+    # the shipped library with the 16-bit steps on the fp32 step's fast-path admission
+    "r06_admit": {"FLAME_T_HALF_ADMIT": 0},
 }
 
 
