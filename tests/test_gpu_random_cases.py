@@ -542,8 +542,8 @@ N_EAGER16 = 20 * SCALE
 def test_random_eager_fedopt_16bit_defer_equals_per_call(case):
     """bf16 / fp16 (and mixed) eager FedOPT rounds: FedOPT(defer=True) -- one flame_fedopt_chain
     launch per dtype per round -- against one fused launch per call, bitwise for base, every
-    round's current, m_t and v_t (the oracle holds these keys to a one-ulp contract, the two
-    GPU paths to each other exactly)."""
+    round's current, m_t and v_t (the oracle tests hold 16-bit keys bitwise to the reference's
+    torch-CPU op sequence; here the two GPU paths are held to each other)."""
     from copy import deepcopy
     from flame_amd.optimizers import optimizer_provider
     rng = np.random.default_rng(13_000 + SEED_OFFSET + case)
