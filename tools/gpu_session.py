@@ -112,7 +112,7 @@ STEPS = {
     **{f"pmc_chain_{dt}_{lb}_{c.split()[0]}": (120, ["pmc:", c, "fedopt_chain", PY, "tools/chain_sweep.py",
                                                      "--variant", "fedadam", "--dtype", dt, "--rounds", "1", "--libs",
                                                      lib])
-       for dt in ("f32", "bf16") for lb, lib in (("r06", "flame_amd/libflame_amd.so"), ("r05", AB))
+       for dt in ("f32", "bf16", "f16") for lb, lib in (("r06", "flame_amd/libflame_amd.so"), ("r05", AB))
        for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU SQ_WAVES")},
 }
 
