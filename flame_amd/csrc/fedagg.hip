@@ -199,6 +199,13 @@ constexpr bool kF16Packed = FLAME_T_F16_PACKED != 0;
 #define FLAME_T_F16_HWROOT 1
 #endif
 constexpr bool kF16HwRoot = FLAME_T_F16_HWROOT != 0;
+// fp16 eager chain (full, aligned chunks): base / current / m / v held as packed fp16 pairs, every
+// fp16-by-fp16 op one v_pk_add_f16 / v_pk_mul_f16, every scalar product two v_fma_mix_f32 and a
+// v_cvt_pk_f16_f32 (1; fedopt_chain_body_f16), or the fp32-register step (0); same bits
+#ifndef FLAME_T_F16_NATIVE
+#define FLAME_T_F16_NATIVE 1
+#endif
+constexpr bool kF16Native = FLAME_T_F16_NATIVE != 0;
 // the 16-bit steps' fast-path admission (adapt_vec_half): 1 = only what their root / quotient need --
 // v in [+0, 2^78] for both, and for fp16 (flame_fm::div_rn) a finite |num|: every nonzero finite
 // fp16 value is >= 2^-24, inside div_rn's range, and the bf16 quotient num * v_rcp_f32 matches on
@@ -287,6 +294,49 @@ __device__ __forceinline__ f2 f16_rnd2(f2 x) {
     uint32_t p;
     asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(x.x), "v"(x.y));
     return f2{f16_to_f32(static_cast<uint16_t>(p)), f16_to_f32(static_cast<uint16_t>(p >> 16))};
+}
+
+// fp16 pairs kept packed (the fp16 eager chain, FLAME_T_F16_NATIVE).  An op on two fp16 values
+// rounded once to fp16 (v_pk_add_f16 / v_pk_mul_f16) equals torch-CPU's op in fp32 rounded to fp16:
+// a product of two 11-bit significands is exact in fp32, and for a sum, square root or quotient
+// fp32's 24 bits are >= 2p + 2 for p = 11, so rounding to fp32 first never changes the fp16
+// rounding (Figueroa's double-rounding theorem).  A Python-scalar operand (beta, eta, a rate) is
+// fp32 (24 bits), so those products go through fp32: smul_h2.
+using h2 = __attribute__((ext_vector_type(2))) _Float16;
+using us2 = __attribute__((ext_vector_type(2))) unsigned short;
+__device__ __forceinline__ h2 h2_of(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t u_of(h2 h) { return __builtin_bit_cast(uint32_t, h); }
+__device__ __forceinline__ f2 widen_h2(uint32_t u) {
+    const h2 h = h2_of(u);
+    return f2{static_cast<float>(h.x), static_cast<float>(h.y)};
+}
+// RN16(RN32(s * x)) of a pair: two v_fma_mix_f32 (a half widened exactly inside the instruction;
+// s * x + neg(0) = s * x + (-0) rounded once is the fp32 product, signed zeros included) and one v_cvt_pk_f16_f32 --
+// instead of two widening converts, a v_pk_mul_f32, the rounding and two more widening converts.
+__device__ __forceinline__ uint32_t smul_h2(float s, uint32_t x) {
+    float lo, hi;
+    uint32_t r;
+    asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(lo) : "s"(s), "v"(x));
+    asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(hi) : "s"(s), "v"(x));
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+// RN16 of an fp32 pair, packed (never on a transcendental's result, see bf16_rnd1)
+__device__ __forceinline__ uint32_t pk_h2(f2 x) {
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(x.x), "v"(x.y));
+    return r;
+}
+// torch.sign of an fp16 pair as FedYogi's t * sign(x) uses it: +-1 for a nonzero x, +0 for +-0.
+// x + 0 turns -0 into +0; x * 65504 * 65504 carries the smallest subnormal (2^-24) past 1 and
+// overflows the rest to inf; the clamp to [-1, 1] keeps +-1 / +0.  A NaN x clamps to +1 (minNum),
+// not to torch's 0 -- but a NaN x = v - d^2 means v or d^2 is a NaN (t * sign is then NaN either
+// way) or v = d^2 = +inf (t = inf: inf * 0 and inf - inf * 1 are both NaN), so v's new value is a
+// NaN on both ways.
+__device__ __forceinline__ h2 sign_h2(h2 x) {
+    const h2 z = x + h2{0, 0};
+    const h2 big = (z * h2{65504, 65504}) * h2{65504, 65504};
+    return __builtin_elementwise_max(__builtin_elementwise_min(big, h2{1, 1}), h2{-1, -1});
 }
 
 // ---------------------------------------------------------------- dtype traits
@@ -1125,6 +1175,135 @@ __device__ __forceinline__ void fedopt_chain_body(const flame_segment& sg, int64
     }
 }
 
+// fedopt_chain_body for an fp16 model on a full, aligned chunk: the same per-arrival accumulate and
+// per-call step (fedopt.py:102-129, each torch op rounded to fp16), with the lane's 8 elements held
+// as 4 packed pairs.  An op whose operands are both fp16 is one packed fp16 instruction (same bits
+// as fp32-then-fp16, see h2 above); a product with a Python scalar is smul_h2; the root and the
+// quotient widen their operands and take v_sqrt_f32 / flame_fm::div_rn as adapt_vec_half does
+// (same admission: v in [+0, 65504] per half, a finite numerator, tau in [2^-20, 2^15]); a lane
+// outside it takes the general sequence per element.
+template <int VARIANT, int CU>
+__device__ __forceinline__ void fedopt_chain_body_f16(const flame_segment& sg, int64_t e0, const uint64_t* __restrict__ cp,
+                                                      int64_t coff, int n_clients, const float* __restrict__ r32,
+                                                      const uint8_t* __restrict__ step_end, unsigned flags, float b1,
+                                                      float omb1, float b2, float omb2, float eta, float tau) {
+    bool aliased = (sg.flags & FLAME_SEG_CUR_IS_AVG) != 0;
+    const bool zero_state = (flags & FLAME_OPT_STATE_ZERO) != 0;
+    const uint16_t* bp = reinterpret_cast<const uint16_t*>(sg.in) + e0;
+    const uint16_t* curp = reinterpret_cast<const uint16_t*>(sg.cur) + e0;
+    uint16_t* mp = reinterpret_cast<uint16_t*>(sg.m) + e0;
+    uint16_t* vp = reinterpret_cast<uint16_t*>(sg.v) + e0;
+    uint32_t b[4], c[4] = {}, m[4] = {}, v[4] = {};
+    auto ld4 = [](const void* p, uint32_t (&x)[4]) {
+        const V16 t = ld_v(p);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = t.w[q];
+    };
+    ld4(bp, b);
+    if (!aliased) ld4(curp, c);
+    if (!zero_state) {
+        ld4(mp, m);
+        ld4(vp, v);
+    }
+    const h2 tau2 = {static_cast<_Float16>(tau), static_cast<_Float16>(tau)};   // tau is fp16-exact
+    const bool tau_ok = (tau >= 0x1p-20f) & (tau <= 0x1p15f);                   // den in [2^-20, 65504]
+    auto adapt = [&]() {
+        f2 num[4];
+        us2 vmax = {0, 0};
+        float nhi = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const h2 d = h2_of(b[p]) - h2_of(c[p]);
+            const h2 mn = h2_of(smul_h2(b1, m[p])) + h2_of(smul_h2(omb1, u_of(d)));
+            const h2 d2 = d * d;
+            const h2 vo = h2_of(v[p]);
+            h2 vn;
+            if constexpr (VARIANT == FLAME_FEDADAM) {
+                vn = h2_of(smul_h2(b2, v[p])) + h2_of(smul_h2(omb2, u_of(d2)));
+            } else if constexpr (VARIANT == FLAME_FEDYOGI) {
+                const h2 t = h2_of(smul_h2(omb2, u_of(d2)));
+                vn = vo - t * sign_h2(vo - d2);      // t * (+-1 or +0) is exact
+            } else {
+                vn = vo + d2;
+            }
+            m[p] = u_of(mn);
+            v[p] = u_of(vn);
+            num[p] = widen_h2(smul_h2(eta, m[p]));
+            vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(us2, v[p]));
+            nhi = fmaxf(nhi, fmaxf(__builtin_fabsf(num[p].x), __builtin_fabsf(num[p].y)));
+        }
+        // v's halves in [+0, 65504] (a sign, an inf or a NaN is above 0x7bff); a NaN numerator
+        // passes (its quotient is a NaN on either path)
+        const bool ok = tau_ok & (max(vmax.x, vmax.y) <= 0x7bffu) & (nhi <= 0x1p100f);
+        if (ok) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const f2 vv = widen_h2(v[p]);
+                const h2 s = {static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.x)),
+                              static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.y))};
+                const f2 den = widen_h2(u_of(s + tau2));
+                const f2 q = {flame_fm::div_rn(num[p].x, den.x), flame_fm::div_rn(num[p].y, den.y)};
+                c[p] = u_of(h2_of(c[p]) + h2_of(pk_h2(q)));
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const f2 vv = widen_h2(v[p]), cc = widen_h2(c[p]);
+                float co[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float den = f16_round(__fadd_rn(f16_round(__builtin_sqrtf(vv[h])), tau));
+                    co[h] = f16_round(__fadd_rn(cc[h], f16_round(__fdiv_rn(num[p][h], den))));
+                }
+                c[p] = u_of(h2{static_cast<_Float16>(co[0]), static_cast<_Float16>(co[1])});   // exact
+            }
+        }
+    };
+    auto arrive = [&](const V16& x, float r, bool ends) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) b[p] = u_of(h2_of(b[p]) + h2_of(smul_h2(r, x.w[p])));
+        if (ends) {     // uniform: one do() call ends here
+            if (__builtin_expect(aliased, 0)) {   // the first step after the passthrough: current IS base
+#pragma unroll
+                for (int p = 0; p < 4; ++p) c[p] = b[p];
+                aliased = false;
+            }
+            adapt();
+        }
+    };
+    auto client = [&](int i) { return reinterpret_cast<const char*>(cp[i]) + coff; };
+    int i = 0;
+    for (; i + CU <= n_clients; i += CU) {
+        V16 x[CU];
+        float rr[CU];
+        bool ends[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) x[u] = ld_nt(client(i + u));
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            rr[u] = r32[i + u];
+            ends[u] = step_ends(step_end, i + u);
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) arrive(x[u], rr[u], ends[u]);
+    }
+    for (; i < n_clients; ++i) arrive(ld_nt(client(i)), r32[i], step_ends(step_end, i));
+    if (aliased) {             // no step closed: current is still the base
+#pragma unroll
+        for (int p = 0; p < 4; ++p) c[p] = b[p];
+    }
+    auto st4 = [](void* p, const uint32_t (&x)[4]) {
+        V16 t;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t.w[q] = x[q];
+        st_v(p, t);
+    };
+    st4(reinterpret_cast<uint16_t*>(sg.out) + e0, b);
+    st4(mp, m);
+    st4(vp, v);
+    st4(reinterpret_cast<uint16_t*>(sg.cur_out) + e0, c);
+}
+
 template <int DT, int VARIANT, int CU>
 __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segment* __restrict__ segs, int n_segs,
                                                               const uint64_t* __restrict__ clients, int n_clients,
@@ -1141,10 +1320,14 @@ __global__ __launch_bounds__(kBlock) void fedopt_chain_kernel(const flame_segmen
     if (e0 >= sg.numel) return;
     const uint64_t* cp = clients + static_cast<int64_t>(s) * n_clients;
     const int64_t coff = client_offset<DT>(sg, chunk);
-    if (c0 + chunk_elems<DT>() <= sg.numel && !(sg.flags & FLAME_SEG_UNALIGNED))    // workgroup-uniform
-        fedopt_chain_body<DT, VARIANT, CU, true>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2,
-                                                 omb2, eta, tau);
-    else
+    if (c0 + chunk_elems<DT>() <= sg.numel && !(sg.flags & FLAME_SEG_UNALIGNED)) {   // workgroup-uniform
+        if constexpr (DT == FLAME_F16 && kF16Native)
+            fedopt_chain_body_f16<VARIANT, CU>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2, omb2,
+                                               eta, tau);
+        else
+            fedopt_chain_body<DT, VARIANT, CU, true>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2,
+                                                     omb2, eta, tau);
+    } else
         fedopt_chain_body<DT, VARIANT, 1, false>(sg, e0, cp, coff, n_clients, r32, step_end, flags, b1, omb1, b2,
                                                  omb2, eta, tau);
 }

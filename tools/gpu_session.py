@@ -50,6 +50,13 @@ STEPS = {
     **{f"chain_admit_{v}_{dt}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", dt, "--rounds",
                                        "18", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_admit.so"])
        for v in ("adam", "yogi", "adagrad") for dt in ("bf16", "f16")},
+    # the fp16 chain on packed halves against the fp32-register step, one process, bitwise
+    **{f"chain_native_{v}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", "f16", "--rounds",
+                                   "8", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_f16.so"])
+       for v in ("adam", "yogi", "adagrad")},
+    "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
+                         "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
+                         "--timeout-method", "thread"]),
     "pytest_half": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_half_admission.py", "-m", "gpu", "-x", "-v",
                           "--timeout", "200", "--timeout-method", "thread"]),
     # the three variants interleaved in ONE process (Yogi within 3 % of Adam)

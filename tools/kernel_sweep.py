@@ -69,6 +69,8 @@ VARIANTS = {
     "r05_yogi": {"FLAME_T_YOGI_SIGN": 0},
     # the shipped library with the 16-bit steps on the fp32 step's fast-path admission
     "r06_admit": {"FLAME_T_HALF_ADMIT": 0},
+    # the fp16 eager chain on fp32 registers (the step before the packed-fp16 chain body)
+    "r06_f16": {"FLAME_T_F16_NATIVE": 0},
 }
 
 
