@@ -206,6 +206,12 @@ constexpr bool kF16HwRoot = FLAME_T_F16_HWROOT != 0;
 #define FLAME_T_F16_NATIVE 1
 #endif
 constexpr bool kF16Native = FLAME_T_F16_NATIVE != 0;
+// ... and its root: v_sqrt_f16 on the packed pair (1; tools/fp_probe.py: equal to the correctly
+// rounded fp16 root on every fp16 v >= +0) or v_sqrt_f32 on the widened halves (0)
+#ifndef FLAME_T_F16_HSQRT
+#define FLAME_T_F16_HSQRT 1
+#endif
+constexpr bool kF16HalfRoot = FLAME_T_F16_HSQRT != 0;
 // the 16-bit steps' fast-path admission (adapt_vec_half): 1 = only what their root / quotient need --
 // v in [+0, 2^78] for both, and for fp16 (flame_fm::div_rn) a finite |num|: every nonzero finite
 // fp16 value is >= 2^-24, inside div_rn's range, and the bf16 quotient num * v_rcp_f32 matches on
@@ -313,13 +319,31 @@ __device__ __forceinline__ f2 widen_h2(uint32_t u) {
 // RN16(RN32(s * x)) of a pair: two v_fma_mix_f32 (a half widened exactly inside the instruction;
 // s * x + neg(0) = s * x + (-0) rounded once is the fp32 product, signed zeros included) and one v_cvt_pk_f16_f32 --
 // instead of two widening converts, a v_pk_mul_f32, the rounding and two more widening converts.
-__device__ __forceinline__ uint32_t smul_h2(float s, uint32_t x) {
-    float lo, hi;
+// (lo, hi: the two fp32 products before the fp16 rounding)
+__device__ __forceinline__ uint32_t smul_h2(float s, uint32_t x, float& lo, float& hi) {
     uint32_t r;
     asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(lo) : "s"(s), "v"(x));
     asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(hi) : "s"(s), "v"(x));
     asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
     return r;
+}
+__device__ __forceinline__ uint32_t smul_h2(float s, uint32_t x) {
+    float lo, hi;
+    return smul_h2(s, x, lo, hi);
+}
+// flame_fm::div_rn(num, den) with the numerator an fp16 half of x (HI: the high one): q0 = y * num
+// as one v_fma_mix_f32 (the widening inside it), the residual's -num folded the same way by the
+// compiler -- the same four roundings as div_rn on the widened value.  y is rcp_rn's fma result,
+// never a v_rcp_f32 result, so no transcendental feeds the inline asm.
+template <int HI>
+__device__ __forceinline__ float div_rn_h(uint32_t x, float den) {
+    const float y = flame_fm::rcp_rn(den);
+    float q0;
+    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(q0) : "v"(y), "v"(x));
+    else asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(q0) : "v"(y), "v"(x));
+    const float a = static_cast<float>(HI ? h2_of(x).y : h2_of(x).x);
+    const float rn = __builtin_fmaf(den, q0, -a);
+    return __builtin_fmaf(-rn, y, q0);
 }
 // RN16 of an fp32 pair, packed (never on a transcendental's result, see bf16_rnd1)
 __device__ __forceinline__ uint32_t pk_h2(f2 x) {
@@ -1208,9 +1232,9 @@ __device__ __forceinline__ void fedopt_chain_body_f16(const flame_segment& sg, i
     const h2 tau2 = {static_cast<_Float16>(tau), static_cast<_Float16>(tau)};   // tau is fp16-exact
     const bool tau_ok = (tau >= 0x1p-20f) & (tau <= 0x1p15f);                   // den in [2^-20, 65504]
     auto adapt = [&]() {
-        f2 num[4];
+        uint32_t num[4];
         us2 vmax = {0, 0};
-        float nhi = 0.f;
+        bool fin = true;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const h2 d = h2_of(b[p]) - h2_of(c[p]);
@@ -1228,32 +1252,41 @@ __device__ __forceinline__ void fedopt_chain_body_f16(const flame_segment& sg, i
             }
             m[p] = u_of(mn);
             v[p] = u_of(vn);
-            num[p] = widen_h2(smul_h2(eta, m[p]));
+            float plo, phi;
+            num[p] = smul_h2(eta, m[p], plo, phi);
             vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(us2, v[p]));
-            nhi = fmaxf(nhi, fmaxf(__builtin_fabsf(num[p].x), __builtin_fabsf(num[p].y)));
+            // compares (lane masks), not fmaxf: an fmaxf of an inline-asm result costs a
+            // canonicalizing max first
+            fin &= (__builtin_fabsf(plo) < 65520.f) & (__builtin_fabsf(phi) < 65520.f);
         }
-        // v's halves in [+0, 65504] (a sign, an inf or a NaN is above 0x7bff); a NaN numerator
-        // passes (its quotient is a NaN on either path)
-        const bool ok = tau_ok & (max(vmax.x, vmax.y) <= 0x7bffu) & (nhi <= 0x1p100f);
+        // v's halves in [+0, 65504] (a sign, an inf or a NaN is above 0x7bff); every numerator
+        // finite: its fp32 product below 65520, the fp16 overflow threshold (a NaN product fails the
+        // compare: that lane takes the general sequence, which gives the same NaN)
+        const bool ok = tau_ok & (max(vmax.x, vmax.y) <= 0x7bffu) & fin;
         if (ok) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-                const f2 vv = widen_h2(v[p]);
-                const h2 s = {static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.x)),
-                              static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.y))};
+                h2 s;
+                if constexpr (kF16HalfRoot) {
+                    s = __builtin_elementwise_sqrt(h2_of(v[p]));      // v_sqrt_f16 (tools/fp_probe.py)
+                } else {
+                    const f2 vv = widen_h2(v[p]);
+                    s = h2{static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.x)),
+                           static_cast<_Float16>(__builtin_amdgcn_sqrtf(vv.y))};
+                }
                 const f2 den = widen_h2(u_of(s + tau2));
-                const f2 q = {flame_fm::div_rn(num[p].x, den.x), flame_fm::div_rn(num[p].y, den.y)};
+                const f2 q = {div_rn_h<0>(num[p], den.x), div_rn_h<1>(num[p], den.y)};
                 c[p] = u_of(h2_of(c[p]) + h2_of(pk_h2(q)));
             }
         } else {
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-                const f2 vv = widen_h2(v[p]), cc = widen_h2(c[p]);
+                const f2 vv = widen_h2(v[p]), cc = widen_h2(c[p]), nn = widen_h2(num[p]);
                 float co[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const float den = f16_round(__fadd_rn(f16_round(__builtin_sqrtf(vv[h])), tau));
-                    co[h] = f16_round(__fadd_rn(cc[h], f16_round(__fdiv_rn(num[p][h], den))));
+                    co[h] = f16_round(__fadd_rn(cc[h], f16_round(__fdiv_rn(nn[h], den))));
                 }
                 c[p] = u_of(h2{static_cast<_Float16>(co[0]), static_cast<_Float16>(co[1])});   // exact
             }

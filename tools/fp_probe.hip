@@ -242,9 +242,55 @@ __global__ void f16_div_kernel(uint32_t dlo, uint32_t dhi, unsigned long long* o
     }
 }
 
+// the packed-fp16 chain body's root (FLAME_T_F16_HSQRT): v_sqrt_f16 on a packed pair (the same
+// builtin the kernel uses, so the same v_sqrt_f16 / v_sqrt_f16_sdwa pair) against the correctly
+// rounded fp16 root; pattern i in the low half, i ^ 0x0155 (masked to the range) in the high half
+using h2p = __attribute__((ext_vector_type(2))) _Float16;
+__global__ void f16_hsqrt_kernel(uint32_t lo, uint32_t hi, unsigned long long* out) {
+    const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const uint32_t j = lo + ((i - lo) ^ 0x0155u) % (hi - lo);
+    const uint32_t pair = i | (j << 16);
+    const h2p s = __builtin_elementwise_sqrt(__builtin_bit_cast(h2p, pair));
+    const uint32_t got = __builtin_bit_cast(uint32_t, s);
+    const uint32_t want = static_cast<uint32_t>(h16(flame_fm::sqrt_rn(f16v(i)))) |
+                          (static_cast<uint32_t>(h16(flame_fm::sqrt_rn(f16v(j)))) << 16);
+    if (got != want) report(out, i, j, got, want);
+}
+
+// the chain body's scalar products: v_fma_mix_f32(s, half, neg(0)) against the fp32 product of the
+// widened half, bit for bit (signed zeros included; NaNs compared as NaN), every fp16 pattern x the
+// scalars in ss[0 .. ns)
+__global__ void f16_mix_kernel(const float* ss, int ns, unsigned long long* out) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;     // 0 .. 65535
+    const uint32_t pair = x | ((x ^ 0x8001u) << 16);
+    for (int k = 0; k < ns; ++k) {
+        const float sv = ss[k];
+        float lo, hi;
+        asm volatile("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(lo) : "v"(sv), "v"(pair));
+        asm volatile("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(hi) : "v"(sv), "v"(pair));
+        const float wl = __fmul_rn(sv, f16v(x)), wh = __fmul_rn(sv, f16v(x ^ 0x8001u));
+        const bool okl = __float_as_uint(lo) == __float_as_uint(wl) || (lo != lo && wl != wl);
+        const bool okh = __float_as_uint(hi) == __float_as_uint(wh) || (hi != hi && wh != wh);
+        if (!(okl && okh)) report(out, x, __float_as_uint(sv), __float_as_uint(okl ? hi : lo), __float_as_uint(okl ? wh : wl));
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int probe_f16_hsqrt(uint32_t lo, uint32_t hi, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    if (hi > lo) f16_hsqrt_kernel<<<(hi - lo + 255) / 256, 256>>>(lo, hi, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+int probe_f16_mix(const float* ss, int ns, unsigned long long* out) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    f16_mix_kernel<<<256, 256>>>(ss, ns, out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
 
 int probe_f16_pack(uint64_t lo, uint64_t hi, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));

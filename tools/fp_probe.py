@@ -110,6 +110,19 @@ def main():
              f"finite fp16 v", L.probe_f16_sqrt(0, 0x7C00, th, p), True)
     show("fp16 (not shipped: the quotient stays div_rn): RN_f16(num * v_rcp_f32(den)) == RN_f16(div_rn(num, den)) on "
          "every finite fp16 num x every fp16 den in [2^-20, 65504]", L.probe_f16_div(0x0010, 0x7C00, p), False)
+    # the packed-fp16 chain body (fedopt_chain_body_f16): v_sqrt_f16 on pairs, v_fma_mix_f32 products
+    L.probe_f16_hsqrt.argtypes = [u32, u32, ctypes.c_void_p]
+    show("fp16 (FLAME_T_F16_HSQRT, shipped): packed v_sqrt_f16 == RN_f16(sqrt_rn(v)) on every non-negative finite "
+         "fp16 v (both halves)", L.probe_f16_hsqrt(0, 0x7C00, p), True)
+    L.probe_f16_mix.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    g = torch.Generator().manual_seed(5)
+    scal = torch.cat([torch.tensor([0.0, -0.0, 1.0, -1.0, 0.9, 0.1, 0.99, 0.01, 1e-2, 1 - 0.99, 4.0, -0.25, 2.0 ** -126,
+                                    2.0 ** -149, 3e38, float("inf"), float("-inf")]),
+                      (torch.randn(1007, generator=g) * torch.pow(2.0, torch.randint(-40, 40, (1007,), generator=g).float()))])
+    scal_d = scal.float().to("cuda")
+    show(f"fp16 (shipped): v_fma_mix_f32(s, half, neg(0)) == RN_f32(s * half) bit for bit on every fp16 pattern x "
+         f"{scal.numel()} scalars (+-0, +-inf, subnormal, random)", L.probe_f16_mix(scal_d.data_ptr(), scal.numel(), p),
+         True)
     # adapt_vec admits v below 2^-96 too: it only reaches sqrt(v) + tau (tau >= 2^-20)
     L.probe_den.argtypes = [u64, u64, ctypes.c_float, ctypes.c_void_p]
     for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):

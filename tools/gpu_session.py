@@ -54,6 +54,11 @@ STEPS = {
     **{f"chain_native_{v}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", "f16", "--rounds",
                                    "8", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_f16.so"])
        for v in ("adam", "yogi", "adagrad")},
+    # the packed-fp16 body's v_sqrt_f16 root and fp16 numerators against its first version (commit
+    # 828bb82's source, built into build/ab/variants/lib_r06_f16a.so), one process, bitwise
+    **{f"chain_f16a_{v}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", "f16", "--rounds",
+                                 "8", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_f16a.so"])
+       for v in ("adam", "yogi", "adagrad")},
     "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
                          "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
                          "--timeout-method", "thread"]),
