@@ -59,6 +59,10 @@ STEPS = {
     **{f"chain_f16a_{v}": (400, [PY, "tools/chain_sweep.py", "--variant", f"fed{v}", "--dtype", "f16", "--rounds",
                                  "8", "--libs", "flame_amd/libflame_amd.so,build/ab/variants/lib_r06_f16a.so"])
        for v in ("adam", "yogi", "adagrad")},
+    # fresh random 16-bit eager cases (the packed-fp16 chain body against the per-call launches)
+    "soak_eager16": (600, ["env", "FLAME_RANDOM_SCALE=50", "FLAME_RANDOM_SEED_OFFSET=200000", PY, "-u", "-m",
+                           "pytest", "tests/test_gpu_random_cases.py", "-m", "gpu", "-k", "eager_fedopt_16bit", "-x",
+                           "-q", "--timeout", "200", "--timeout-method", "thread"]),
     "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
                          "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
                          "--timeout-method", "thread"]),
