@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("FLAME_AMD_LIB", os.path.join(PKG, "libflame_amd.so"))
 # constants mirrored from include/flame_amd.h
 FLAME_OK, FLAME_EINVAL, FLAME_EHIP, FLAME_ENOTSUP = 0, 1, 2, 3
 FLAME_F32, FLAME_BF16, FLAME_F16, FLAME_F64, FLAME_I64, FLAME_I32 = range(6)
+FLAME_U8, FLAME_I8, FLAME_I16, FLAME_BOOL = range(6, 10)       # flame_elementwise only
 FLAME_AGG_INIT_FIRST = 1
 FLAME_AGG_SEG_RATES = 2
 FLAME_AGG_XCD_MAP = 4
@@ -37,7 +38,7 @@ FLAME_TILE_BYTES = 4096
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
     "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedopt_chain", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
-    "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_synth_fill",
+    "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_elementwise", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
     "flame_slab_write", "flame_slab_write_2d",
     "flame_launch_branches", "flame_launch_branch_name", "flame_launch_branch_count",
@@ -95,6 +96,8 @@ def lib() -> ctypes.CDLL:
     L.flame_feddyn_round.restype = ctypes.c_int
     L.flame_feddyn_round.argtypes = [ctypes.c_int, vp, i32, i64, vp, vp, i32, i32, ctypes.c_double,
                                      ctypes.c_double, vp]
+    L.flame_elementwise.restype = ctypes.c_int
+    L.flame_elementwise.argtypes = [vp, i32, vp, i32, i64, vp]
     L.flame_synth_fill.restype = ctypes.c_int
     L.flame_synth_fill.argtypes = [ctypes.c_int, vp, i64, u64, u64, i64, f32, vp]
     L.flame_host_register.restype = ctypes.c_int

@@ -98,4 +98,48 @@ __device__ __forceinline__ bool admits_finite(const float (&num)[N]) {
     return nhi <= 0x1p100f;
 }
 
+// fp64 divide and root correctly rounded, for the elementwise programs' fp64 keys (torch-CPU's
+// are IEEE double ops): the compiler's sequences, then one exact-residual step.
+//  * divide: of q = a / b and its two neighbours, the one with the smallest |a - c * b| (one fma
+//    each, exact while a, b and q stay inside [2^-960, 2^960] in magnitude -- outside, q as the
+//    compiler gives it), a tie to the even significand: |a - c b| = |b| |a / b - c|;
+//  * root: s moves up iff x - s^2 > s * (s+ - s), down iff x - s^2 <= -s * (s - s-) -- x against
+//    the squares of the two midpoints (x - s^2 is exact and a multiple of ulp(s)^2, so the ulp^2/4
+//    terms never decide; a root is never a midpoint); x below 2^-900 is scaled by 2^1000 first.
+// tools/fp_probe.py counts how often the compiler's results needed the step.
+// the neighbours of a finite nonzero double toward +inf / -inf (its bits +-1)
+__device__ __forceinline__ double dnext(double x, bool up) {
+    const long long b = __double_as_longlong(x);
+    return __longlong_as_double((x > 0.0) == up ? b + 1 : b - 1);
+}
+__device__ __forceinline__ bool dmid(double x) {
+    const double ax = __builtin_fabs(x);
+    return ax >= 0x1p-960 && ax <= 0x1p960;
+}
+__device__ __forceinline__ double ddiv_rn(double a, double b) {
+    const double q = a / b;
+    if (!(dmid(a) && dmid(b) && dmid(q))) return q;
+    const double qp = dnext(q, true), qm = dnext(q, false);
+    const double r = __builtin_fabs(__builtin_fma(-q, b, a)), rp = __builtin_fabs(__builtin_fma(-qp, b, a)),
+                 rm = __builtin_fabs(__builtin_fma(-qm, b, a));
+    auto odd = [](double x) { return (__double_as_longlong(x) & 1) != 0; };
+    double best = q, rb = r;
+    if (rp < rb || (rp == rb && odd(best))) { best = qp; rb = rp; }
+    if (rm < rb || (rm == rb && odd(best))) { best = qm; rb = rm; }
+    return best;
+}
+__device__ __forceinline__ double dsqrt_core(double x) {     // 2^-900 <= x < inf
+    const double s = __builtin_sqrt(x);
+    const double sp = dnext(s, true), sm = dnext(s, false);                  // s > 0
+    const double r = __builtin_fma(-s, s, x);
+    if (r > s * (sp - s)) return sp;
+    if (r <= -s * (s - sm)) return sm;
+    return s;
+}
+__device__ __forceinline__ double dsqrt_rn(double x) {
+    if (!(x > 0.0) || !__builtin_isfinite(x)) return __builtin_sqrt(x);      // +-0, negatives, NaN, inf
+    if (x < 0x1p-900) return dsqrt_core(x * 0x1p1000) * 0x1p-500;           // exact scalings
+    return dsqrt_core(x);
+}
+
 }  // namespace flame_fm

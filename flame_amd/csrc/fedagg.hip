@@ -1930,6 +1930,162 @@ __global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, 
         if (kind[j] == 1) st_plain(dp[j], v[j]);
 }
 
+// ---------------------------------------------------------------- elementwise programs
+// flame_elementwise (include/flame_amd.h): the reference's torch statements for keys the fused
+// kernels do not take -- an int buffer (num_batches_tracked), a mixed-dtype or fp64 key -- as a
+// short typed op list read from the kernel arguments in place (scalar loads; every wave takes the
+// same switch arm).  A register holds a double (every fp32 / bf16 / fp16 value is exact in one)
+// or an int64.  Such keys are small, so the registers may live in scratch.
+struct EwArgs {
+    flame_ew_op ops[FLAME_EW_MAX_OPS];
+    void* bufs[FLAME_EW_MAX_BUFS];
+    int64_t numel;
+    int32_t n_ops;
+};
+union EwVal {
+    double f;
+    int64_t i;
+};
+
+__host__ __device__ __forceinline__ bool ew_float(int dt) { return dt >= FLAME_F32 && dt <= FLAME_F64; }
+// an fp32 result into a 32-bit-or-narrower float dtype (torch's opmath result, rounded once)
+__device__ __forceinline__ double ew_rnd32(float x, int dt) {
+    if (dt == FLAME_BF16) return bf16_round(x);
+    if (dt == FLAME_F16) return f16_round(x);
+    return x;
+}
+// an int64 wrapped to the integer dtype's width (two's complement, as torch's int ops wrap)
+__device__ __forceinline__ int64_t ew_wrap(int64_t x, int dt) {
+    switch (dt) {
+    case FLAME_I32: return static_cast<int32_t>(static_cast<uint32_t>(x));
+    case FLAME_I16: return static_cast<int16_t>(static_cast<uint16_t>(x));
+    case FLAME_I8: return static_cast<int8_t>(static_cast<uint8_t>(x));
+    case FLAME_U8: return static_cast<uint8_t>(x);
+    case FLAME_BOOL: return x != 0;
+    default: return x;
+    }
+}
+__device__ __forceinline__ EwVal ew_load(const void* p, int64_t i, int dt) {
+    EwVal v;
+    switch (dt) {
+    case FLAME_F32: v.f = ld1(static_cast<const float*>(p) + i); break;
+    case FLAME_BF16: v.f = bf16_to_f32(ld1(static_cast<const uint16_t*>(p) + i)); break;
+    case FLAME_F16: v.f = f16_to_f32(ld1(static_cast<const uint16_t*>(p) + i)); break;
+    case FLAME_F64: v.f = ld1(static_cast<const double*>(p) + i); break;
+    case FLAME_I64: v.i = ld1(static_cast<const int64_t*>(p) + i); break;
+    case FLAME_I32: v.i = ld1(static_cast<const int32_t*>(p) + i); break;
+    case FLAME_I16: v.i = ld1(static_cast<const int16_t*>(p) + i); break;
+    case FLAME_I8: v.i = ld1(static_cast<const int8_t*>(p) + i); break;
+    default: v.i = ld1(static_cast<const uint8_t*>(p) + i); break;        // U8, BOOL
+    }
+    return v;
+}
+__device__ __forceinline__ void ew_store(void* p, int64_t i, int dt, EwVal v) {
+    switch (dt) {
+    case FLAME_F32: st1(static_cast<float*>(p) + i, static_cast<float>(v.f)); break;
+    case FLAME_BF16: st1(static_cast<uint16_t*>(p) + i, f32_to_bf16_exact(static_cast<float>(v.f))); break;
+    case FLAME_F16: st1(static_cast<uint16_t*>(p) + i, f32_to_f16_bits(static_cast<float>(v.f))); break;
+    case FLAME_F64: st1(static_cast<double*>(p) + i, v.f); break;
+    case FLAME_I64: st1(static_cast<int64_t*>(p) + i, v.i); break;
+    case FLAME_I32: st1(static_cast<int32_t*>(p) + i, static_cast<int32_t>(v.i)); break;
+    case FLAME_I16: st1(static_cast<int16_t*>(p) + i, static_cast<int16_t>(v.i)); break;
+    case FLAME_I8: st1(static_cast<int8_t*>(p) + i, static_cast<int8_t>(v.i)); break;
+    default: st1(static_cast<uint8_t*>(p) + i, static_cast<uint8_t>(v.i)); break;
+    }
+}
+// CAST from dtype s to dtype t (c10's conversions: an int or an fp64 value reaches bf16 / fp16
+// through fp32; a float reaches an int toward zero)
+__device__ __forceinline__ EwVal ew_cast(EwVal x, int s, int t) {
+    EwVal r;
+    if (ew_float(t)) {
+        if (t == FLAME_F64) r.f = ew_float(s) ? x.f : __ll2double_rn(x.i);
+        else {
+            const float f = ew_float(s) ? (s == FLAME_F64 ? __double2float_rn(x.f) : static_cast<float>(x.f))
+                                        : __ll2float_rn(x.i);
+            r.f = ew_rnd32(f, t);
+        }
+    } else if (t == FLAME_BOOL) {
+        r.i = ew_float(s) ? (x.f != 0.0) : (x.i != 0);
+    } else {
+        r.i = ew_wrap(ew_float(s) ? __double2ll_rz(x.f) : x.i, t);
+    }
+    return r;
+}
+// a binary op in dtype dt on two values of dt (fp32 opmath for bf16 / fp16, as torch-CPU)
+template <int OP>
+__device__ __forceinline__ EwVal ew_bin(EwVal a, EwVal b, int dt) {
+    EwVal r;
+    if (dt == FLAME_F64) {
+        r.f = OP == FLAME_EW_ADD ? __dadd_rn(a.f, b.f) : OP == FLAME_EW_SUB ? __dsub_rn(a.f, b.f)
+            : OP == FLAME_EW_MUL ? __dmul_rn(a.f, b.f) : flame_fm::ddiv_rn(a.f, b.f);
+    } else if (ew_float(dt)) {
+        const float x = static_cast<float>(a.f), y = static_cast<float>(b.f);
+        r.f = ew_rnd32(OP == FLAME_EW_ADD ? __fadd_rn(x, y) : OP == FLAME_EW_SUB ? __fsub_rn(x, y)
+                       : OP == FLAME_EW_MUL ? __fmul_rn(x, y) : __fdiv_rn(x, y), dt);
+    } else {
+        const uint64_t x = static_cast<uint64_t>(a.i), y = static_cast<uint64_t>(b.i);
+        r.i = ew_wrap(static_cast<int64_t>(OP == FLAME_EW_ADD ? x + y : OP == FLAME_EW_SUB ? x - y : x * y), dt);
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kEwBlock) void ew_kernel(EwArgs args) {
+    (void)sizeof(args);      // read in place from the kernarg segment (see agg_reduce_kernel_argmeta)
+    const EwArgs* P = (const EwArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int64_t numel = P->numel;
+    const int n_ops = P->n_ops;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < numel; i += stride) {
+        EwVal r[FLAME_EW_MAX_REGS];
+        for (int k = 0; k < n_ops; ++k) {
+            const flame_ew_op& o = P->ops[k];
+            const int dt = o.dtype;
+            switch (o.op) {
+            case FLAME_EW_LOAD: r[o.dst] = ew_load(P->bufs[o.a], i, dt); break;
+            case FLAME_EW_STORE: ew_store(P->bufs[o.a], i, dt, r[o.b]); break;
+            case FLAME_EW_ZERO: if (ew_float(dt)) r[o.dst].f = 0.0; else r[o.dst].i = 0; break;
+            case FLAME_EW_CAST: r[o.dst] = ew_cast(r[o.a], o.b, dt); break;
+            case FLAME_EW_ADD: r[o.dst] = ew_bin<FLAME_EW_ADD>(r[o.a], r[o.b], dt); break;
+            case FLAME_EW_SUB: r[o.dst] = ew_bin<FLAME_EW_SUB>(r[o.a], r[o.b], dt); break;
+            case FLAME_EW_MUL: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.b], dt); break;
+            case FLAME_EW_DIV: r[o.dst] = ew_bin<FLAME_EW_DIV>(r[o.a], r[o.b], dt); break;
+            case FLAME_EW_ADD_S:
+            case FLAME_EW_MUL_S: {
+                EwVal s;
+                if (dt == FLAME_F64) s.f = o.scalar;
+                else if (ew_float(dt)) {
+                    // torch-CPU: a Python scalar multiplies a float tensor in fp32 (opmath) but is
+                    // rounded to a bf16 / fp16 tensor's dtype before it is added
+                    const float sf = __double2float_rn(o.scalar);
+                    s.f = o.op == FLAME_EW_ADD_S ? ew_rnd32(sf, dt) : sf;
+                } else {
+                    s.i = __double2ll_rz(o.scalar);
+                }
+                r[o.dst] = o.op == FLAME_EW_ADD_S ? ew_bin<FLAME_EW_ADD>(r[o.a], s, dt)
+                                                  : ew_bin<FLAME_EW_MUL>(r[o.a], s, dt);
+                break;
+            }
+            case FLAME_EW_SQUARE: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.a], dt); break;
+            case FLAME_EW_SIGN: {
+                EwVal v = r[o.a];
+                if (ew_float(dt)) v.f = static_cast<double>((0.0 < v.f) - (v.f < 0.0));   // NaN, -0 -> +0
+                else v.i = (v.i > 0) - (v.i < 0);
+                r[o.dst] = v;
+                break;
+            }
+            case FLAME_EW_SQRT: {
+                EwVal v = r[o.a];
+                if (dt == FLAME_F64) v.f = flame_fm::dsqrt_rn(v.f);
+                else v.f = ew_rnd32(__builtin_sqrtf(static_cast<float>(v.f)), dt);   // correctly rounded
+                r[o.dst] = v;
+                break;
+            }
+            default: break;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launch-branch counters
 // Every host-side launch branch of the C ABI has an index; a successful launch counts it, so
 // tests can assert which instantiation a call took and that every branch is reached by an
@@ -1953,7 +2109,8 @@ enum : int {
     BR_HIER_ARG_LDS = 74,   // + dt * 2 + sync: flame_hier_fedbuff_argmeta, LDS store groups
     BR_CHAIN = 80,          // + dt * 3 + variant (f32, bf16, f16): flame_fedopt_chain
     BR_AGG_LOB = 89,        // + dt (f32, bf16, f16): flame_agg_reduce, low residency, LDS-held output bursts
-    BR_COUNT = 92
+    BR_EW = 92,             // flame_elementwise
+    BR_COUNT = 93
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -1982,7 +2139,8 @@ const char* branch_name(int i) {
             else if (b < BR_HIER_ARG_LDS) snprintf(n, z, "flame_fedopt_reduce_adapt_argmeta/multi/f32/%s", var[b - BR_OPT_ARG_MULTI]);
             else if (b < BR_CHAIN) snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
             else if (b < BR_AGG_LOB) snprintf(n, z, "flame_fedopt_chain/%s/%s", dts[(b - BR_CHAIN) / 3], var[(b - BR_CHAIN) % 3]);
-            else snprintf(n, z, "flame_agg_reduce/lo_burst/%s", dts[b - BR_AGG_LOB]);
+            else if (b < BR_EW) snprintf(n, z, "flame_agg_reduce/lo_burst/%s", dts[b - BR_AGG_LOB]);
+            else snprintf(n, z, "flame_elementwise");
         }
         return true;
     }();
@@ -2522,6 +2680,70 @@ int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_
     default: return set_err(FLAME_ENOTSUP, "flame_synth_fill: dtype %d not supported", dtype);
     }
     return check_launch("flame_synth_fill");
+}
+
+int flame_elementwise(const flame_ew_op* prog, int32_t n_ops, void* const* bufs, int32_t n_bufs, int64_t numel,
+                      void* stream) {
+    if (n_ops < 0 || n_ops > FLAME_EW_MAX_OPS || (n_ops > 0 && !prog))
+        return set_err(FLAME_EINVAL, "flame_elementwise: n_ops %d outside [0, %d] or NULL program", n_ops, FLAME_EW_MAX_OPS);
+    if (n_bufs < 0 || n_bufs > FLAME_EW_MAX_BUFS || (n_bufs > 0 && !bufs))
+        return set_err(FLAME_EINVAL, "flame_elementwise: n_bufs %d outside [0, %d] or NULL table", n_bufs, FLAME_EW_MAX_BUFS);
+    if (numel < 0) return set_err(FLAME_EINVAL, "flame_elementwise: numel < 0");
+    // host-side check of the program: every register defined before it is read, in the dtype the
+    // reading op says; every buffer it names present; an op / dtype the kernel knows
+    int rdt[FLAME_EW_MAX_REGS];
+    for (int k = 0; k < FLAME_EW_MAX_REGS; ++k) rdt[k] = -1;
+    auto reg = [](int x) { return x >= 0 && x < FLAME_EW_MAX_REGS; };
+    for (int32_t k = 0; k < n_ops; ++k) {
+        const flame_ew_op& o = prog[k];
+        const int dt = o.dtype;
+        if (dt < FLAME_F32 || dt > FLAME_BOOL) return set_err(FLAME_EINVAL, "flame_elementwise: op %d: dtype %d", k, dt);
+        auto bad = [&](const char* why) { return set_err(FLAME_EINVAL, "flame_elementwise: op %d (%d): %s", k, o.op, why); };
+        switch (o.op) {
+        case FLAME_EW_LOAD:
+            if (!reg(o.dst) || o.a < 0 || o.a >= n_bufs || (numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
+            rdt[o.dst] = dt;
+            break;
+        case FLAME_EW_STORE:
+            if (!reg(o.b) || o.a < 0 || o.a >= n_bufs || (numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
+            if (rdt[o.b] != dt) return bad("stored register is not of the buffer's dtype");
+            break;
+        case FLAME_EW_ZERO:
+            if (!reg(o.dst)) return bad("bad register");
+            rdt[o.dst] = dt;
+            break;
+        case FLAME_EW_CAST:
+            if (!reg(o.dst) || !reg(o.a) || rdt[o.a] < 0 || rdt[o.a] != o.b) return bad("source register undefined or not of dtype b");
+            rdt[o.dst] = dt;
+            break;
+        case FLAME_EW_ADD: case FLAME_EW_SUB: case FLAME_EW_MUL: case FLAME_EW_DIV:
+            if (!reg(o.dst) || !reg(o.a) || !reg(o.b) || rdt[o.a] != dt || rdt[o.b] != dt) return bad("operand not of the op's dtype");
+            if (o.op == FLAME_EW_DIV && !ew_float(dt)) return bad("division in an integer dtype");
+            // bool: torch's + is a logical or, * a logical and (the sum / product != 0); - raises
+            if (dt == FLAME_BOOL && o.op == FLAME_EW_SUB) return bad("subtraction in bool");
+            rdt[o.dst] = dt;
+            break;
+        case FLAME_EW_ADD_S: case FLAME_EW_MUL_S: case FLAME_EW_SQUARE: case FLAME_EW_SIGN: case FLAME_EW_SQRT:
+            if (!reg(o.dst) || !reg(o.a) || rdt[o.a] != dt) return bad("operand not of the op's dtype");
+            if (o.op == FLAME_EW_SQRT && !ew_float(dt)) return bad("sqrt in an integer dtype");
+            if (dt == FLAME_BOOL && (o.op == FLAME_EW_ADD_S || o.op == FLAME_EW_MUL_S))
+                return bad("a scalar op in bool");
+            rdt[o.dst] = dt;
+            break;
+        default: return bad("unknown op");
+        }
+    }
+    if (numel == 0 || n_ops == 0) return FLAME_OK;
+    EwArgs a{};
+    for (int32_t k = 0; k < n_ops; ++k) a.ops[k] = prog[k];
+    for (int32_t k = 0; k < n_bufs; ++k) a.bufs[k] = bufs[k];
+    a.numel = numel;
+    a.n_ops = n_ops;
+    int64_t blocks = (numel + kEwBlock - 1) / kEwBlock;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(ew_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kEwBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    return launched(BR_EW, "flame_elementwise");
 }
 
 static int check_tile_copies(const flame_tile_copy* t, int32_t n, const char* who) {

@@ -648,7 +648,15 @@ def _scale_add_promoted(b: torch.Tensor, a: torch.Tensor, goal: int, delta, devi
     old = b.clone() if delta is not None else None
     _add_promoted(b.view(-1), q)
     if delta is not None:
-        torch.sub(b.view(-1), old.view(-1), out=delta.view(-1))
+        from . import elementwise as ew
+        dv = delta.view(-1)
+        d = ew.Lazy.of(b.view(-1)) - ew.Lazy.of(old.view(-1))
+        if d.dtype != dv.dtype:             # torch.sub(..., out=delta) casts into delta's dtype
+            d = d.to(dv.dtype)
+        if dv.is_cuda and dv.is_contiguous():
+            ew.materialize(d, device=dv.device, into=[dv])
+        else:
+            dv.copy_(ew.materialize(d, device=device)[0])
 
 
 # ------------------------------------------------------------------ co-located FedBuff hierarchy
@@ -1130,18 +1138,11 @@ def _check_cast(acc_dt, v_dt) -> None:
 def _add_promoted(acc: torch.Tensor, tmp: torch.Tensor) -> None:
     """``acc += tmp`` in place with torch's semantics when the dtypes differ: computed in
     promote_types(acc, tmp) and rounded back to acc's dtype (bf16 += f32, f16 += bf16,
-    f32 += f64, ...: the add runs in the kernel in the promoted dtype with rate 1, the
-    up/down casts are device copies); integer promotions (int32 += int64) are an exact
-    integer add, wrapping like torch's."""
-    p = torch.promote_types(acc.dtype, tmp.dtype)
+    f32 += f64, ...; integer promotions such as int32 += int64 wrap like torch's) -- one
+    flame_elementwise launch (casts, the add, the cast back)."""
+    from . import elementwise as ew
     _check_cast(acc.dtype, tmp.dtype)
-    if p.is_floating_point:
-        accp = acc if p == acc.dtype else acc.to(p)
-        reduce_([accp], [accp], [[tmp if tmp.dtype == p else tmp.to(p)]], [1.0])
-        if accp is not acc:
-            acc.copy_(accp)
-    else:
-        acc.copy_(acc.to(p) + tmp.to(p))
+    ew.iadd(acc, ew.Lazy.of(tmp))
 
 
 def logical_shape(weights, k):

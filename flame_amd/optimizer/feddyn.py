@@ -11,7 +11,8 @@ updated history written once, instead of the reference's four passes (history,
 average, mean, cld).  The average sums in cache order and the mean in
 ``local_param_dict`` order, each op rounded as torch-CPU rounds it, so results
 are bit-identical.  Keys whose dtypes mix (int buffers, whose ``rate * h`` the
-reference promotes to fp32) follow the reference ops with torch on the device.
+reference promotes to fp32) run the reference's statements as ``flame_elementwise``
+programs (``flame_amd.elementwise``: torch's promotions, torch-CPU's arithmetic).
 
 History tensors are private device copies: the reference aliases the first
 update it sees for an end (``local_param_dict[end] = tres.weights``) and then
@@ -34,7 +35,7 @@ import logging
 import torch
 
 from .. import _native as N
-from .. import engine
+from .. import elementwise as ew, engine
 from .fedavg import FedAvg
 
 logger = logging.getLogger(__name__)
@@ -386,12 +387,16 @@ class FedDyn(FedAvg):
 
     # ------------------------------------------------------------------ mixed-dtype keys
     def _reference_round(self, keys, arrivals, had, rate, device, new_hist, cld):
-        """The reference's op sequence with torch on the device (its dtype promotions)."""
+        """The reference's statements (feddyn.py:90-113,125-139) for the mixed-dtype keys, with
+        torch's dtype promotions: each one recorded on elementwise.Lazy operands and run as a
+        flame_elementwise program on ``device`` (the mean of the histories in launches of up
+        to _MEAN_TERMS terms); the FedAvg part through engine.accumulate."""
         for e, w in arrivals:
             if e in had:
                 h = self.local_param_dict[e]
                 for k in keys:
-                    h[k] = h[k] + engine.logical_tensor(w, k).to(h[k].device)
+                    s = ew.materialize(ew.Lazy.of(h[k]) + ew.Lazy.of(engine.logical_tensor(w, k)), device=device)[0]
+                    h[k] = s if h[k].device == device else s.to(h[k].device)
             else:
                 for k in keys:
                     new_hist[e][k] = _own_copy(w, k, device)
@@ -402,10 +407,17 @@ class FedDyn(FedAvg):
                 if h is not None or e in new_hist]
         for k in keys:
             a = self.agg_weights[k]
-            mean = 0.0
+            mean, terms = 0.0, 0          # mean = 0.0; mean = mean + rate_mean * h[k] per history
             for h in hist:
-                mean = mean + rate_mean * h[k]
-            cld[k] = (a.to(device) + mean).to(a.device)
+                mean = mean + rate_mean * ew.Lazy.of(h[k])
+                terms += 1
+                if terms == _MEAN_TERMS:
+                    mean, terms = ew.Lazy.of(ew.materialize(mean, device=device)[0]), 0
+            c = ew.materialize(ew.Lazy.of(a) + mean, device=device)[0]
+            cld[k] = c if a.device == device else c.to(a.device)
+
+
+_MEAN_TERMS = 8      # histories per flame_elementwise launch of the mean (<= 6 ops each; 64 per program)
 
 
 def _own_copy(weights, k, device):

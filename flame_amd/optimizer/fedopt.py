@@ -11,9 +11,10 @@ reduction, ``d``, ``m_t``, ``v_t`` and the new ``current`` are computed in
 registers with one rounding per reference op, reading base/cur/m/v once and
 writing avg/m/v/cur once, instead of ~12 unfused torch passes.  Other keys
 (BatchNorm's int64 ``num_batches_tracked``, which the reference silently
-promotes to fp32 in this step, and any key whose dtype changed) are reduced by
-the FedAvg kernel and then follow the reference op sequence with torch ops on
-the device.
+promotes to fp32 in this step, fp64 keys, and any key whose dtype changed) are
+reduced by the FedAvg kernel and then run the reference's statements as one
+``flame_elementwise`` program per key (``flame_amd.elementwise``: torch's own dtype
+promotions, torch-CPU's arithmetic per dtype).
 
 Ownership: ``base_weights`` is mutated in place into the
 FedAvg result (``self.agg_weights``); ``m_t``/``v_t`` persist across rounds on
@@ -39,7 +40,7 @@ from collections import OrderedDict
 
 import torch
 
-from .. import engine, metrics
+from .. import elementwise as ew, engine, metrics
 from .fedavg import FedAvg
 
 logger = logging.getLogger(__name__)
@@ -398,21 +399,20 @@ class FedOPT(FedAvg):
                                f"re-create the optimizer ({type(e).__name__}: {e})") from e
 
     def _adapt_generic(self, keys, average, current, state_zero):
-        """fedopt.py:106-129 op sequence (torch ops on the device) for non-fp32 keys."""
+        """fedopt.py:106-129 for the keys the fused kernel does not take (int buffers such as
+        num_batches_tracked, mixed-dtype and fp64 keys): the reference's statements, the
+        subclass's _delta_v_tensor included, recorded on elementwise.Lazy operands and run as
+        ONE flame_elementwise launch per key -- torch's own dtype promotions, torch-CPU's
+        arithmetic per dtype (include/flame_amd.h), no PyTorch compute."""
         out = {}
         for k in keys:
-            d = average[k] - current[k]
-            m = torch.zeros_like(d) if state_zero or k not in self.m_t else self.m_t[k]
+            d = ew.Lazy.of(average[k]) - ew.Lazy.of(current[k])
+            m = torch.zeros_like(d) if state_zero or k not in self.m_t else ew.Lazy.of(self.m_t[k])
             m = self.beta_1 * m + (1 - self.beta_1) * d
-            v = torch.zeros_like(d) if state_zero or k not in self.v_t else self.v_t[k]
+            v = torch.zeros_like(d) if state_zero or k not in self.v_t else ew.Lazy.of(self.v_t[k])
             v = self._delta_v_tensor(v, d)
-            self.m_t[k], self.v_t[k] = m, v
-            sq = torch.sqrt(v)
-            # torch-CPU adds a Python scalar to a bf16/fp16 tensor after rounding the scalar
-            # to that dtype (unlike mul/div, which use it in fp32); GPU torch keeps it fp32.
-            tau = float(torch.tensor(self.tau, dtype=sq.dtype)) if sq.dtype in (torch.bfloat16, torch.float16) \
-                else self.tau
-            out[k] = current[k] + self.eta * m / (sq + tau)
+            new = ew.Lazy.of(current[k]) + self.eta * m / (torch.sqrt(v) + self.tau)
+            self.m_t[k], self.v_t[k], out[k] = ew.materialize(m, v, new, device=average[k].device)
         return out
 
     @abstractmethod

@@ -8,8 +8,8 @@ is FedAvg over the model updates with the uniform rate ``1/len(cache)``
 (:127-134).  Both are the sequential weighted client reduction: one
 ``flame_agg_reduce`` launch per dtype over every key and every trainer,
 bit-identical to the reference's per-trainer / per-key torch-CPU loop.
-A control variate whose dtype differs from ``c_glob``'s follows the
-reference ops (``(v*rate).to(c.dtype)`` then ``+=``) with torch on the device.
+A control variate whose dtype differs from ``c_glob``'s runs the reference's
+statements (``(v*rate).to(c.dtype)`` then ``+=``) as ``flame_elementwise`` programs.
 
 ``c_glob`` is created ``zeros_like`` the global weights (:81-90), but in HBM:
 it is state the server updates every round and only reads out when it sends
@@ -19,7 +19,7 @@ import logging
 
 import torch
 
-from .. import engine
+from .. import elementwise as ew, engine
 from .fedavg import FedAvg
 
 logger = logging.getLogger(__name__)
@@ -92,9 +92,9 @@ class Scaffold(FedAvg):
         if same:
             engine.accumulate({k: c[k] for k in same}, [({k: w[k] for k in same}, rate) for w in controls],
                               device=device)
-        for w in controls:   # keys with another dtype, in trainer order (reference ops)
-            for k in w.keys():
+        for w in controls:   # keys with another dtype, in trainer order: the reference's statements
+            for k in w.keys():   # as flame_elementwise programs (elementwise.py)
                 if k in same:
                     continue
-                tmp = engine.logical_tensor(w, k).to(device) * rate
-                c[k] += tmp.to(dtype=c[k].dtype) if tmp.dtype != c[k].dtype else tmp
+                tmp = ew.Lazy.of(engine.logical_tensor(w, k)) * rate
+                ew.iadd(c[k], tmp.to(c[k].dtype) if tmp.dtype != c[k].dtype else tmp)

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from .. import _native as N
-from .. import engine
+from .. import elementwise as ew, engine
 from .fedbuff import _tiled_stride, _write_tiled
 
 _KERNEL_DTYPES = (N.FLAME_F32, N.FLAME_BF16, N.FLAME_F16)
@@ -168,14 +168,15 @@ def _fused(keys, mids, entries, top_weights, top_rates, device, deltas, update_m
 
 
 def _compose(keys, mids, entries, top_weights, top_rates, device, deltas, update_middle_weights):
-    """The reference's op sequence for ``keys``: FedAvg per middle (kernel), delta (torch
-    sub, common/util.py:152-159), FedAvg of the deltas at the top (kernel)."""
+    """The reference's op sequence for ``keys``: FedAvg per middle (kernel), delta
+    (common/util.py:152-159, a flame_elementwise program), FedAvg of the deltas at the top
+    (kernel)."""
     top_entries = []
     for i, (w, e) in enumerate(zip(mids, entries)):
         lw = {k: engine.logical_tensor(w, k) for k in keys}      # slab-slot middles: logical copies
         new = {k: lw[k].clone() for k in keys}                   # deepcopy(self.weights)
         engine.accumulate(new, [({k: x[k] for k in keys}, r) for x, r in e], device=device)
-        d = {k: new[k] - lw[k] for k in keys}
+        d = {k: ew.materialize(ew.Lazy.of(new[k]) - ew.Lazy.of(lw[k]), device=device)[0] for k in keys}
         if update_middle_weights:
             for k in keys:
                 if lw[k] is w[k]:

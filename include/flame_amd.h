@@ -23,6 +23,9 @@
  *                               fed to the top's FedBuff (asyncfl/top_aggregator.py:85-109)
  *   flame_feddyn_round          optimizer/feddyn.py:90-113,125-139 (FedDyn.do: add_to_hist,
  *                               FedAvg with rate 1/len(cache), mean of the histories, cld_model)
+ *   flame_elementwise           the same statements for the keys the fused kernels do not take
+ *                               (int / mixed-dtype / fp64 keys): optimizer/fedopt.py:102-129,
+ *                               scaffold.py:141-150, feddyn.py:90-113,125-139
  *   flame_synth_fill            (bench/test plumbing: counter-based synthetic updates)
  *   flame_hier_resident_per_cu  (no reference counterpart: occupancy query the parameter
  *                               shard uses to size its waves, flame_amd/shard.py)
@@ -311,6 +314,62 @@ typedef struct flame_dyn_segment {
 int flame_feddyn_round(int dtype, const flame_dyn_segment *segs, int32_t n_segs, int64_t n_chunks,
                        const void *const *steps, const uint32_t *step_flags, int32_t n_steps,
                        int32_t n_phase1, double rate_avg, double rate_mean, void *stream);
+/*
+ * flame_elementwise: one elementwise program -- a short typed op sequence, the reference's
+ * own torch statements for the keys the fused kernels do not take (int buffers such as
+ * num_batches_tracked, mixed-dtype keys, fp64 / int8 / uint8 / int16 tensors):
+ *   optimizer/fedopt.py:102-129 + fedadam.py:33-35 / fedyogi.py:34-36 / fedadagrad.py:33-35
+ *     (FedOPT's adaptive step: d, m, v, sqrt(v) + tau, the quotient, current + ...),
+ *   optimizer/scaffold.py:141-150 (c += (w * rate).to(c.dtype) for a control of another dtype),
+ *   optimizer/feddyn.py:90-113,125-139 (the history / mean / cld statements of mixed keys).
+ * flame_amd/elementwise.py records the statements on lazy tensors and takes every result dtype
+ * from torch's own promotion (the statements run on meta tensors of the same shapes), so a
+ * program only ever computes what torch-CPU would: an op whose operands are cast (FLAME_EW_CAST)
+ * to its result dtype first, then
+ *   fp32 / fp64: one IEEE round-to-nearest-even op (sqrt / divide correctly rounded);
+ *   bf16 / fp16: the op in fp32 on the widened operands, rounded once to the dtype; a scalar
+ *     is used in fp32 by MUL_S and rounded to the dtype first by ADD_S (torch-CPU's behaviour);
+ *   integers: two's-complement arithmetic wrapped to the dtype's width (bool: + is a logical
+ *     or, * a logical and, - is refused as torch refuses it).
+ * Per element i of [0, numel): registers r[0..FLAME_EW_MAX_REGS) start undefined; ops run in
+ * order.  prog (n_ops <= FLAME_EW_MAX_OPS) and bufs (n_bufs <= FLAME_EW_MAX_BUFS) are HOST
+ * arrays, copied into the launch; every buffer is a contiguous DEVICE array of numel elements.
+ */
+#define FLAME_U8 6     /* element types only flame_elementwise takes */
+#define FLAME_I8 7
+#define FLAME_I16 8
+#define FLAME_BOOL 9
+#define FLAME_EW_LOAD 0    /* r[dst] = bufs[a][i], read as dtype */
+#define FLAME_EW_STORE 1   /* bufs[a][i] = r[b], written as dtype (= r[b]'s dtype) */
+#define FLAME_EW_ZERO 2    /* r[dst] = 0 (torch.zeros_like) */
+#define FLAME_EW_CAST 3    /* r[dst] = r[a] (dtype b) as dtype: int -> float RNE (via fp32 for
+                              bf16 / fp16, as c10 converts), float -> narrower float RNE (fp64 ->
+                              bf16 / fp16 via fp32), float -> int toward zero, int -> int wrapped,
+                              to bool: != 0 */
+#define FLAME_EW_ADD 4     /* r[dst] = r[a] + r[b] (both already dtype) */
+#define FLAME_EW_SUB 5     /* r[a] - r[b] */
+#define FLAME_EW_MUL 6     /* r[a] * r[b] */
+#define FLAME_EW_DIV 7     /* r[a] / r[b] (float dtype: torch's true division) */
+#define FLAME_EW_ADD_S 8   /* r[a] + scalar */
+#define FLAME_EW_MUL_S 9   /* r[a] * scalar */
+#define FLAME_EW_SQUARE 10 /* r[a] ** 2 */
+#define FLAME_EW_SIGN 11   /* torch.sign (NaN and -0 -> +0 for floats) */
+#define FLAME_EW_SQRT 12   /* torch.sqrt (float dtype) */
+#define FLAME_EW_MAX_OPS 64
+#define FLAME_EW_MAX_REGS 32
+#define FLAME_EW_MAX_BUFS 16
+typedef struct flame_ew_op {
+    int32_t op;      /* FLAME_EW_* */
+    int32_t dtype;   /* the result's element type (LOAD / STORE: the buffer's) */
+    int32_t dst;     /* register written */
+    int32_t a;       /* register read (LOAD / STORE: the buffer index) */
+    int32_t b;       /* second register read (STORE: the register stored; CAST: r[a]'s dtype) */
+    int32_t pad;
+    double scalar;   /* ADD_S / MUL_S: the Python scalar */
+} flame_ew_op;
+int flame_elementwise(const flame_ew_op *prog, int32_t n_ops, void *const *bufs, int32_t n_bufs,
+                      int64_t numel, void *stream);
+
 /*
  * flame_hier_fedbuff for small launches: the metadata block (segments, then the mid_w,
  * mid_delta, client, mid_rates, mid_goal and top_rates tables at the given byte offsets;

@@ -223,9 +223,15 @@ class OracleFedGFT(OracleFedAvg):
 class OracleFedOPT(OracleFedAvg):
     """fedopt.py:58-129 with the three _delta_v variants."""
 
-    def __init__(self, sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3):
+    def __init__(self, sort, beta_1=0.9, beta_2=0.99, eta=1e-2, tau=1e-3, sqrt_rn=False):
         super().__init__()
         self.sort = sort
+        # sqrt_rn: the reference's statements with every fp32 / fp64 op correctly rounded, as the
+        # C oracle and the kernels compute them -- an fp32 root via fp64, an all-fp64 key in numpy
+        # (IEEE ops); torch-CPU's own fp32 sqrt is not correctly rounded (~0.6 % of values one ulp
+        # off) and its fp64 step differs from IEEE on some CPUs (one element in 513 on the MI355X
+        # box's EPYC, profiles/r06z_ew_debug.log)
+        self.sqrt_rn = sqrt_rn
         self.beta_1, self.beta_2, self.eta, self.tau = beta_1, beta_2, eta, tau
         self.hyper = fedopt_scalars(beta_1, beta_2, eta, tau)
         self.current_weights = None
@@ -263,6 +269,9 @@ class OracleFedOPT(OracleFedAvg):
         _delta_v variants), which carries its dtype promotions (int64 -> fp32, bf16 rounding)."""
         consult.note()
         b1, b2, eta, tau = self.beta_1, self.beta_2, self.eta, self.tau
+        if self.sqrt_rn and avg.dtype == cur.dtype == torch.float64 and (
+                first or (self.m_t[k].dtype == self.v_t[k].dtype == torch.float64)):
+            return self._adapt_numpy64(k, avg, cur, first)
         d = avg - cur
         m = torch.zeros_like(d) if first else self.m_t[k]
         m = b1 * m + (1 - b1) * d
@@ -274,7 +283,34 @@ class OracleFedOPT(OracleFedAvg):
         else:
             v = v + d**2
         self.m_t[k], self.v_t[k] = m, v
-        return cur + eta * m / (torch.sqrt(v) + tau)
+        sq = torch.sqrt(v)
+        if self.sqrt_rn and sq.dtype == torch.float32:
+            sq = torch.sqrt(v.to(torch.float32).double()).float()
+        return cur + eta * m / (sq + tau)
+
+
+    def _adapt_numpy64(self, k, avg, cur, first):
+        """_adapt_torch's statements for an all-fp64 key in numpy: IEEE double ops, the root
+        correctly rounded, torch.sign as (0 < x) - (x < 0) (NaN and -0 give +0)."""
+        with np.errstate(all="ignore"):     # overflows / NaNs are part of the sequence (IEEE)
+            return self._numpy64_step(k, avg, cur, first)
+
+    def _numpy64_step(self, k, avg, cur, first):
+        b1, b2, eta, tau = self.beta_1, self.beta_2, self.eta, self.tau
+        a, c = avg.numpy(), cur.numpy()
+        d = a - c
+        m = np.zeros_like(d) if first else self.m_t[k].numpy()
+        m = b1 * m + (1 - b1) * d
+        v = np.zeros_like(d) if first else self.v_t[k].numpy()
+        if self.sort == "fedadam":
+            v = b2 * v + (1 - b2) * (d * d)
+        elif self.sort == "fedyogi":
+            x = v - d * d
+            v = v - (1 - b2) * (d * d) * ((0 < x).astype(np.float64) - (x < 0).astype(np.float64))   # torch.sign
+        else:
+            v = v + d * d
+        self.m_t[k], self.v_t[k] = torch.from_numpy(np.array(m)), torch.from_numpy(np.array(v))
+        return torch.from_numpy(np.array(c + eta * m / (np.sqrt(v) + tau)))
 
 
 class OracleFedBuff:

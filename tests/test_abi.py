@@ -143,3 +143,61 @@ def test_fedopt_argmeta_validates_without_gpu():
     assert L.flame_fedopt_reduce_adapt_argmeta(0, 0, 4, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_EINVAL
     assert b"unknown flags" in L.flame_last_error()
     assert L.flame_fedopt_reduce_adapt_argmeta(0, 7, 0, blk, 512, 1, 1, 2, 504, 96, *hyper, None) == _native.FLAME_ENOTSUP
+
+
+def test_elementwise_validates_programs_without_gpu():
+    """flame_elementwise checks a program on the host before any launch: registers defined
+    before they are read and of the dtype the reading op says, buffers present, known ops."""
+    from flame_amd import _native
+    from flame_amd import elementwise as E
+    L = _native.lib()
+    fake = ctypes.c_void_p(4096)    # never dereferenced: every call below fails (or is empty) on the host
+    bufs = (ctypes.c_void_p * 2)(fake, fake)
+
+    def run(ops, numel=8):
+        arr = (E.EwOp * len(ops))(*ops)
+        return L.flame_elementwise(arr, len(ops), bufs, 2, numel, None)
+    f32, i64 = _native.FLAME_F32, _native.FLAME_I64
+    assert run([E.EwOp(E.ADD, f32, 0, 1, 2, 0, 0.0)]) == _native.FLAME_EINVAL          # reads undefined registers
+    assert run([E.EwOp(E.LOAD, i64, 0, 0, 0, 0, 0.0), E.EwOp(E.SQRT, f32, 1, 0, 0, 0, 0.0)]) == _native.FLAME_EINVAL
+    assert b"dtype" in L.flame_last_error()                                             # an int64 register read as fp32
+    assert run([E.EwOp(E.LOAD, i64, 0, 0, 0, 0, 0.0), E.EwOp(E.SQRT, i64, 1, 0, 0, 0, 0.0)]) == _native.FLAME_EINVAL
+    assert b"sqrt" in L.flame_last_error()
+    assert run([E.EwOp(E.LOAD, f32, 0, 5, 0, 0, 0.0)]) == _native.FLAME_EINVAL          # no buffer 5
+    assert run([E.EwOp(E.LOAD, f32, 0, 0, 0, 0, 0.0), E.EwOp(E.STORE, i64, 0, 1, 0, 0, 0.0)]) == _native.FLAME_EINVAL
+    assert run([E.EwOp(99, f32, 0, 0, 0, 0, 0.0)]) == _native.FLAME_EINVAL
+    assert run([E.EwOp(E.LOAD, 12, 0, 0, 0, 0, 0.0)]) == _native.FLAME_EINVAL           # unknown dtype
+    ok = [E.EwOp(E.LOAD, i64, 0, 0, 0, 0, 0.0), E.EwOp(E.CAST, f32, 1, 0, i64, 0, 0.0),
+          E.EwOp(E.SQRT, f32, 2, 1, 0, 0, 0.0), E.EwOp(E.STORE, f32, 0, 1, 2, 0, 0.0)]
+    assert run(ok, numel=0) == _native.FLAME_OK                                          # valid, nothing to launch
+    assert L.flame_elementwise(None, 65, bufs, 2, 8, None) == _native.FLAME_EINVAL
+
+
+def test_elementwise_programs_follow_torch_promotion():
+    """The recorded FedOPT statements compile to programs whose every result dtype is torch's
+    own (no GPU: compile only)."""
+    import torch
+    from flame_amd import elementwise as E
+    for da, dc in [(torch.int64, torch.int64), (torch.int32, torch.float32), (torch.float64, torch.float64),
+                   (torch.bfloat16, torch.float16), (torch.uint8, torch.int64), (torch.float16, torch.float16)]:
+        for shape in [(5,), ()]:
+            a, c = torch.ones(shape, dtype=da), torch.zeros(shape, dtype=dc)
+            d = E.Lazy.of(a) - E.Lazy.of(c)
+            m = 0.9 * torch.zeros_like(d) + (1 - 0.9) * d
+            y = torch.zeros_like(d)
+            y = y - (1 - 0.99) * d ** 2 * torch.sign(y - d ** 2)
+            new = E.Lazy.of(c) + 1e-2 * m / (torch.sqrt(y) + 1e-3)
+            d2 = a - c
+            m2 = 0.9 * torch.zeros_like(d2) + (1 - 0.9) * d2
+            y2 = torch.zeros_like(d2)
+            y2 = y2 - (1 - 0.99) * d2 ** 2 * torch.sign(y2 - d2 ** 2)
+            new2 = c + 1e-2 * m2 / (torch.sqrt(y2) + 1e-3)
+            assert (m.dtype, y.dtype, new.dtype) == (m2.dtype, y2.dtype, new2.dtype), (da, dc)
+            prog, bufs = E._compile([m, y, new], [torch.empty(o.shape, dtype=o.dtype) for o in (m, y, new)])
+            assert len(prog) <= E.MAX_OPS and len(bufs) <= E.MAX_BUFS
+            assert max(op.dst for op in prog) < E.MAX_REGS
+    import pytest
+    with pytest.raises(RuntimeError):           # torch refuses bool subtraction; so does the recording
+        E.Lazy.of(torch.ones(3, dtype=torch.bool)) - E.Lazy.of(torch.ones(3, dtype=torch.bool))
+    with pytest.raises(NotImplementedError):
+        E.Lazy.of(torch.ones(3)) + E.Lazy.of(torch.ones(2, 3))

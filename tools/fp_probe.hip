@@ -276,9 +276,53 @@ __global__ void f16_mix_kernel(const float* ss, int ns, unsigned long long* out)
     }
 }
 
+// fp64 (the elementwise programs' fp64 keys): how often the compiler's a / b and sqrt(x) differ
+// from flame_fm::ddiv_rn / dsqrt_rn (the exact-residual step), on counter-drawn operands with
+// exponents in [-(span), span); the step itself is checked for the nearest-value property it rests
+// on: no neighbour of the result has a strictly smaller residual (divide) / the result's squared
+// midpoints bracket x (root) -- a violation is a FAIL, a difference from the compiler is counted.
+__global__ void f64_kernel(uint64_t seed, uint64_t n, int span, int root, unsigned long long* out,
+                           unsigned long long* diff) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+        const uint64_t r1 = mix(seed * 0x9e3779b97f4a7c15ull + 2 * i), r2 = mix(seed * 0x9e3779b97f4a7c15ull + 2 * i + 1);
+        const int64_t ea = static_cast<int64_t>(r1 >> 52) % (2 * span) - span + 1023;
+        const int64_t eb = static_cast<int64_t>(r2 >> 52) % (2 * span) - span + 1023;
+        const double a = __longlong_as_double((static_cast<long long>(ea) << 52) | (r1 & 0x000fffffffffffffull) |
+                                              (root ? 0ull : (r2 & 0x8000000000000000ull)));
+        const double b = __longlong_as_double((static_cast<long long>(eb) << 52) | (r2 & 0x000fffffffffffffull));
+        double raw, got;
+        bool ok;
+        if (root) {
+            raw = __builtin_sqrt(a);
+            got = flame_fm::dsqrt_rn(a);
+            const double sp = flame_fm::dnext(got, true), sm = flame_fm::dnext(got, false);
+            const double rr = __builtin_fma(-got, got, a);
+            ok = a < 0x1p-900 || (rr <= got * (sp - got) && rr > -got * (got - sm));
+        } else {
+            raw = a / b;
+            got = flame_fm::ddiv_rn(a, b);
+            const double gp = flame_fm::dnext(got, true), gm = flame_fm::dnext(got, false);
+            const double rg = __builtin_fabs(__builtin_fma(-got, b, a));
+            ok = !flame_fm::dmid(got) || (rg <= __builtin_fabs(__builtin_fma(-gp, b, a)) &&
+                                          rg <= __builtin_fabs(__builtin_fma(-gm, b, a)));
+        }
+        if (__double_as_longlong(raw) != __double_as_longlong(got)) atomicAdd(diff, 1ull);
+        if (!ok) report(out, static_cast<uint32_t>(i), static_cast<uint32_t>(i >> 32),
+                        static_cast<uint32_t>(__double_as_longlong(got)), static_cast<uint32_t>(__double_as_longlong(raw)));
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int probe_f64(uint64_t seed, uint64_t n, int span, int root, unsigned long long* out, unsigned long long* diff) {
+    (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));
+    (void)hipMemset(diff, 0, sizeof(unsigned long long));
+    f64_kernel<<<8192, 256>>>(seed, n, span, root, out, diff);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
 
 int probe_f16_hsqrt(uint32_t lo, uint32_t hi, unsigned long long* out) {
     (void)hipMemset(out, 0, 5 * sizeof(unsigned long long));

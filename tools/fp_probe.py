@@ -123,6 +123,15 @@ def main():
     show(f"fp16 (shipped): v_fma_mix_f32(s, half, neg(0)) == RN_f32(s * half) bit for bit on every fp16 pattern x "
          f"{scal.numel()} scalars (+-0, +-inf, subnormal, random)", L.probe_f16_mix(scal_d.data_ptr(), scal.numel(), p),
          True)
+    # fp64 (flame_elementwise): the exact-residual step of ddiv_rn / dsqrt_rn, and how often it moved
+    # the compiler's result
+    L.probe_f64.argtypes = [u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    diff = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for root, span, nm in ((0, 60, "a / b"), (0, 1000, "a / b (wide exponents)"), (1, 60, "sqrt(x)"),
+                           (1, 1022, "sqrt(x) (wide exponents)")):
+        rc = L.probe_f64(u64(7 + root), u64(1 << 28), span, root, p, ctypes.c_void_p(diff.data_ptr()))
+        show(f"fp64 {nm}: the corrected result is the nearest on {1 << 28} draws (the compiler's differed on "
+             f"{int(diff.item())})", rc, True)
     # adapt_vec admits v below 2^-96 too: it only reaches sqrt(v) + tau (tau >= 2^-20)
     L.probe_den.argtypes = [u64, u64, ctypes.c_float, ctypes.c_void_p]
     for tau in (2.0 ** -20, 1e-3, 1e-2, 0.1, 1.0, 2.0 ** 38):

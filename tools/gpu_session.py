@@ -63,6 +63,11 @@ STEPS = {
     "soak_eager16": (600, ["env", "FLAME_RANDOM_SCALE=50", "FLAME_RANDOM_SEED_OFFSET=200000", PY, "-u", "-m",
                            "pytest", "tests/test_gpu_random_cases.py", "-m", "gpu", "-k", "eager_fedopt_16bit", "-x",
                            "-q", "--timeout", "200", "--timeout-method", "thread"]),
+    # the keys the fused kernels do not take, as flame_elementwise programs, and every suite that
+    # reaches them (mixed / narrow / int / fp64 keys of FedAvg, FedOPT, FedBuff, FedDyn, SCAFFOLD)
+    "pytest_ew": (600, [PY, "-u", "-m", "pytest", "tests/test_gpu_elementwise.py", "tests/test_gpu_dtype_matrix.py",
+                        "tests/test_gpu_parity.py", "tests/test_gpu_random_cases.py", "-m", "gpu", "-x", "-q",
+                        "--timeout", "200", "--timeout-method", "thread"]),
     "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
                          "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
                          "--timeout-method", "thread"]),
