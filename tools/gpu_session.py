@@ -68,6 +68,11 @@ STEPS = {
     "pytest_ew": (600, [PY, "-u", "-m", "pytest", "tests/test_gpu_elementwise.py", "tests/test_gpu_dtype_matrix.py",
                         "tests/test_gpu_parity.py", "tests/test_gpu_random_cases.py", "-m", "gpu", "-x", "-q",
                         "--timeout", "200", "--timeout-method", "thread"]),
+    # fresh random cases through every optimizer (mixed / int / fp64 keys reach flame_elementwise)
+    "soak_random": (900, ["env", "FLAME_RANDOM_SCALE=6", "FLAME_RANDOM_SEED_OFFSET=300000", PY, "-u", "-m", "pytest",
+                          "tests/test_gpu_random_cases.py", "-m", "gpu", "-k",
+                          "random_case_vs_oracle or random_stateful or random_hierarchy", "-x", "-q", "--timeout",
+                          "300", "--timeout-method", "thread"]),
     "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
                          "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
                          "--timeout-method", "thread"]),
