@@ -38,7 +38,7 @@ FLAME_TILE_BYTES = 4096
 EXPORTS = (
     "flame_abi_version", "flame_last_error", "flame_chunk_elems", "flame_scale_add_chunk_elems",
     "flame_agg_reduce", "flame_agg_reduce_argmeta", "flame_agg_argmeta_max_bytes", "flame_fedopt_reduce_adapt", "flame_fedopt_reduce_adapt_argmeta", "flame_fedopt_chain", "flame_fedbuff_scale_add", "flame_hier_fedbuff", "flame_hier_fedbuff_argmeta",
-    "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_elementwise", "flame_synth_fill",
+    "flame_hier_resident_per_cu", "flame_feddyn_round", "flame_elementwise", "flame_elementwise_segments", "flame_synth_fill",
     "flame_host_register", "flame_host_unregister", "flame_host_device_pointer",
     "flame_slab_write", "flame_slab_write_2d",
     "flame_launch_branches", "flame_launch_branch_name", "flame_launch_branch_count",
@@ -98,6 +98,8 @@ def lib() -> ctypes.CDLL:
                                      ctypes.c_double, vp]
     L.flame_elementwise.restype = ctypes.c_int
     L.flame_elementwise.argtypes = [vp, i32, vp, i32, i64, vp]
+    L.flame_elementwise_segments.restype = ctypes.c_int
+    L.flame_elementwise_segments.argtypes = [vp, i32, vp, i32, vp, i32, i64, vp]
     L.flame_synth_fill.restype = ctypes.c_int
     L.flame_synth_fill.argtypes = [ctypes.c_int, vp, i64, u64, u64, i64, f32, vp]
     L.flame_host_register.restype = ctypes.c_int

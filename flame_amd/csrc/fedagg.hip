@@ -1938,9 +1938,11 @@ __global__ __launch_bounds__(kBlock) void slab_write_kernel(const ArgMeta meta, 
 // or an int64.  Such keys are small, so the registers may live in scratch.
 struct EwArgs {
     flame_ew_op ops[FLAME_EW_MAX_OPS];
-    void* bufs[FLAME_EW_MAX_BUFS];
+    void* bufs[FLAME_EW_MAX_BUFS];       // one segment: the buffers
+    void* const* table;                  // segments: device [n_segs][n_bufs] buffers (else NULL)
+    const int64_t* seg_end;              // segments: device [n_segs] inclusive element prefix sums
     int64_t numel;
-    int32_t n_ops;
+    int32_t n_ops, n_segs, n_bufs;
 };
 union EwVal {
     double f;
@@ -2035,14 +2037,27 @@ __global__ __launch_bounds__(kEwBlock) void ew_kernel(EwArgs args) {
     const int64_t numel = P->numel;
     const int n_ops = P->n_ops;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < numel; i += stride) {
+    void* const* table = P->table;
+    for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < numel; g += stride) {
+        // the element's segment (several keys of one program in one launch) and index in it
+        int64_t i = g;
+        void* const* bufs = P->bufs;
+        if (table) {
+            int lo = 0, hi = P->n_segs - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (P->seg_end[mid] > g) hi = mid; else lo = mid + 1;
+            }
+            i = g - (lo ? P->seg_end[lo - 1] : 0);
+            bufs = table + static_cast<int64_t>(lo) * P->n_bufs;
+        }
         EwVal r[FLAME_EW_MAX_REGS];
         for (int k = 0; k < n_ops; ++k) {
             const flame_ew_op& o = P->ops[k];
             const int dt = o.dtype;
             switch (o.op) {
-            case FLAME_EW_LOAD: r[o.dst] = ew_load(P->bufs[o.a], i, dt); break;
-            case FLAME_EW_STORE: ew_store(P->bufs[o.a], i, dt, r[o.b]); break;
+            case FLAME_EW_LOAD: r[o.dst] = ew_load(bufs[o.a], i, dt); break;
+            case FLAME_EW_STORE: ew_store(bufs[o.a], i, dt, r[o.b]); break;
             case FLAME_EW_ZERO: if (ew_float(dt)) r[o.dst].f = 0.0; else r[o.dst].i = 0; break;
             case FLAME_EW_CAST: r[o.dst] = ew_cast(r[o.a], o.b, dt); break;
             case FLAME_EW_ADD: r[o.dst] = ew_bin<FLAME_EW_ADD>(r[o.a], r[o.b], dt); break;
@@ -2110,7 +2125,8 @@ enum : int {
     BR_CHAIN = 80,          // + dt * 3 + variant (f32, bf16, f16): flame_fedopt_chain
     BR_AGG_LOB = 89,        // + dt (f32, bf16, f16): flame_agg_reduce, low residency, LDS-held output bursts
     BR_EW = 92,             // flame_elementwise
-    BR_COUNT = 93
+    BR_EW_SEG = 93,         // flame_elementwise_segments
+    BR_COUNT = 94
 };
 std::atomic<long long> g_launches[BR_COUNT];
 
@@ -2140,7 +2156,8 @@ const char* branch_name(int i) {
             else if (b < BR_CHAIN) snprintf(n, z, "flame_hier_fedbuff_argmeta/lds/%s/%s", dts[(b - BR_HIER_ARG_LDS) / 2], (b - BR_HIER_ARG_LDS) % 2 ? "sync" : "fedbuff");
             else if (b < BR_AGG_LOB) snprintf(n, z, "flame_fedopt_chain/%s/%s", dts[(b - BR_CHAIN) / 3], var[(b - BR_CHAIN) % 3]);
             else if (b < BR_EW) snprintf(n, z, "flame_agg_reduce/lo_burst/%s", dts[b - BR_AGG_LOB]);
-            else snprintf(n, z, "flame_elementwise");
+            else if (b < BR_EW_SEG) snprintf(n, z, "flame_elementwise");
+            else snprintf(n, z, "flame_elementwise_segments");
         }
         return true;
     }();
@@ -2682,12 +2699,57 @@ int flame_synth_fill(int dtype, void* out, int64_t numel, uint64_t seed, uint64_
     return check_launch("flame_synth_fill");
 }
 
+static int ew_check(const flame_ew_op* prog, int32_t n_ops, void* const* bufs, int32_t n_bufs, int64_t numel);
+
 int flame_elementwise(const flame_ew_op* prog, int32_t n_ops, void* const* bufs, int32_t n_bufs, int64_t numel,
                       void* stream) {
-    if (n_ops < 0 || n_ops > FLAME_EW_MAX_OPS || (n_ops > 0 && !prog))
-        return set_err(FLAME_EINVAL, "flame_elementwise: n_ops %d outside [0, %d] or NULL program", n_ops, FLAME_EW_MAX_OPS);
     if (n_bufs < 0 || n_bufs > FLAME_EW_MAX_BUFS || (n_bufs > 0 && !bufs))
         return set_err(FLAME_EINVAL, "flame_elementwise: n_bufs %d outside [0, %d] or NULL table", n_bufs, FLAME_EW_MAX_BUFS);
+    const int rc = ew_check(prog, n_ops, bufs, n_bufs, numel);
+    if (rc != FLAME_OK) return rc;
+    if (numel == 0 || n_ops == 0) return FLAME_OK;
+    EwArgs a{};
+    for (int32_t k = 0; k < n_ops; ++k) a.ops[k] = prog[k];
+    for (int32_t k = 0; k < n_bufs; ++k) a.bufs[k] = bufs[k];
+    a.numel = numel;
+    a.n_ops = n_ops;
+    int64_t blocks = (numel + kEwBlock - 1) / kEwBlock;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(ew_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kEwBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    return launched(BR_EW, "flame_elementwise");
+}
+
+int flame_elementwise_segments(const flame_ew_op* prog, int32_t n_ops, void* const* table, int32_t n_bufs,
+                               const int64_t* seg_end, int32_t n_segs, int64_t numel, void* stream) {
+    if (n_bufs < 0 || n_bufs > FLAME_EW_MAX_BUFS)
+        return set_err(FLAME_EINVAL, "flame_elementwise_segments: n_bufs %d outside [0, %d]", n_bufs, FLAME_EW_MAX_BUFS);
+    if (n_segs <= 0 || !table || !seg_end)
+        return set_err(FLAME_EINVAL, "flame_elementwise_segments: n_segs <= 0 or a NULL table");
+    const int rc = ew_check(prog, n_ops, nullptr, n_bufs, numel);      // the buffers live on the device
+    if (rc != FLAME_OK) return rc;
+    if (numel == 0 || n_ops == 0) return FLAME_OK;
+    EwArgs a{};
+    for (int32_t k = 0; k < n_ops; ++k) a.ops[k] = prog[k];
+    a.table = table;
+    a.seg_end = seg_end;
+    a.numel = numel;
+    a.n_ops = n_ops;
+    a.n_segs = n_segs;
+    a.n_bufs = n_bufs;
+    int64_t blocks = (numel + kEwBlock - 1) / kEwBlock;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(ew_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kEwBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    return launched(BR_EW_SEG, "flame_elementwise_segments");
+}
+
+// the host-side check of a program (both entry points): every register defined before it is read,
+// in the dtype the reading op says; every buffer it names present (bufs NULL: the segments'
+// buffers are on the device, only the index is checked); an op / dtype the kernel knows
+static int ew_check(const flame_ew_op* prog, int32_t n_ops, void* const* bufs, int32_t n_bufs, int64_t numel) {
+    if (n_ops < 0 || n_ops > FLAME_EW_MAX_OPS || (n_ops > 0 && !prog))
+        return set_err(FLAME_EINVAL, "flame_elementwise: n_ops %d outside [0, %d] or NULL program", n_ops, FLAME_EW_MAX_OPS);
     if (numel < 0) return set_err(FLAME_EINVAL, "flame_elementwise: numel < 0");
     // host-side check of the program: every register defined before it is read, in the dtype the
     // reading op says; every buffer it names present; an op / dtype the kernel knows
@@ -2701,11 +2763,11 @@ int flame_elementwise(const flame_ew_op* prog, int32_t n_ops, void* const* bufs,
         auto bad = [&](const char* why) { return set_err(FLAME_EINVAL, "flame_elementwise: op %d (%d): %s", k, o.op, why); };
         switch (o.op) {
         case FLAME_EW_LOAD:
-            if (!reg(o.dst) || o.a < 0 || o.a >= n_bufs || (numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
+            if (!reg(o.dst) || o.a < 0 || o.a >= n_bufs || (bufs && numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
             rdt[o.dst] = dt;
             break;
         case FLAME_EW_STORE:
-            if (!reg(o.b) || o.a < 0 || o.a >= n_bufs || (numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
+            if (!reg(o.b) || o.a < 0 || o.a >= n_bufs || (bufs && numel > 0 && !bufs[o.a])) return bad("bad register or buffer");
             if (rdt[o.b] != dt) return bad("stored register is not of the buffer's dtype");
             break;
         case FLAME_EW_ZERO:
@@ -2733,17 +2795,7 @@ int flame_elementwise(const flame_ew_op* prog, int32_t n_ops, void* const* bufs,
         default: return bad("unknown op");
         }
     }
-    if (numel == 0 || n_ops == 0) return FLAME_OK;
-    EwArgs a{};
-    for (int32_t k = 0; k < n_ops; ++k) a.ops[k] = prog[k];
-    for (int32_t k = 0; k < n_bufs; ++k) a.bufs[k] = bufs[k];
-    a.numel = numel;
-    a.n_ops = n_ops;
-    int64_t blocks = (numel + kEwBlock - 1) / kEwBlock;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(ew_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kEwBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), a);
-    return launched(BR_EW, "flame_elementwise");
+    return FLAME_OK;
 }
 
 static int check_tile_copies(const flame_tile_copy* t, int32_t n, const char* who) {

@@ -953,8 +953,7 @@ def accumulate(agg: dict, entries, *, device=None, key_groups=None, after_group=
             reduce_(outs, outs, clients, [entries[ci][1] for ci in cis])
             for t in targets:
                 t.writeback()
-        for k in mixed:
-            _accumulate_promoted(agg, k, [entries[ci] for ci in cis], device)
+        _accumulate_mixed(agg, mixed, [entries[ci] for ci in cis], device)
 
 
 def weight_dtype(weights, k) -> torch.dtype:
@@ -1061,6 +1060,45 @@ def _accumulate_slab(agg: dict, entries, device, key_groups=None, after_group=No
     for t in targets.values():
         t.writeback()
     return True
+
+
+def _accumulate_mixed(agg: dict, keys, entries, device) -> None:
+    """:func:`_accumulate_promoted` for many keys at once: each key's whole arrival loop
+    (``tmp = (v * rate).to(v.dtype); agg[k] += tmp`` per entry, fedavg.py:93-104 /
+    fedbuff.py:147-157) is ONE flame_elementwise program written in place into agg[k], and the
+    keys whose dtypes / 0-dim-ness agree share one program and one launch (e.g. a ResNet's 53
+    BatchNorm ``num_batches_tracked``: int64 updates into the fp32 aggregate FedOPT's promotion
+    left).  Aggregates that are not contiguous device tensors, and entries holding tiled slab
+    slots, take the per-key path."""
+    from . import elementwise as ew
+    rates = tuple(float(r) for _, r in entries)
+    groups = collections.OrderedDict()
+    for k in keys:
+        acc = agg[k]
+        vs = [w[k] for w, _ in entries]
+        for v in vs:
+            _check_cast(acc.dtype, v.dtype)
+        if (not (acc.is_cuda and acc.device == device and acc.is_contiguous())
+                or any(tuple(v.shape) != tuple(acc.shape) for v in vs) or len(vs) > ew.MAX_BUFS - 2):
+            _accumulate_promoted(agg, k, entries, device)
+            continue
+        sig = (acc.dtype, acc.dim() == 0, tuple((v.dtype, v.dim() == 0) for v in vs), rates)
+        groups.setdefault(sig, []).append(k)
+    for sig, ks in groups.items():
+        def stmt(acc, *vs):
+            for v, r in zip(vs, rates):
+                tmp = v * r
+                acc = (acc + tmp.to(v.dtype)).to(acc.dtype)       # agg[k] += tmp, in place
+            return acc
+        k0 = ks[0]
+        specs = [(agg[k0].dtype, tuple(agg[k0].shape))] + [(w[k0].dtype, tuple(w[k0].shape)) for w, _ in entries]
+        try:
+            prog = ew.cached(("accumulate",) + sig, stmt, specs)
+        except NotImplementedError:      # a statement longer than one program: per key, as before
+            for k in ks:
+                _accumulate_promoted(agg, k, entries, device)
+            continue
+        prog.run_many([[agg[k]] + [w[k] for w, _ in entries] for k in ks], device, into=[[agg[k]] for k in ks])
 
 
 def _accumulate_promoted(agg: dict, k, entries, device) -> None:

@@ -405,15 +405,33 @@ class FedOPT(FedAvg):
         ONE flame_elementwise launch per key -- torch's own dtype promotions, torch-CPU's
         arithmetic per dtype (include/flame_amd.h), no PyTorch compute."""
         out = {}
+        programs = self.__dict__.setdefault("_ew_programs", {})
+        hyper = (self.beta_1, self.beta_2, self.eta, self.tau)
+        groups = {}
         for k in keys:
-            d = ew.Lazy.of(average[k]) - ew.Lazy.of(current[k])
-            m = torch.zeros_like(d) if state_zero or k not in self.m_t else ew.Lazy.of(self.m_t[k])
-            m = self.beta_1 * m + (1 - self.beta_1) * d
-            v = torch.zeros_like(d) if state_zero or k not in self.v_t else ew.Lazy.of(self.v_t[k])
-            v = self._delta_v_tensor(v, d)
-            new = ew.Lazy.of(current[k]) + self.eta * m / (torch.sqrt(v) + self.tau)
-            self.m_t[k], self.v_t[k], out[k] = ew.materialize(m, v, new, device=average[k].device)
+            ins = [average[k], current[k]]
+            if not (state_zero or k not in self.m_t or k not in self.v_t):
+                ins += [self.m_t[k], self.v_t[k]]
+            # one compiled program per dtype / 0-dim signature, one launch per program and device:
+            # a ResNet's BatchNorm num_batches_tracked keys all share one
+            sig = (hyper, tuple((t.dtype, t.dim() == 0) for t in ins))
+            if sig not in programs:
+                programs[sig] = ew.trace(self._adapt_statement, [(t.dtype, tuple(t.shape)) for t in ins])
+            groups.setdefault((sig, average[k].device), []).append((k, ins))
+        for (sig, device), rows in groups.items():
+            res = programs[sig].run_many([ins for _, ins in rows], device)
+            for (k, _), (m, v, new) in zip(rows, res):
+                self.m_t[k], self.v_t[k], out[k] = m, v, new
         return out
+
+    def _adapt_statement(self, avg, cur, m=None, v=None):
+        """fedopt.py:106-129 on Lazy operands (m / v None: the first adaptive round's zeros)."""
+        d = avg - cur
+        m = torch.zeros_like(d) if m is None else m
+        m = self.beta_1 * m + (1 - self.beta_1) * d
+        v = torch.zeros_like(d) if v is None else v
+        v = self._delta_v_tensor(v, d)
+        return m, v, cur + self.eta * m / (torch.sqrt(v) + self.tau)
 
     @abstractmethod
     def _delta_v_tensor(self, v, d):

@@ -369,6 +369,14 @@ typedef struct flame_ew_op {
 } flame_ew_op;
 int flame_elementwise(const flame_ew_op *prog, int32_t n_ops, void *const *bufs, int32_t n_bufs,
                       int64_t numel, void *stream);
+/*
+ * The same program over several segments in one launch (e.g. a ResNet's BatchNorm
+ * num_batches_tracked keys, which share one program): table = DEVICE [n_segs][n_bufs] buffer
+ * pointers, seg_end = DEVICE [n_segs] inclusive prefix sums of the segments' element counts,
+ * numel = seg_end[n_segs - 1].  prog is a HOST array as above.
+ */
+int flame_elementwise_segments(const flame_ew_op *prog, int32_t n_ops, void *const *table, int32_t n_bufs,
+                               const int64_t *seg_end, int32_t n_segs, int64_t numel, void *stream);
 
 /*
  * flame_hier_fedbuff for small launches: the metadata block (segments, then the mid_w,

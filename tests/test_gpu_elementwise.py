@@ -21,9 +21,12 @@ DEV = "cuda:0"
 SORTS = ["fedadam", "fedyogi", "fedadagrad"]
 
 # key -> (dtype, shape, value scale): the fused kernel takes only "w"
+# (keys of one dtype / 0-dim signature share one program and ONE flame_elementwise_segments launch:
+# the two num_batches_tracked, the two int32 buffers of different lengths)
 KEYS = {"w": (torch.float32, (300,), 1.0), "num_batches_tracked": (torch.int64, (), 0),
         "cnt": (torch.int32, (7,), 0), "d64": (torch.float64, (513,), 1.0), "u8": (torch.uint8, (33,), 0),
-        "i16": (torch.int16, (9,), 0), "h": (torch.bfloat16, (64,), 1.0)}
+        "i16": (torch.int16, (9,), 0), "h": (torch.bfloat16, (64,), 1.0),
+        "bn2.num_batches_tracked": (torch.int64, (), 0), "cnt2": (torch.int32, (1031,), 0)}
 
 
 def _tensor(g, dt, shape, scale, r, i):
@@ -92,7 +95,7 @@ def test_fedopt_keys_outside_the_fused_kernel_vs_oracle(sort):
     finally:
         engine._recorders.remove(launches)
     names = [ev[0] for ev in launches]
-    assert "flame_elementwise" in names, names
+    assert "flame_elementwise" in names and "flame_elementwise_segments" in names, names
     # the promoted keys end the run in fp32 (int * python float -> fp32), AdaGrad's int v aside
     assert got["num_batches_tracked"].dtype == torch.float32 and got["d64"].dtype == torch.float64
 
