@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--keys", type=int, default=53)
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--fp64", action="store_true", help="instead: an fp64 key's step, device time (fp64_rate)")
     a = ap.parse_args()
     from flame_amd.optimizers import optimizer_provider
     dev = torch.device("cuda", 0)
@@ -93,5 +94,43 @@ def main():
           f"num_batches_tracked results equal: {same}", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--fp64" not in sys.argv:
     main()
+
+
+def fp64_rate(n=25_000_000, rounds=5):
+    """Device time of one FedAdam adaptive step of an n-element fp64 key: the elementwise program
+    (flame_elementwise, one launch) against the same statements as torch ops (round 5's path)."""
+    from flame_amd.optimizers import optimizer_provider
+    dev = torch.device("cuda", 0)
+    opt = optimizer_provider.get("fedadam")
+    g = torch.Generator(device=dev).manual_seed(3)
+    avg = torch.randn(n, dtype=torch.float64, device=dev, generator=g)
+    cur = torch.randn(n, dtype=torch.float64, device=dev, generator=g)
+    opt.m_t = {"k": torch.randn(n, dtype=torch.float64, device=dev, generator=g) * 1e-2}
+    opt.v_t = {"k": torch.rand(n, dtype=torch.float64, device=dev, generator=g) * 1e-2}
+    m0, v0 = opt.m_t["k"].clone(), opt.v_t["k"].clone()
+    res = {}
+    for name, fn in (("elementwise", lambda: opt._adapt_generic(["k"], {"k": avg}, {"k": cur}, False)),
+                     ("torch-ops", lambda: torch_ops_generic(opt, ["k"], {"k": avg}, {"k": cur}, False))):
+        ts = []
+        for r in range(rounds + 1):
+            opt.m_t, opt.v_t = {"k": m0.clone()}, {"k": v0.clone()}
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        res[name] = (sorted(ts)[len(ts) // 2], out["k"].clone())
+    same = torch.equal(res["elementwise"][1], res["torch-ops"][1])
+    gb = n * 8 * 7 / 1e9          # avg, cur, m, v read; m, v, out written
+    print(f"fp64 FedAdam step, {n} elements: elementwise {res['elementwise'][0]:.3f} ms "
+          f"({gb / res['elementwise'][0] * 1e3:.0f} GB/s of its {gb:.2f} GB), torch ops {res['torch-ops'][0]:.3f} ms; "
+          f"bitwise equal: {same}", flush=True)
+
+
+if __name__ == "__main__" and "--fp64" in sys.argv:
+    fp64_rate()
