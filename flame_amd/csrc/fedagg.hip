@@ -2031,6 +2031,9 @@ __device__ __forceinline__ EwVal ew_bin(EwVal a, EwVal b, int dt) {
     return r;
 }
 
+// (The registers live in a private array, which the dynamic indexing puts in scratch; held in LDS
+// instead, [register][lane], a 25M-element fp64 FedAdam step ran slower: 1.520 vs 1.407 ms,
+// profiles/r06zh_ew_fp64_lds.log -- the op dispatch and fp64's divide / root sequences bound it.)
 __global__ __launch_bounds__(kEwBlock) void ew_kernel(EwArgs args) {
     (void)sizeof(args);      // read in place from the kernarg segment (see agg_reduce_kernel_argmeta)
     const EwArgs* P = (const EwArgs*)__builtin_amdgcn_kernarg_segment_ptr();

@@ -74,6 +74,7 @@ STEPS = {
                           "random_case_vs_oracle or random_stateful or random_hierarchy", "-x", "-q", "--timeout",
                           "300", "--timeout-method", "thread"]),
     "ew_overhead": (200, [PY, "tools/ew_overhead.py"]),
+    "ew_fp64": (200, [PY, "tools/ew_overhead.py", "--fp64"]),
     "pytest_f16": (400, [PY, "-u", "-m", "pytest", "tests/test_gpu_f16_chain_edges.py", "tests/test_gpu_half_admission.py",
                          "tests/test_gpu_eager_fedopt_chain.py", "-m", "gpu", "-x", "-v", "--timeout", "200",
                          "--timeout-method", "thread"]),
