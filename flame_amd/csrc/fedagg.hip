@@ -2033,7 +2033,56 @@ __device__ __forceinline__ EwVal ew_bin(EwVal a, EwVal b, int dt) {
 
 // (The registers live in a private array, which the dynamic indexing puts in scratch; held in LDS
 // instead, [register][lane], a 25M-element fp64 FedAdam step ran slower: 1.520 vs 1.407 ms,
-// profiles/r06zh_ew_fp64_lds.log -- the op dispatch and fp64's divide / root sequences bound it.)
+// profiles/r06zh_ew_fp64_lds.log.)
+// One op of a program on one element (registers r, the element's buffers and index).
+__device__ __forceinline__ void ew_step(const flame_ew_op& o, EwVal* r, void* const* bufs, int64_t i) {
+    const int dt = o.dtype;
+    switch (o.op) {
+    case FLAME_EW_LOAD: r[o.dst] = ew_load(bufs[o.a], i, dt); break;
+    case FLAME_EW_STORE: ew_store(bufs[o.a], i, dt, r[o.b]); break;
+    case FLAME_EW_ZERO: if (ew_float(dt)) r[o.dst].f = 0.0; else r[o.dst].i = 0; break;
+    case FLAME_EW_CAST: r[o.dst] = ew_cast(r[o.a], o.b, dt); break;
+    case FLAME_EW_ADD: r[o.dst] = ew_bin<FLAME_EW_ADD>(r[o.a], r[o.b], dt); break;
+    case FLAME_EW_SUB: r[o.dst] = ew_bin<FLAME_EW_SUB>(r[o.a], r[o.b], dt); break;
+    case FLAME_EW_MUL: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.b], dt); break;
+    case FLAME_EW_DIV: r[o.dst] = ew_bin<FLAME_EW_DIV>(r[o.a], r[o.b], dt); break;
+    case FLAME_EW_ADD_S:
+    case FLAME_EW_MUL_S: {
+        EwVal s;
+        if (dt == FLAME_F64) s.f = o.scalar;
+        else if (ew_float(dt)) {
+            // torch-CPU: a Python scalar multiplies a float tensor in fp32 (opmath) but is
+            // rounded to a bf16 / fp16 tensor's dtype before it is added
+            const float sf = __double2float_rn(o.scalar);
+            s.f = o.op == FLAME_EW_ADD_S ? ew_rnd32(sf, dt) : sf;
+        } else {
+            s.i = __double2ll_rz(o.scalar);
+        }
+        r[o.dst] = o.op == FLAME_EW_ADD_S ? ew_bin<FLAME_EW_ADD>(r[o.a], s, dt) : ew_bin<FLAME_EW_MUL>(r[o.a], s, dt);
+        break;
+    }
+    case FLAME_EW_SQUARE: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.a], dt); break;
+    case FLAME_EW_SIGN: {
+        EwVal v = r[o.a];
+        if (ew_float(dt)) v.f = static_cast<double>((0.0 < v.f) - (v.f < 0.0));   // NaN, -0 -> +0
+        else v.i = (v.i > 0) - (v.i < 0);
+        r[o.dst] = v;
+        break;
+    }
+    case FLAME_EW_SQRT: {
+        EwVal v = r[o.a];
+        if (dt == FLAME_F64) v.f = flame_fm::dsqrt_rn(v.f);
+        else v.f = ew_rnd32(__builtin_sqrtf(static_cast<float>(v.f)), dt);   // correctly rounded
+        r[o.dst] = v;
+        break;
+    }
+    default: break;
+    }
+}
+
+// One element per lane per pass over the program: two or four (the op fetch and dispatch paid
+// once for several) ran slower, 1.616 / 1.757 vs 1.411 ms per 25M-element fp64 FedAdam step
+// (profiles/r06zi_ew_fp64_ilp.log) -- more registers in scratch; so did registers in LDS (1.520).
 __global__ __launch_bounds__(kEwBlock) void ew_kernel(EwArgs args) {
     (void)sizeof(args);      // read in place from the kernarg segment (see agg_reduce_kernel_argmeta)
     const EwArgs* P = (const EwArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -2055,52 +2104,7 @@ __global__ __launch_bounds__(kEwBlock) void ew_kernel(EwArgs args) {
             bufs = table + static_cast<int64_t>(lo) * P->n_bufs;
         }
         EwVal r[FLAME_EW_MAX_REGS];
-        for (int k = 0; k < n_ops; ++k) {
-            const flame_ew_op& o = P->ops[k];
-            const int dt = o.dtype;
-            switch (o.op) {
-            case FLAME_EW_LOAD: r[o.dst] = ew_load(bufs[o.a], i, dt); break;
-            case FLAME_EW_STORE: ew_store(bufs[o.a], i, dt, r[o.b]); break;
-            case FLAME_EW_ZERO: if (ew_float(dt)) r[o.dst].f = 0.0; else r[o.dst].i = 0; break;
-            case FLAME_EW_CAST: r[o.dst] = ew_cast(r[o.a], o.b, dt); break;
-            case FLAME_EW_ADD: r[o.dst] = ew_bin<FLAME_EW_ADD>(r[o.a], r[o.b], dt); break;
-            case FLAME_EW_SUB: r[o.dst] = ew_bin<FLAME_EW_SUB>(r[o.a], r[o.b], dt); break;
-            case FLAME_EW_MUL: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.b], dt); break;
-            case FLAME_EW_DIV: r[o.dst] = ew_bin<FLAME_EW_DIV>(r[o.a], r[o.b], dt); break;
-            case FLAME_EW_ADD_S:
-            case FLAME_EW_MUL_S: {
-                EwVal s;
-                if (dt == FLAME_F64) s.f = o.scalar;
-                else if (ew_float(dt)) {
-                    // torch-CPU: a Python scalar multiplies a float tensor in fp32 (opmath) but is
-                    // rounded to a bf16 / fp16 tensor's dtype before it is added
-                    const float sf = __double2float_rn(o.scalar);
-                    s.f = o.op == FLAME_EW_ADD_S ? ew_rnd32(sf, dt) : sf;
-                } else {
-                    s.i = __double2ll_rz(o.scalar);
-                }
-                r[o.dst] = o.op == FLAME_EW_ADD_S ? ew_bin<FLAME_EW_ADD>(r[o.a], s, dt)
-                                                  : ew_bin<FLAME_EW_MUL>(r[o.a], s, dt);
-                break;
-            }
-            case FLAME_EW_SQUARE: r[o.dst] = ew_bin<FLAME_EW_MUL>(r[o.a], r[o.a], dt); break;
-            case FLAME_EW_SIGN: {
-                EwVal v = r[o.a];
-                if (ew_float(dt)) v.f = static_cast<double>((0.0 < v.f) - (v.f < 0.0));   // NaN, -0 -> +0
-                else v.i = (v.i > 0) - (v.i < 0);
-                r[o.dst] = v;
-                break;
-            }
-            case FLAME_EW_SQRT: {
-                EwVal v = r[o.a];
-                if (dt == FLAME_F64) v.f = flame_fm::dsqrt_rn(v.f);
-                else v.f = ew_rnd32(__builtin_sqrtf(static_cast<float>(v.f)), dt);   // correctly rounded
-                r[o.dst] = v;
-                break;
-            }
-            default: break;
-            }
-        }
+        for (int k = 0; k < n_ops; ++k) ew_step(P->ops[k], r, bufs, i);
     }
 }
 
