@@ -314,6 +314,10 @@ class Program:
         self.ops = (EwOp * len(prog))(*prog)
         self.n_ops, self.n_in, self.out_dtypes = len(prog), n_in, list(out_dtypes)
 
+    def __reduce__(self):       # picklable (an optimizer that holds programs can be checkpointed)
+        return (_program, ([(o.op, o.dtype, o.dst, o.a, o.b, o.pad, o.scalar) for o in self.ops], self.n_in,
+                           self.out_dtypes))
+
     def __call__(self, *inputs, device):
         from . import engine
         if len(inputs) != self.n_in:
@@ -382,6 +386,10 @@ class Program:
                                                        len(rows), total, engine._stream_ptr(device)))
         engine._keepalive([t for row in ins + outs for t in row] + [dm], device)
         return outs
+
+
+def _program(ops, n_in, out_dtypes):
+    return Program([EwOp(*o) for o in ops], n_in, out_dtypes)
 
 
 def trace(fn, specs):

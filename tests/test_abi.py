@@ -201,3 +201,17 @@ def test_elementwise_programs_follow_torch_promotion():
         E.Lazy.of(torch.ones(3, dtype=torch.bool)) - E.Lazy.of(torch.ones(3, dtype=torch.bool))
     with pytest.raises(NotImplementedError):
         E.Lazy.of(torch.ones(3)) + E.Lazy.of(torch.ones(2, 3))
+
+
+def test_traced_programs_pickle():
+    """An optimizer holding compiled elementwise programs stays picklable (checkpoints)."""
+    import pickle
+    import torch
+    from flame_amd import elementwise as E
+    from flame_amd.optimizers import optimizer_provider
+    opt = optimizer_provider.get("fedyogi")
+    p = E.trace(opt._adapt_statement, [(torch.int64, ()), (torch.int64, ())])
+    q = pickle.loads(pickle.dumps(p))
+    assert (q.n_ops, q.n_in, q.out_dtypes) == (p.n_ops, p.n_in, p.out_dtypes)
+    assert [(o.op, o.dtype, o.dst, o.a, o.b, o.scalar) for o in q.ops] == \
+        [(o.op, o.dtype, o.dst, o.a, o.b, o.scalar) for o in p.ops]
