@@ -22,7 +22,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = sys.executable or "python3"
 AB = "build/ab/variants/lib_r05_step.so"     # the round-5 step (tools/kernel_sweep.py --build --variants r05_step)
-PARAMS = {"clients": "64", "params": "2000000", "steps": "10", "warmup": "3", "offsets": "0,4,356"}
+PARAMS = {"clients": "64", "params": "2000000", "steps": "10", "warmup": "3", "offsets": "0,4,356",
+          "seed_offset": "300000"}
 
 # name -> (seconds, command).  Commands are lists; "rocprof:" prefixes run under rocprofv3 stats.
 STEPS = {
@@ -69,7 +70,7 @@ STEPS = {
                         "tests/test_gpu_parity.py", "tests/test_gpu_random_cases.py", "-m", "gpu", "-x", "-q",
                         "--timeout", "200", "--timeout-method", "thread"]),
     # fresh random cases through every optimizer (mixed / int / fp64 keys reach flame_elementwise)
-    "soak_random": (900, ["env", "FLAME_RANDOM_SCALE=6", "FLAME_RANDOM_SEED_OFFSET=300000", PY, "-u", "-m", "pytest",
+    "soak_random": (900, ["env", "FLAME_RANDOM_SCALE=6", "FLAME_RANDOM_SEED_OFFSET={seed_offset}", PY, "-u", "-m", "pytest",
                           "tests/test_gpu_random_cases.py", "-m", "gpu", "-k",
                           "random_case_vs_oracle or random_stateful or random_hierarchy", "-x", "-q", "--timeout",
                           "300", "--timeout-method", "thread"]),
